@@ -1,0 +1,483 @@
+// Flash attention (forward + backward), bf16 in/out, fp32 accumulate, gfx950 MFMA 32x32x16.
+//
+// Forward (per workgroup: 4 waves x 32 query rows, K/V tiles of 64 keys double-buffered in LDS):
+//   S^T = K . Q^T with swapped operands so each lane owns ONE query row (lane&31) and 32 of the
+//   tile's 64 keys -> online softmax is lane-local plus one xor-32 exchange (T12 idea);
+//   the fp32 S^T accumulator is converted to bf16 and used directly as the B operand of
+//   O^T += V^T . P^T (cdna_hip_programming.md §3 'An accumulator tile as the next MFMA's operand');
+//   V^T fragments come from ds_read_b64_tr_b16 on the row-major V tile (T10).
+//   LDS images use an XOR swizzle found by exhaustive search to be conflict-free for both the
+//   ds_read_b128 K reads and the transposed V reads (128-B rows), or T10 image (b) for 256-B rows.
+// Backward (per workgroup: 4 waves x 32 keys; loop over 64-query tiles):
+//   S, dP are computed with the KEY on the lane so P and dS feed dV^T and dK^T as B operands with
+//   no data movement; dS^T goes through LDS once for dQ = dS . K, whose per-key-block partials are
+//   written with plain fp32 stores (no atomics, deterministic) and summed by a finishing kernel.
+// Strided Q/K/V/O views are supported so that the fused QKV projection output [B,S,3,H,D] and the
+// [B,S,H,D] output feed/leave the kernel without permute copies.
+//
+// Reference counterpart: src/ops/attention.cu (cuDNN multi-head attention, fwd+bwd); the
+// reference HIP build disables it entirely (src/ops/attention.cpp:33-43 '#if 0').
+#include "common.h"
+#include "ops.h"
+#include "attention.h"
+
+namespace ffk {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <int D>
+__device__ __forceinline__ int aswz(int row) {
+  if (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 3) & 1) | (((row >> 4) & 1) << 1);
+  else return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+// byte offset of element (row, col) of a [rows][D] bf16 tile image
+template <int D>
+__device__ __forceinline__ int aoff(int row, int col) {
+  const int ch = col >> 3;
+  return row * (D * 2) + ((ch ^ aswz<D>(row)) << 4) + ((col & 7) << 1);
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x4 tr_read(const char* lds, int off) {
+  v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds + off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// Stage a [ROWS][D] bf16 tile (rows r0.., clamp at rlim) from global (row stride ss) into regs.
+template <int D, int ROWS, int NTH>
+struct TileStage {
+  static constexpr int CH = ROWS * D / 8 / NTH;  // 16-B chunks per thread
+  uint4 r[CH];
+  __device__ __forceinline__ void load(const bf16_t* g, int64_t ss, int r0, int rlim, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int id = tid + i * NTH;
+      const int row = id / (D / 8), c = id % (D / 8);
+      if (r0 + row < rlim) r[i] = *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * ss + c * 8);
+      else r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int id = tid + i * NTH;
+      const int row = id / (D / 8), c = id % (D / 8);
+      *reinterpret_cast<uint4*>(lds + aoff<D>(row, c * 8)) = r[i];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)a[base + j];
+  return o;
+}
+
+// ------------------------------------------------------------------------------------ forward
+template <int D>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+  constexpr int KV = 64;
+  constexpr int TB = KV * D * 2;  // bytes of one K or V tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int qblk0 = blockIdx.x * 128;
+  const int q0 = qblk0 + wave * 32;
+  const int qrow = q0 + (lane & 31);
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qrow < a.Sq) qf[s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
+    else qf[s] = bf16x8{};
+  }
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+  const float sl2 = a.scale * LOG2E;
+
+  int nkv = (a.Sk + KV - 1) / KV;
+  if (a.causal) nkv = min(nkv, (min(qblk0 + 128, a.Sq) + KV - 1) / KV);
+
+  TileStage<D, KV, 256> sk, sv;
+  if (nkv > 0) {
+    sk.load(K, a.k_ss, 0, a.Sk, tid);
+    sv.load(V, a.v_ss, 0, a.Sk, tid);
+    sk.store(smem, tid);
+    sv.store(smem + TB, tid);
+    __syncthreads();
+  }
+  for (int t = 0; t < nkv; ++t) {
+    const char* kl = smem + (t & 1) * 2 * TB;
+    const char* vl = kl + TB;
+    char* nk = smem + ((t + 1) & 1) * 2 * TB;
+    const bool more = t + 1 < nkv;
+    if (more) {
+      sk.load(K, a.k_ss, (t + 1) * KV, a.Sk, tid);
+      sv.load(V, a.v_ss, (t + 1) * KV, a.Sk, tid);
+    }
+    // S^T[key][q] for keys 32kt..32kt+31 of this tile
+    f32x16 sacc[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int row = 32 * kt + (lane & 31);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + aoff<D>(row, 16 * s + 8 * h));
+        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
+      }
+    }
+    // scale, mask, online softmax (lane-local + xor-32 partner)
+    float mx = -INFINITY;
+    const int kbase = t * KV;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = sacc[kt][r] * sl2;
+        if (key >= a.Sk || (a.causal && key > qrow)) v = -INFINITY;
+        sacc[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float msafe = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = exp2f(m - msafe);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(sacc[kt][r] - msafe);
+        sacc[kt][r] = p;
+        rs += p;
+      }
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    lsum = lsum * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) { pf[kt][0] = pack8(sacc[kt], 0); pf[kt][1] = pack8(sacc[kt], 8); }
+    const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r0 = 32 * kt + 16 * s2 + 4 * h + qi;
+          const bf16x4 lo = tr_read(vl, aoff<D>(r0, col));
+          const bf16x4 hi = tr_read(vl, aoff<D>(r0 + 8, col));
+          bf16x8 vf;
+          vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+          vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s2], oacc[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      sk.store(nk, tid);
+      sv.store(nk + TB, tid);
+    }
+    __syncthreads();
+  }
+  // epilogue
+  if (qrow < a.Sq) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16_t* O = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * h;
+        ushort4 o;
+        o.x = f2bf(oacc[dt][4 * g + 0] * inv);
+        o.y = f2bf(oacc[dt][4 * g + 1] * inv);
+        o.z = f2bf(oacc[dt][4 * g + 2] * inv);
+        o.w = f2bf(oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<ushort4*>(O + d) = o;
+      }
+    }
+    if (h == 0 && a.lse) a.lse[(int64_t)bh * a.Sq + qrow] = lsum > 0.f ? (m * LN2 + __logf(lsum)) : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------ backward
+// delta[bh][q] = sum_d dO[q][d] * O[q][d]
+template <int D>
+__global__ void attn_bwd_pre_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t total = (int64_t)a.B * a.H * a.Sq;
+  if (gw >= total) return;
+  const int bh = gw / a.Sq, q = gw % a.Sq, b = bh / a.H, hh = bh % a.H;
+  const bf16_t* O = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh + (int64_t)q * a.o_ss;
+  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh + (int64_t)q * a.do_ss;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += bf2f(O[d]) * bf2f(dO[d]);
+  s = wave_sum(s);
+  if (lane == 0) a.delta[gw] = s;
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
+  constexpr int QT = 64;     // queries per loop step
+  constexpr int KB = 128;    // keys per workgroup (4 waves x 32)
+  constexpr int QB = QT * D * 2;
+  // LDS: Q tile, dO tile, K block image, dS^T image [KB][QT], lse/delta
+  __shared__ __attribute__((aligned(16))) char smem[2 * QB + KB * D * 2 + KB * QT * 2 + 2 * QT * 4];
+  char* q_l = smem;
+  char* do_l = smem + QB;
+  char* k_l = smem + 2 * QB;
+  char* ds_l = k_l + KB * D * 2;
+  float* lse_l = reinterpret_cast<float*>(ds_l + KB * QT * 2);
+  float* dl_l = lse_l + QT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int kb0 = blockIdx.x * KB;
+  const int key = kb0 + wave * 32 + (lane & 31);
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh;
+  const float* LSE = a.lse + (int64_t)bh * a.Sq;
+  const float* DL = a.delta + (int64_t)bh * a.Sq;
+  const float sl2 = a.scale * LOG2E;
+
+  // K block -> LDS (needed for dQ), K^T / V^T fragments -> registers (B operands, key on lane)
+  {
+    TileStage<D, KB, 256> st;
+    st.load(K, a.k_ss, kb0, a.Sk, tid);
+    st.store(k_l, tid);
+  }
+  bf16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (key < a.Sk) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * a.k_ss + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const bf16x8*>(V + (int64_t)key * a.v_ss + 16 * s + 8 * h);
+    } else {
+      kf[s] = bf16x8{};
+      vf[s] = bf16x8{};
+    }
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
+
+  int qt_begin = 0;
+  if (a.causal) qt_begin = (kb0 / QT);
+  const int nqt = (a.Sq + QT - 1) / QT;
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  float* dq_part = a.dq_acc + (int64_t)blockIdx.x * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
+
+  for (int t = qt_begin; t < nqt; ++t) {
+    const int qbase = t * QT;
+    __syncthreads();  // previous iteration done with q_l/do_l/ds_l
+    {
+      TileStage<D, QT, 256> sq, sd;
+      sq.load(Q, a.q_ss, qbase, a.Sq, tid);
+      sd.load(dO, a.do_ss, qbase, a.Sq, tid);
+      sq.store(q_l, tid);
+      sd.store(do_l, tid);
+      if (tid < QT) {
+        const int q = qbase + tid;
+        lse_l[tid] = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
+        dl_l[tid] = q < a.Sq ? DL[q] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      // S[q][key] and dP[q][key] for 32 queries x this wave's 32 keys
+      f32x16 sacc = f32x16{}, pacc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const int row = 32 * qt + (lane & 31);
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
+      }
+      // P = exp2(S*sl2 - lse2), dS = P * (dP - delta)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int q = qbase + ql;
+        float p = exp2f(sacc[r] * sl2 - lse_l[ql]);
+        if (key >= a.Sk || (a.causal && key > q)) p = 0.f;
+        sacc[r] = p;
+        pacc[r] = p * (pacc[r] - dl_l[ql]);
+      }
+      const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
+      const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
+      // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
+          bf16x8 ao, aq;
+          {
+            const bf16x4 lo = tr_read(do_l, aoff<D>(r0, col));
+            const bf16x4 hi = tr_read(do_l, aoff<D>(r0 + 8, col));
+            ao[0] = lo[0]; ao[1] = lo[1]; ao[2] = lo[2]; ao[3] = lo[3];
+            ao[4] = hi[0]; ao[5] = hi[1]; ao[6] = hi[2]; ao[7] = hi[3];
+          }
+          {
+            const bf16x4 lo = tr_read(q_l, aoff<D>(r0, col));
+            const bf16x4 hi = tr_read(q_l, aoff<D>(r0 + 8, col));
+            aq[0] = lo[0]; aq[1] = lo[1]; aq[2] = lo[2]; aq[3] = lo[3];
+            aq[4] = hi[0]; aq[5] = hi[1]; aq[6] = hi[2]; aq[7] = hi[3];
+          }
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, s2 ? pb1 : pb0, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, s2 ? sb1 : sb0, dk[dt], 0, 0, 0);
+        }
+      }
+      // dS^T image [key][q] (key = wave*32 + lane&31), 4 consecutive q per 8-B write
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ql = 32 * qt + 8 * g + 4 * h;
+        const int krow = wave * 32 + (lane & 31);
+        ushort4 o;
+        o.x = f2bf(pacc[4 * g + 0]); o.y = f2bf(pacc[4 * g + 1]);
+        o.z = f2bf(pacc[4 * g + 2]); o.w = f2bf(pacc[4 * g + 3]);
+        *reinterpret_cast<ushort4*>(ds_l + krow * (QT * 2) + ql * 2) = o;
+      }
+    }
+    __syncthreads();
+    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's 128 keys; wave -> (qt, dt) tiles
+    for (int tile = wave; tile < 2 * (D / 32); tile += 4) {
+      const int qt = tile / (D / 32), dt = tile % (D / 32);
+      f32x16 acc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KB / 16; ++ks) {
+        // A = dS[q][key]: lane q = 32qt + lane&31, keys 16ks + 8h + j -> column reads of dS^T image
+        bf16x8 af;
+        {
+          // tr read of dS^T [key][q]: 16-lane group G covers q cols 32qt + 16(G&1) + i, key rows
+          const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
+          const int kr = 16 * ks + 8 * h + qi;
+          const bf16x4 lo = tr_read(ds_l, kr * (QT * 2) + cq * 2);
+          const bf16x4 hi = tr_read(ds_l, (kr + 4) * (QT * 2) + cq * 2);
+          af[0] = lo[0]; af[1] = lo[1]; af[2] = lo[2]; af[3] = lo[3];
+          af[4] = hi[0]; af[5] = hi[1]; af[6] = hi[2]; af[7] = hi[3];
+        }
+        // B = K[key][d]: lane d = 32dt + lane&31, keys 16ks + 8h + j -> transposed reads of K image
+        bf16x8 bk;
+        {
+          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
+          const int kr = 16 * ks + 8 * h + qi;
+          const bf16x4 lo = tr_read(k_l, aoff<D>(kr, cd));
+          const bf16x4 hi = tr_read(k_l, aoff<D>(kr + 4, cd));
+          bk[0] = lo[0]; bk[1] = lo[1]; bk[2] = lo[2]; bk[3] = lo[3];
+          bk[4] = hi[0]; bk[5] = hi[1]; bk[6] = hi[2]; bk[7] = hi[3];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
+      }
+      // acc: col = d (lane&31), row = q
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int d = 32 * dt + (lane & 31);
+        if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
+      }
+    }
+  }
+  // causal: query tiles before qt_begin contribute nothing; zero their partial rows
+  if (a.causal) {
+    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += 256) dq_part[i] = 0.f;
+  }
+  // write dK, dV: lane holds key (lane&31), d = 32dt + (r&3) + 8(r>>2) + 4h
+  if (key < a.Sk) {
+    bf16_t* dK = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh + (int64_t)key * a.dk_ss;
+    bf16_t* dV = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh + (int64_t)key * a.dv_ss;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * h;
+        ushort4 o;
+        o.x = f2bf(dk[dt][4 * g + 0] * a.scale); o.y = f2bf(dk[dt][4 * g + 1] * a.scale);
+        o.z = f2bf(dk[dt][4 * g + 2] * a.scale); o.w = f2bf(dk[dt][4 * g + 3] * a.scale);
+        *reinterpret_cast<ushort4*>(dK + d) = o;
+        o.x = f2bf(dv[dt][4 * g + 0]); o.y = f2bf(dv[dt][4 * g + 1]);
+        o.z = f2bf(dv[dt][4 * g + 2]); o.w = f2bf(dv[dt][4 * g + 3]);
+        *reinterpret_cast<ushort4*>(dV + d) = o;
+      }
+    }
+  }
+}
+
+// dq[q][d] = scale * sum_kb dq_part[kb][bh][q][d]
+template <int D>
+__global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
+  const int64_t per = (int64_t)a.B * a.H * a.Sq * D;
+  const int64_t nv = per / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(a.dq_acc)[i];
+    for (int kb = 1; kb < nkb; ++kb) {
+      const float4 t = reinterpret_cast<const float4*>(a.dq_acc + kb * per)[i];
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    const int64_t e = i * 4;
+    const int d = e % D;
+    const int64_t q = (e / D) % a.Sq;
+    const int64_t bh = e / ((int64_t)D * a.Sq);
+    const int b = bh / a.H, hh = bh % a.H;
+    bf16_t* dst = a.dq + (int64_t)b * a.dq_sb + (int64_t)hh * a.dq_sh + q * a.dq_ss + d;
+    ushort4 o;
+    o.x = f2bf(s.x * a.scale); o.y = f2bf(s.y * a.scale); o.z = f2bf(s.z * a.scale); o.w = f2bf(s.w * a.scale);
+    *reinterpret_cast<ushort4*>(dst) = o;
+  }
+}
+
+int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
+  const int nkb = (Sk + 127) / 128;
+  return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
+}
+
+void attn_fwd(AttnArgs a, hipStream_t st) {
+  dim3 grid((a.Sq + 127) / 128, a.B * a.H);
+  if (a.D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  else if (a.D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, st, a);
+}
+
+void attn_bwd(AttnArgs a, hipStream_t st) {
+  const int nkb = (a.Sk + 127) / 128;
+  const int64_t rows = (int64_t)a.B * a.H * a.Sq;
+  dim3 gpre((unsigned)((rows + 3) / 4));
+  dim3 grid(nkb, a.B * a.H);
+  const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
+  dim3 gfin(ew_grid(per / 4, 256));
+  if (a.D == 64) {
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
+  } else if (a.D == 128) {
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, gpre, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
+  }
+}
+
+}  // namespace ffk

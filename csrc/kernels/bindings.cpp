@@ -1,0 +1,277 @@
+// PyTorch <-> HIP kernel glue for flexflow_amd._C. Only this translation unit includes torch
+// headers; the kernels themselves are torch-free .hip files. Every entry point launches on the
+// caller's current HIP stream (so the executor can route ops to its compute / comm streams and
+// capture whole steps into hipGraphs) and checks shapes before launching.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "attention.h"
+#include "gemm.h"
+#include "ops.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtcode(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return ffk::DT_BF16;
+  if (t.scalar_type() == at::kFloat) return ffk::DT_F32;
+  TORCH_CHECK(false, "flexflow_amd kernels support bf16/fp32 only, got ", t.scalar_type());
+  return -1;
+}
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+}
+template <typename T = void>
+T* ptr(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> Z, int64_t M, int64_t N,
+          int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t batch,
+          bool a_k, bool b_k, double alpha, double beta, int64_t act, int64_t splitk, optional<Tensor> ws) {
+  check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A/B must be bf16");
+  TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm: C must be bf16/fp32");
+  // bounds: the furthest element touched must lie inside each storage
+  auto last = [](int64_t rows, int64_t cols, int64_t ld, int64_t stride, int64_t nb) {
+    return (nb - 1) * stride + (rows - 1) * ld + cols;
+  };
+  TORCH_CHECK(last(a_k ? M : K, a_k ? K : M, lda, sA, batch) <= A.numel(), "gemm: A too small");
+  TORCH_CHECK(last(b_k ? N : K, b_k ? K : N, ldb, sB, batch) <= B.numel(), "gemm: B too small");
+  TORCH_CHECK(last(M, N, ldc, sC, batch) <= C.numel(), "gemm: C too small");
+  ffk::GemmArgs p;
+  p.A = reinterpret_cast<const uint16_t*>(A.data_ptr());
+  p.B = reinterpret_cast<const uint16_t*>(B.data_ptr());
+  p.C = C.data_ptr();
+  p.Z = ptr(Z);
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N, "gemm: bias too small");
+    p.bias = bias->data_ptr();
+    p.bias_bf16 = bias->scalar_type() == at::kBFloat16;
+  }
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.sA = sA; p.sB = sB; p.sC = sC; p.batch = batch;
+  p.alpha = alpha; p.beta = beta; p.act = act;
+  p.a_kcontig = a_k; p.b_kcontig = b_k;
+  p.out_f32 = C.scalar_type() == at::kFloat;
+  p.splitk = 1;
+  if (splitk > 1 && ws.has_value() && ws->defined()) {
+    TORCH_CHECK(ws->numel() * ws->element_size() >= ffk::gemm_workspace_bytes(M, N, K, batch, splitk),
+                "gemm: split-K workspace too small");
+    p.splitk = splitk;
+    p.ws = reinterpret_cast<float*>(ws->data_ptr());
+  }
+  ffk::gemm_bf16(p, cur_stream());
+}
+
+int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  return ffk::gemm_pick_splitk(M, N, K, batch);
+}
+
+void unary_fwd(Tensor x, Tensor y, int64_t op, double s) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous());
+  ffk::unary_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), x.numel(), op, s, cur_stream());
+}
+void unary_bwd(Tensor x, Tensor y, Tensor dy, Tensor dx, int64_t op, double s, bool acc) {
+  TORCH_CHECK(x.numel() == dx.numel() && dy.numel() == dx.numel() && y.numel() == dx.numel());
+  ffk::unary_bwd(dtcode(x), x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), op, s, acc,
+                 cur_stream());
+}
+void binary_fwd(Tensor a, Tensor b, Tensor c, int64_t op, std::vector<int64_t> shape, std::vector<int64_t> sa,
+                std::vector<int64_t> sb, bool same) {
+  TORCH_CHECK(shape.size() <= 6 && sa.size() == shape.size() && sb.size() == shape.size());
+  ffk::binary_fwd(dtcode(c), a.data_ptr(), b.data_ptr(), c.data_ptr(), c.numel(), op, shape.size(), shape.data(),
+                  sa.data(), sb.data(), same, cur_stream());
+}
+void binary_bwd(Tensor a, Tensor b, Tensor dc, optional<Tensor> da, optional<Tensor> db, int64_t op,
+                std::vector<int64_t> shape, std::vector<int64_t> sa, std::vector<int64_t> sb, bool same) {
+  TORCH_CHECK(shape.size() <= 6);
+  ffk::binary_bwd(dtcode(dc), a.data_ptr(), b.data_ptr(), dc.data_ptr(), ptr(da), ptr(db), dc.numel(), op,
+                  shape.size(), shape.data(), sa.data(), sb.data(), same, cur_stream());
+}
+void cast(Tensor x, Tensor y) {
+  TORCH_CHECK(x.numel() == y.numel());
+  ffk::cast(dtcode(x), dtcode(y), x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+}
+void dropout_fwd(Tensor x, Tensor y, Tensor mask, double rate, int64_t seed, int64_t offset) {
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() == x.numel());
+  ffk::dropout_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), rate, seed, offset,
+                   cur_stream());
+}
+void dropout_bwd(Tensor dy, Tensor mask, Tensor dx, double rate, bool acc) {
+  ffk::dropout_bwd(dtcode(dy), dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), rate, acc,
+                   cur_stream());
+}
+void bias_act_bwd(Tensor dy, optional<Tensor> z, optional<Tensor> dz, optional<Tensor> dbias, int64_t rows,
+                  int64_t cols, int64_t act) {
+  TORCH_CHECK(dy.numel() == rows * cols);
+  if (dbias.has_value() && dbias->defined()) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->numel() >= cols);
+  ffk::bias_act_bwd(dtcode(dy), dy.data_ptr(), ptr(z), ptr(dz), ptr<float>(dbias), rows, cols, act, cur_stream());
+}
+void layernorm_fwd(Tensor x, optional<Tensor> res, optional<Tensor> sum_out, optional<Tensor> gamma,
+                   optional<Tensor> beta, Tensor y, Tensor mean, Tensor rstd, int64_t rows, int64_t cols,
+                   double eps) {
+  TORCH_CHECK(x.numel() == rows * cols && y.numel() == rows * cols && mean.numel() >= rows && rstd.numel() >= rows);
+  ffk::layernorm_fwd(dtcode(x), x.data_ptr(), ptr(res), ptr(sum_out), ptr(gamma), ptr(beta), y.data_ptr(),
+                     mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, cols, eps, cur_stream());
+}
+void layernorm_bwd(Tensor dy, Tensor x, optional<Tensor> gamma, Tensor mean, Tensor rstd, Tensor dx,
+                   optional<Tensor> dres, optional<Tensor> dgamma, optional<Tensor> dbeta, int64_t rows,
+                   int64_t cols, bool acc) {
+  TORCH_CHECK(dy.numel() == rows * cols && dx.numel() == rows * cols);
+  ffk::layernorm_bwd(dtcode(dy), dy.data_ptr(), x.data_ptr(), ptr(gamma), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), dx.data_ptr(), ptr(dres), ptr<float>(dgamma), ptr<float>(dbeta), rows,
+                     cols, acc, cur_stream());
+}
+void softmax_fwd(Tensor x, Tensor y, int64_t rows, int64_t cols, double scale) {
+  TORCH_CHECK(x.numel() == rows * cols);
+  ffk::softmax_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), rows, cols, scale, cur_stream());
+}
+void softmax_bwd(Tensor y, Tensor dy, Tensor dx, int64_t rows, int64_t cols, double scale, bool acc) {
+  ffk::softmax_bwd(dtcode(y), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), rows, cols, scale, acc, cur_stream());
+}
+void softmax_xent(Tensor logits, Tensor labels, optional<Tensor> loss, optional<Tensor> dlogits, int64_t rows,
+                  int64_t cols, double gscale) {
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= rows);
+  ffk::softmax_xent_fwd_bwd(dtcode(logits), logits.data_ptr(), labels.data_ptr<int>(), ptr<float>(loss),
+                            ptr(dlogits), rows, cols, gscale, cur_stream());
+}
+void xent_grad(Tensor probs, optional<Tensor> labels, optional<Tensor> onehot, Tensor dprobs, optional<Tensor> loss,
+               int64_t rows, int64_t cols, double gscale, bool sparse) {
+  ffk::xent_grad(dtcode(probs), probs.data_ptr(), ptr<int>(labels), ptr(onehot), dprobs.data_ptr(),
+                 ptr<float>(loss), rows, cols, gscale, sparse, cur_stream());
+}
+void mse_grad(Tensor pred, Tensor label, Tensor dpred, optional<Tensor> loss, double gscale) {
+  TORCH_CHECK(pred.numel() == label.numel());
+  ffk::mse_grad(dtcode(pred), pred.data_ptr(), label.data_ptr(), dpred.data_ptr(), ptr<float>(loss), pred.numel(),
+                gscale, cur_stream());
+}
+void metrics_classify(Tensor probs, Tensor labels, int64_t rows, int64_t cols, Tensor out) {
+  ffk::metrics_classify(dtcode(probs), probs.data_ptr(), labels.data_ptr<int>(), rows, cols, out.data_ptr<float>(),
+                        cur_stream());
+}
+void reduce_rows(Tensor x, Tensor y, int64_t outer, int64_t red, int64_t inner, bool mean) {
+  ffk::reduce_rows(dtcode(x), x.data_ptr(), y.data_ptr(), outer, red, inner, mean, cur_stream());
+}
+void sgd_update(Tensor master, Tensor grad, optional<Tensor> mom, optional<Tensor> lowp, double lr,
+                double momentum, bool nesterov, double wd, double gscale) {
+  TORCH_CHECK(master.scalar_type() == at::kFloat && grad.scalar_type() == at::kFloat);
+  TORCH_CHECK(master.numel() == grad.numel());
+  if (momentum > 0) TORCH_CHECK(mom.has_value() && mom->numel() == master.numel());
+  if (lowp.has_value() && lowp->defined())
+    TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel());
+  ffk::sgd_update(master.data_ptr<float>(), grad.data_ptr<float>(), ptr<float>(mom), ptr(lowp), master.numel(), lr,
+                  momentum, nesterov, wd, gscale, cur_stream());
+}
+void adam_update(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> lowp, double alpha_t, double b1,
+                 double b2, double wd, double eps, double gscale) {
+  TORCH_CHECK(master.numel() == grad.numel() && m.numel() == master.numel() && v.numel() == master.numel());
+  if (lowp.has_value() && lowp->defined())
+    TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel());
+  ffk::adam_update(master.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                   ptr(lowp), master.numel(), alpha_t, b1, b2, wd, eps, gscale, cur_stream());
+}
+void embedding_fwd(Tensor idx, Tensor table, Tensor out, int64_t n_rows, int64_t bag, int64_t dim, bool avg) {
+  TORCH_CHECK(idx.numel() == n_rows * bag && out.numel() == n_rows * dim && table.size(-1) == dim);
+  const bool i64 = idx.scalar_type() == at::kLong;
+  ffk::embedding_fwd(dtcode(table), i64, idx.data_ptr(), table.data_ptr(), out.data_ptr(), n_rows, bag, dim,
+                     table.numel() / dim, avg, cur_stream());
+}
+void embedding_bwd(Tensor idx, Tensor dout, Tensor dtable, int64_t n_rows, int64_t bag, int64_t dim, bool avg) {
+  TORCH_CHECK(dtable.scalar_type() == at::kFloat && dout.numel() == n_rows * dim);
+  const bool i64 = idx.scalar_type() == at::kLong;
+  ffk::embedding_bwd(dtcode(dout), i64, idx.data_ptr(), dout.data_ptr(), dtable.data_ptr<float>(), n_rows, bag, dim,
+                     dtable.numel() / dim, avg, cur_stream());
+}
+void init_uniform(Tensor out, double lo, double hi, int64_t seed, int64_t offset) {
+  ffk::init_uniform(dtcode(out), out.data_ptr(), out.numel(), lo, hi, seed, offset, cur_stream());
+}
+void init_normal(Tensor out, double mean, double stdv, int64_t seed, int64_t offset) {
+  ffk::init_normal(dtcode(out), out.data_ptr(), out.numel(), mean, stdv, seed, offset, cur_stream());
+}
+void fill(Tensor out, double v) { ffk::fill(dtcode(out), out.data_ptr(), out.numel(), v, cur_stream()); }
+
+// q/k/v/o given with explicit [b,h,s] element strides (d contiguous)
+void attn_fwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
+              std::vector<int64_t> vs, Tensor o, std::vector<int64_t> os, Tensor lse, int64_t B, int64_t H,
+              int64_t Sq, int64_t Sk, int64_t D, double scale, bool causal) {
+  TORCH_CHECK(D == 64 || D == 128, "flash attention supports head_dim 64/128");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && o.scalar_type() == at::kBFloat16);
+  TORCH_CHECK(lse.numel() >= B * H * Sq && lse.scalar_type() == at::kFloat);
+  for (auto* s : {&qs, &ks, &vs, &os}) TORCH_CHECK(s->size() == 3 && (*s)[2] % 8 == 0, "attn: row stride % 8");
+  ffk::AttnArgs a;
+  a.q = (const uint16_t*)q.data_ptr(); a.q_sb = qs[0]; a.q_sh = qs[1]; a.q_ss = qs[2];
+  a.k = (const uint16_t*)k.data_ptr(); a.k_sb = ks[0]; a.k_sh = ks[1]; a.k_ss = ks[2];
+  a.v = (const uint16_t*)v.data_ptr(); a.v_sb = vs[0]; a.v_sh = vs[1]; a.v_ss = vs[2];
+  a.o = (uint16_t*)o.data_ptr(); a.o_sb = os[0]; a.o_sh = os[1]; a.o_ss = os[2];
+  a.lse = lse.data_ptr<float>();
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.D = D; a.scale = scale; a.causal = causal;
+  ffk::attn_fwd(a, cur_stream());
+}
+int64_t attn_bwd_ws(int64_t B, int64_t H, int64_t Sq, int64_t Sk, int64_t D) {
+  return ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D);
+}
+void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
+              std::vector<int64_t> vs, Tensor o, std::vector<int64_t> os, Tensor dout, std::vector<int64_t> dos,
+              Tensor lse, Tensor dq, std::vector<int64_t> dqs, Tensor dk, std::vector<int64_t> dks, Tensor dv,
+              std::vector<int64_t> dvs, Tensor ws, int64_t B, int64_t H, int64_t Sq, int64_t Sk, int64_t D,
+              double scale, bool causal) {
+  TORCH_CHECK(D == 64 || D == 128, "flash attention supports head_dim 64/128");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D),
+              "attn_bwd: workspace too small");
+  ffk::AttnArgs a;
+  a.q = (const uint16_t*)q.data_ptr(); a.q_sb = qs[0]; a.q_sh = qs[1]; a.q_ss = qs[2];
+  a.k = (const uint16_t*)k.data_ptr(); a.k_sb = ks[0]; a.k_sh = ks[1]; a.k_ss = ks[2];
+  a.v = (const uint16_t*)v.data_ptr(); a.v_sb = vs[0]; a.v_sh = vs[1]; a.v_ss = vs[2];
+  a.o = (uint16_t*)o.data_ptr(); a.o_sb = os[0]; a.o_sh = os[1]; a.o_ss = os[2];
+  a.dout = (const uint16_t*)dout.data_ptr(); a.do_sb = dos[0]; a.do_sh = dos[1]; a.do_ss = dos[2];
+  a.dq = (uint16_t*)dq.data_ptr(); a.dq_sb = dqs[0]; a.dq_sh = dqs[1]; a.dq_ss = dqs[2];
+  a.dk = (uint16_t*)dk.data_ptr(); a.dk_sb = dks[0]; a.dk_sh = dks[1]; a.dk_ss = dks[2];
+  a.dv = (uint16_t*)dv.data_ptr(); a.dv_sb = dvs[0]; a.dv_sh = dvs[1]; a.dv_ss = dvs[2];
+  a.lse = lse.data_ptr<float>();
+  const int nkb = (Sk + 127) / 128;
+  a.dq_acc = ws.data_ptr<float>();
+  a.delta = a.dq_acc + (int64_t)nkb * B * H * Sq * D;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.D = D; a.scale = scale; a.causal = causal;
+  ffk::attn_bwd(a, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "flexflow_amd HIP/CDNA4 kernels (gfx950)";
+  m.def("gemm", &gemm);
+  m.def("gemm_pick_splitk", &gemm_pick_splitk);
+  m.def("unary_fwd", &unary_fwd);
+  m.def("unary_bwd", &unary_bwd);
+  m.def("binary_fwd", &binary_fwd);
+  m.def("binary_bwd", &binary_bwd);
+  m.def("cast", &cast);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd", &dropout_bwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("softmax_fwd", &softmax_fwd);
+  m.def("softmax_bwd", &softmax_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("xent_grad", &xent_grad);
+  m.def("mse_grad", &mse_grad);
+  m.def("metrics_classify", &metrics_classify);
+  m.def("reduce_rows", &reduce_rows);
+  m.def("sgd_update", &sgd_update);
+  m.def("adam_update", &adam_update);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("init_uniform", &init_uniform);
+  m.def("init_normal", &init_normal);
+  m.def("fill", &fill);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd_ws", &attn_bwd_ws);
+}

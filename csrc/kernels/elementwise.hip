@@ -1,0 +1,372 @@
+// Element-wise kernels (unary / scalar / binary with broadcast / cast / dropout / bias+act grad).
+// Memory-bound: 16 B per lane vector path (Guideline 13), grid-stride, capped grid (Guideline 11).
+// Replaces reference src/ops/element_unary.cu, src/ops/kernels/element_binary_kernels.cu,
+// src/ops/kernels/dropout_kernels.cu, src/ops/kernels/cast_kernels.cu.
+#include "common.h"
+#include "ops.h"
+
+namespace ffk {
+
+__device__ __forceinline__ float unary_f(int op, float x, float s) {
+  switch (op) {
+    case U_RELU: return fmaxf(x, 0.f);
+    case U_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case U_TANH: return tanhf(x);
+    case U_ELU: return x > 0.f ? x : (__expf(x) - 1.f);
+    case U_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case U_EXP: return __expf(x);
+    case U_SIN: return __sinf(x);
+    case U_COS: return __cosf(x);
+    case U_RSQRT: return rsqrtf(x);
+    case U_POW: return powf(x, s);
+    case U_IDENTITY: return x;
+    case U_SCALAR_MUL: return x * s;
+    case U_SCALAR_ADD: return x + s;
+    case U_SCALAR_SUB: return x - s;
+    case U_SCALAR_TRUEDIV: return x / s;
+    case U_SCALAR_FLOORDIV: return floorf(x / s);
+    case U_LOG: return __logf(x);
+    case U_SQRT: return sqrtf(x);
+    case U_NEG: return -x;
+    case U_LEAKY_RELU: return x > 0.f ? x : x * s;
+    default: return x;
+  }
+}
+// d out / d in, given input x and output y
+__device__ __forceinline__ float unary_df(int op, float x, float y, float s) {
+  switch (op) {
+    case U_RELU: return x > 0.f ? 1.f : 0.f;
+    case U_SIGMOID: return y * (1.f - y);
+    case U_TANH: return 1.f - y * y;
+    case U_ELU: return x > 0.f ? 1.f : y + 1.f;
+    case U_GELU: {
+      float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+    }
+    case U_EXP: return y;
+    case U_SIN: return __cosf(x);
+    case U_COS: return -__sinf(x);
+    case U_RSQRT: return -0.5f * y * y * y;
+    case U_POW: return s * powf(x, s - 1.f);
+    case U_IDENTITY: return 1.f;
+    case U_SCALAR_MUL: return s;
+    case U_SCALAR_ADD: return 1.f;
+    case U_SCALAR_SUB: return 1.f;
+    case U_SCALAR_TRUEDIV: return 1.f / s;
+    case U_SCALAR_FLOORDIV: return 0.f;
+    case U_LOG: return 1.f / x;
+    case U_SQRT: return 0.5f / y;
+    case U_NEG: return -1.f;
+    case U_LEAKY_RELU: return x > 0.f ? 1.f : s;
+    default: return 1.f;
+  }
+}
+
+template <typename T>
+__global__ void unary_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int op, float s) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t nv = n / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float v[V];
+    load16(x + i * V, v);
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = unary_f(op, v[j], s);
+    store16(y + i * V, v);
+  }
+  for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = Cvt<T>::from_f(unary_f(op, Cvt<T>::to_f(x[i]), s));
+}
+
+template <typename T>
+__global__ void unary_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy,
+                                 T* __restrict__ dx, int64_t n, int op, float s, int accumulate) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t nv = n / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float xv[V], yv[V], g[V], o[V];
+    load16(x + i * V, xv);
+    load16(y + i * V, yv);
+    load16(dy + i * V, g);
+    if (accumulate) load16(dx + i * V, o);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float d = g[j] * unary_df(op, xv[j], yv[j], s);
+      o[j] = accumulate ? o[j] + d : d;
+    }
+    store16(dx + i * V, o);
+  }
+  for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float d = Cvt<T>::to_f(dy[i]) * unary_df(op, Cvt<T>::to_f(x[i]), Cvt<T>::to_f(y[i]), s);
+    dx[i] = Cvt<T>::from_f(accumulate ? Cvt<T>::to_f(dx[i]) + d : d);
+  }
+}
+
+__device__ __forceinline__ float binary_f(int op, float a, float b) {
+  switch (op) {
+    case B_ADD: return a + b;
+    case B_SUB: return a - b;
+    case B_MUL: return a * b;
+    case B_DIV: return a / b;
+    case B_MAX: return fmaxf(a, b);
+    case B_MIN: return fminf(a, b);
+    default: return a;
+  }
+}
+
+// Same-shape fast path.
+template <typename T>
+__global__ void binary_same_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ c,
+                                   int64_t n, int op) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t nv = n / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float av[V], bv[V];
+    load16(a + i * V, av);
+    load16(b + i * V, bv);
+#pragma unroll
+    for (int j = 0; j < V; ++j) av[j] = binary_f(op, av[j], bv[j]);
+    store16(c + i * V, av);
+  }
+  for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    c[i] = Cvt<T>::from_f(binary_f(op, Cvt<T>::to_f(a[i]), Cvt<T>::to_f(b[i])));
+}
+
+// General broadcast path: output shape `shape` (ndim <= 6), strides of a/b in elements
+// (0 on broadcast dims).
+struct BcastDesc {
+  int ndim;
+  int64_t shape[6];
+  int64_t sa[6];
+  int64_t sb[6];
+};
+template <typename T>
+__global__ void binary_bcast_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ c,
+                                    int64_t n, int op, BcastDesc d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t rem = i, oa = 0, ob = 0;
+    for (int k = d.ndim - 1; k >= 0; --k) {
+      const int64_t idx = rem % d.shape[k];
+      rem /= d.shape[k];
+      oa += idx * d.sa[k];
+      ob += idx * d.sb[k];
+    }
+    c[i] = Cvt<T>::from_f(binary_f(op, Cvt<T>::to_f(a[oa]), Cvt<T>::to_f(b[ob])));
+  }
+}
+
+// Binary backward at full output shape: da_full = dc * d(op)/da, db_full = dc * d(op)/db.
+// (Reduction over broadcast dims is done by the caller.)
+template <typename T>
+__global__ void binary_bwd_kernel(const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ dc,
+                                  T* __restrict__ da, T* __restrict__ db, int64_t n, int op, BcastDesc d,
+                                  int same) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t oa = i, ob = i;
+    if (!same) {
+      int64_t rem = i;
+      oa = 0; ob = 0;
+      for (int k = d.ndim - 1; k >= 0; --k) {
+        const int64_t idx = rem % d.shape[k];
+        rem /= d.shape[k];
+        oa += idx * d.sa[k];
+        ob += idx * d.sb[k];
+      }
+    }
+    const float g = Cvt<T>::to_f(dc[i]);
+    const float av = Cvt<T>::to_f(a[oa]), bv = Cvt<T>::to_f(b[ob]);
+    float ga, gb;
+    switch (op) {
+      case B_ADD: ga = g; gb = g; break;
+      case B_SUB: ga = g; gb = -g; break;
+      case B_MUL: ga = g * bv; gb = g * av; break;
+      case B_DIV: ga = g / bv; gb = -g * av / (bv * bv); break;
+      case B_MAX: ga = av >= bv ? g : 0.f; gb = av >= bv ? 0.f : g; break;
+      case B_MIN: ga = av <= bv ? g : 0.f; gb = av <= bv ? 0.f : g; break;
+      default: ga = g; gb = 0.f;
+    }
+    if (da) da[i] = Cvt<T>::from_f(ga);
+    if (db) db[i] = Cvt<T>::from_f(gb);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = Cvt<TO>::from_f(Cvt<TI>::to_f(x[i]));
+}
+
+// Counter-based RNG (splitmix64 finaliser of (seed, offset, index)): deterministic per global
+// element index, so every shard of a partitioned tensor draws the same mask as a 1-GPU run.
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ mask, int64_t n,
+                               float rate, uint64_t seed, uint64_t offset) {
+  const float scale = 1.f / (1.f - rate);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const bool keep = hash_uniform(seed, offset + i) >= rate;
+    mask[i] = keep;
+    y[i] = Cvt<T>::from_f(keep ? Cvt<T>::to_f(x[i]) * scale : 0.f);
+  }
+}
+template <typename T>
+__global__ void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask, T* __restrict__ dx,
+                                   int64_t n, float rate, int accumulate) {
+  const float scale = 1.f / (1.f - rate);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = mask[i] ? Cvt<T>::to_f(dy[i]) * scale : 0.f;
+    if (accumulate) v += Cvt<T>::to_f(dx[i]);
+    dx[i] = Cvt<T>::from_f(v);
+  }
+}
+
+// Fused activation-backward + bias-gradient for Linear/Conv epilogues:
+//   dz[r][c] = dy[r][c] * act'(z[r][c]);  dbias[c] += sum_r dz[r][c]   (fp32 atomics, one per
+//   column per block-row-chunk; Guideline 12 sizing: N*gridDim.y atomics total).
+// Each thread owns 8 consecutive columns (16 B of bf16) and walks ROWS_PER_BLOCK rows.
+template <typename T>
+__global__ void bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z, T* __restrict__ dz,
+                                    float* __restrict__ dbias, int rows, int cols, int act, int rows_per_block) {
+  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c0 >= cols) return;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool vec = (c0 + 8 <= cols) && ((cols & 7) == 0) && sizeof(T) == 2;
+  for (int r = r0; r < r1; ++r) {
+    const int64_t base = (int64_t)r * cols + c0;
+    float g[8], zz[8];
+    if (vec) {
+      load16(dy + base, g);
+      if (act != ACT_NONE) load16(z + base, zz);
+    } else {
+      for (int j = 0; j < 8; ++j) {
+        g[j] = (c0 + j < cols) ? Cvt<T>::to_f(dy[base + j]) : 0.f;
+        zz[j] = (act != ACT_NONE && c0 + j < cols) ? Cvt<T>::to_f(z[base + j]) : 0.f;
+      }
+    }
+    if (act != ACT_NONE) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] *= act_grad(act, zz[j]);
+      if (dz) {
+        if (vec) store16(dz + base, g);
+        else for (int j = 0; j < 8; ++j) if (c0 + j < cols) dz[base + j] = Cvt<T>::from_f(g[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += g[j];
+  }
+  if (dbias) {
+    for (int j = 0; j < 8; ++j)
+      if (c0 + j < cols) atomicAdd(dbias + c0 + j, acc[j]);
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+#define FFK_DT_DISPATCH(dt, ...)                        \
+  do {                                                  \
+    if (dt == DT_BF16) { using T = bf16_t; __VA_ARGS__; } \
+    else { using T = float; __VA_ARGS__; }              \
+  } while (0)
+
+void unary_fwd(int dt, const void* x, void* y, int64_t n, int op, float s, hipStream_t st) {
+  if (n == 0) return;
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(unary_fwd_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
+                       (const T*)x, (T*)y, n, op, s);
+  });
+}
+void unary_bwd(int dt, const void* x, const void* y, const void* dy, void* dx, int64_t n, int op, float s,
+               int accumulate, hipStream_t st) {
+  if (n == 0) return;
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(unary_bwd_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
+                       (const T*)x, (const T*)y, (const T*)dy, (T*)dx, n, op, s, accumulate);
+  });
+}
+void binary_fwd(int dt, const void* a, const void* b, void* c, int64_t n, int op, int ndim,
+                const int64_t* shape, const int64_t* sa, const int64_t* sb, int same, hipStream_t st) {
+  if (n == 0) return;
+  BcastDesc d;
+  d.ndim = ndim;
+  for (int i = 0; i < ndim; ++i) { d.shape[i] = shape[i]; d.sa[i] = sa[i]; d.sb[i] = sb[i]; }
+  FFK_DT_DISPATCH(dt, {
+    if (same && ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && ((uintptr_t)c % 16 == 0))
+      hipLaunchKernelGGL(binary_same_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
+                         (const T*)a, (const T*)b, (T*)c, n, op);
+    else {
+      if (same) { d.ndim = 1; d.shape[0] = n; d.sa[0] = 1; d.sb[0] = 1; }
+      hipLaunchKernelGGL(binary_bcast_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)a,
+                         (const T*)b, (T*)c, n, op, d);
+    }
+  });
+}
+void binary_bwd(int dt, const void* a, const void* b, const void* dc, void* da, void* db, int64_t n, int op,
+                int ndim, const int64_t* shape, const int64_t* sa, const int64_t* sb, int same, hipStream_t st) {
+  if (n == 0) return;
+  BcastDesc d;
+  d.ndim = ndim;
+  for (int i = 0; i < ndim; ++i) { d.shape[i] = shape[i]; d.sa[i] = sa[i]; d.sb[i] = sb[i]; }
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(binary_bwd_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)a,
+                       (const T*)b, (const T*)dc, (T*)da, (T*)db, n, op, d, same);
+  });
+}
+void cast(int dt_in, int dt_out, const void* x, void* y, int64_t n, hipStream_t st) {
+  if (n == 0) return;
+  dim3 g(ew_grid(n, 256));
+  if (dt_in == DT_F32 && dt_out == DT_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), g, dim3(256), 0, st, (const float*)x, (bf16_t*)y, n);
+  else if (dt_in == DT_BF16 && dt_out == DT_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), g, dim3(256), 0, st, (const bf16_t*)x, (float*)y, n);
+  else if (dt_in == DT_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, dim3(256), 0, st, (const float*)x, (float*)y, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), g, dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, n);
+}
+void dropout_fwd(int dt, const void* x, void* y, uint8_t* mask, int64_t n, float rate, uint64_t seed,
+                 uint64_t offset, hipStream_t st) {
+  if (n == 0) return;
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(dropout_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)x, (T*)y, mask, n,
+                       rate, seed, offset);
+  });
+}
+void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float rate, int accumulate,
+                 hipStream_t st) {
+  if (n == 0) return;
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(dropout_bwd_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)dy, mask,
+                       (T*)dx, n, rate, accumulate);
+  });
+}
+void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, int rows, int cols, int act,
+                  hipStream_t st) {
+  if (rows == 0 || cols == 0) return;
+  const int threads = 256;
+  const int gx = (cols / 8 + threads) / threads;
+  // enough row chunks to fill the chip (~1024 blocks), at least 16 rows each
+  int gy = max(1, min(rows / 16, 1024 / max(gx, 1)));
+  const int rpb = (rows + gy - 1) / gy;
+  gy = (rows + rpb - 1) / rpb;
+  FFK_DT_DISPATCH(dt, {
+    hipLaunchKernelGGL(bias_act_bwd_kernel<T>, dim3(gx, gy), dim3(threads), 0, st, (const T*)dy, (const T*)z,
+                       (T*)dz, dbias, rows, cols, act, rpb);
+  });
+}
+
+}  // namespace ffk

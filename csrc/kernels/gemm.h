@@ -1,0 +1,32 @@
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ffk {
+
+struct GemmArgs {
+  const uint16_t* A = nullptr;  // bf16
+  const uint16_t* B = nullptr;  // bf16
+  void* C = nullptr;            // bf16 or fp32 (out_f32)
+  void* Z = nullptr;            // optional bf16 pre-activation output (same layout as C)
+  const void* bias = nullptr;   // optional [N], fp32 or bf16 (bias_bf16)
+  float* ws = nullptr;          // split-K workspace
+  int M = 0, N = 0, K = 0;
+  int64_t lda = 0, ldb = 0, ldc = 0;
+  int64_t sA = 0, sB = 0, sC = 0;  // batch strides in elements
+  int batch = 1;
+  float alpha = 1.f, beta = 0.f;
+  int act = 10;  // ACT_NONE
+  bool a_kcontig = true, b_kcontig = true;
+  bool out_f32 = false;
+  bool bias_bf16 = false;
+  bool vec_ok = false;
+  int splitk = 1;
+  int kchunk = 0;
+};
+
+void gemm_bf16(GemmArgs p, hipStream_t stream);
+int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk);
+int gemm_pick_splitk(int M, int N, int K, int batch);
+
+}  // namespace ffk

@@ -1,0 +1,275 @@
+// LayerNorm forward (optionally fused with a residual add) and backward.
+// One wave per row; the row stays in VGPRs between the statistics pass and the normalise pass
+// (≤ 4096 columns at 16 B/lane), so HBM traffic is one read of x (+res) and one write of y.
+// dgamma/dbeta: per-wave register partials across a grid-stride set of rows, then one fp32
+// atomic per column per wave (Guideline 12).
+// Replaces reference src/ops/layer_norm.cu (LayerNormForwardCUDAKernel / backward kernels).
+#include "common.h"
+#include "ops.h"
+
+namespace ffk {
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                     T* __restrict__ sum_out, const T* __restrict__ gamma,
+                                                     const T* __restrict__ beta, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int cols, float eps) {
+  constexpr int V = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    float v[NCH][V];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols) {
+        load16(x + base + col, v[c]);
+        if (res) {
+          float r[V];
+          load16(res + base + col, r);
+#pragma unroll
+          for (int j = 0; j < V; ++j) v[c][j] += r[j];
+          if (sum_out) store16(sum_out + base + col, v[c]);
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) s += v[c][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[c][j] = 0.f;
+      }
+    }
+    const float mean = wave_sum(s) / cols;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) { const float d = v[c][j] - mean; q += d * d; }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols) {
+        float g[V], bb[V], o[V];
+        if (gamma) load16(gamma + col, g); else for (int j = 0; j < V; ++j) g[j] = 1.f;
+        if (beta) load16(beta + col, bb); else for (int j = 0; j < V; ++j) bb[j] = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = (v[c][j] - mean) * rstd * g[j] + bb[j];
+        store16(y + base + col, o);
+      }
+    }
+  }
+}
+
+// Generic scalar path (any cols / alignment).
+template <typename T>
+__global__ void ln_fwd_generic(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ sum_out,
+                               const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
+                               float* __restrict__ mean_out, float* __restrict__ rstd_out, int rows, int cols,
+                               float eps) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    float s = 0.f;
+    for (int c = lane; c < cols; c += 64) {
+      float v = Cvt<T>::to_f(x[base + c]);
+      if (res) { v += Cvt<T>::to_f(res[base + c]); if (sum_out) sum_out[base + c] = Cvt<T>::from_f(v); }
+      s += v;
+    }
+    const float mean = wave_sum(s) / cols;
+    float q = 0.f;
+    for (int c = lane; c < cols; c += 64) {
+      float v = Cvt<T>::to_f(x[base + c]) + (res ? Cvt<T>::to_f(res[base + c]) : 0.f);
+      q += (v - mean) * (v - mean);
+    }
+    const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    for (int c = lane; c < cols; c += 64) {
+      float v = Cvt<T>::to_f(x[base + c]) + (res ? Cvt<T>::to_f(res[base + c]) : 0.f);
+      float g = gamma ? Cvt<T>::to_f(gamma[c]) : 1.f;
+      float b = beta ? Cvt<T>::to_f(beta[c]) : 0.f;
+      y[base + c] = Cvt<T>::from_f((v - mean) * rstd * g + b);
+    }
+  }
+}
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const T* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                     const T* __restrict__ dres_in, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, int rows, int cols, int accumulate) {
+  constexpr int V = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  float pg[NCH][V], pb[NCH][V];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < V; ++j) { pg[c][j] = 0.f; pb[c][j] = 0.f; }
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NCH][V], gy[NCH][V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols) {
+        float xv[V], dv[V], g[V];
+        load16(x + base + col, xv);
+        load16(dy + base + col, dv);
+        if (gamma) load16(gamma + col, g); else for (int j = 0; j < V; ++j) g[j] = 1.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          xh[c][j] = (xv[j] - mean) * rstd;
+          pg[c][j] += dv[j] * xh[c][j];
+          pb[c][j] += dv[j];
+          gy[c][j] = dv[j] * g[j];
+          s1 += gy[c][j];
+          s2 += gy[c][j] * xh[c][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) { xh[c][j] = 0.f; gy[c][j] = 0.f; }
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols) {
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = rstd * (gy[c][j] - s1 - xh[c][j] * s2);
+        if (dres_in) {
+          float r[V];
+          load16(dres_in + base + col, r);
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] += r[j];
+        }
+        if (accumulate) {
+          float r[V];
+          load16(dx + base + col, r);
+#pragma unroll
+          for (int j = 0; j < V; ++j) o[j] += r[j];
+        }
+        store16(dx + base + col, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * V;
+    if (col < cols) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (dgamma) atomicAdd(dgamma + col + j, pg[c][j]);
+        if (dbeta) atomicAdd(dbeta + col + j, pb[c][j]);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void ln_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ gamma,
+                               const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                               T* __restrict__ dx, const T* __restrict__ dres_in, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta, int rows, int cols, int accumulate) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = lane; c < cols; c += 64) {
+      const float xh = (Cvt<T>::to_f(x[base + c]) - mean) * rstd;
+      const float d = Cvt<T>::to_f(dy[base + c]);
+      const float g = (gamma ? Cvt<T>::to_f(gamma[c]) : 1.f) * d;
+      s1 += g; s2 += g * xh;
+      if (dgamma) atomicAdd(dgamma + c, d * xh);
+      if (dbeta) atomicAdd(dbeta + c, d);
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+    for (int c = lane; c < cols; c += 64) {
+      const float xh = (Cvt<T>::to_f(x[base + c]) - mean) * rstd;
+      const float g = (gamma ? Cvt<T>::to_f(gamma[c]) : 1.f) * Cvt<T>::to_f(dy[base + c]);
+      float o = rstd * (g - s1 - xh * s2);
+      if (dres_in) o += Cvt<T>::to_f(dres_in[base + c]);
+      if (accumulate) o += Cvt<T>::to_f(dx[base + c]);
+      dx[base + c] = Cvt<T>::from_f(o);
+    }
+  }
+}
+
+static bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
+                   void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st) {
+  if (rows == 0) return;
+  const int esz = dt == DT_BF16 ? 2 : 4;
+  const int V = 16 / esz;
+  const bool vec = (cols % V == 0) && a16(x) && a16(y) && (!res || a16(res)) && (!sum_out || a16(sum_out)) &&
+                   (!gamma || a16(gamma)) && (!beta || a16(beta));
+  const int nch = (cols + 64 * V - 1) / (64 * V);
+  const int blocks = std::max(1, std::min((rows + 3) / 4, 4096));
+#define LNF(T, N) hipLaunchKernelGGL((ln_fwd_kernel<T, N>), dim3(blocks), dim3(256), 0, st, (const T*)x, (const T*)res, \
+                                     (T*)sum_out, (const T*)gamma, (const T*)beta, (T*)y, mean, rstd, rows, cols, eps)
+  if (dt == DT_BF16) {
+    using T = bf16_t;
+    if (vec && nch <= 1) LNF(T, 1); else if (vec && nch <= 2) LNF(T, 2); else if (vec && nch <= 4) LNF(T, 4);
+    else if (vec && nch <= 8) LNF(T, 8);
+    else hipLaunchKernelGGL(ln_fwd_generic<T>, dim3(blocks), dim3(256), 0, st, (const T*)x, (const T*)res, (T*)sum_out,
+                            (const T*)gamma, (const T*)beta, (T*)y, mean, rstd, rows, cols, eps);
+  } else {
+    using T = float;
+    if (vec && nch <= 1) LNF(T, 1); else if (vec && nch <= 2) LNF(T, 2); else if (vec && nch <= 4) LNF(T, 4);
+    else if (vec && nch <= 8) LNF(T, 8);
+    else hipLaunchKernelGGL(ln_fwd_generic<T>, dim3(blocks), dim3(256), 0, st, (const T*)x, (const T*)res, (T*)sum_out,
+                            (const T*)gamma, (const T*)beta, (T*)y, mean, rstd, rows, cols, eps);
+  }
+#undef LNF
+}
+
+void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, int rows, int cols, int accumulate,
+                   hipStream_t st) {
+  if (rows == 0) return;
+  const int esz = dt == DT_BF16 ? 2 : 4;
+  const int V = 16 / esz;
+  const bool vec = (cols % V == 0) && a16(x) && a16(dy) && a16(dx) && (!dres_in || a16(dres_in)) &&
+                   (!gamma || a16(gamma));
+  const int nch = (cols + 64 * V - 1) / (64 * V);
+  // ~16 rows per wave keeps the dgamma/dbeta atomics small while filling the chip
+  const int blocks = std::max(1, std::min((rows + 63) / 64, 1024));
+#define LNB(T, N) hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x, \
+                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, dgamma, dbeta, rows, cols, accumulate)
+  if (dt == DT_BF16) {
+    using T = bf16_t;
+    if (vec && nch <= 1) LNB(T, 1); else if (vec && nch <= 2) LNB(T, 2); else if (vec && nch <= 4) LNB(T, 4);
+    else hipLaunchKernelGGL(ln_bwd_generic<T>, dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                            (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, dgamma, dbeta, rows, cols, accumulate);
+  } else {
+    using T = float;
+    if (vec && nch <= 1) LNB(T, 1); else if (vec && nch <= 2) LNB(T, 2); else if (vec && nch <= 4) LNB(T, 4);
+    else hipLaunchKernelGGL(ln_bwd_generic<T>, dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                            (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, dgamma, dbeta, rows, cols, accumulate);
+  }
+#undef LNB
+}
+
+}  // namespace ffk

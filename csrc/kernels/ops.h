@@ -1,0 +1,86 @@
+// Host-side launcher declarations of the flexflow_amd HIP kernel library. Every launcher takes raw
+// device pointers and a hipStream_t so that it can be captured into a hipGraph (no allocation or
+// synchronisation inside: Guideline 9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ffk {
+
+enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+
+enum UnaryOp : int {
+  U_RELU = 0, U_SIGMOID, U_TANH, U_ELU, U_GELU, U_EXP, U_SIN, U_COS, U_RSQRT, U_POW, U_IDENTITY,
+  U_SCALAR_MUL, U_SCALAR_ADD, U_SCALAR_SUB, U_SCALAR_TRUEDIV, U_SCALAR_FLOORDIV, U_LOG, U_SQRT, U_NEG,
+  U_LEAKY_RELU
+};
+enum BinaryOp : int { B_ADD = 0, B_SUB, B_MUL, B_DIV, B_MAX, B_MIN };
+
+// elementwise.hip
+void unary_fwd(int dt, const void* x, void* y, int64_t n, int op, float s, hipStream_t st);
+void unary_bwd(int dt, const void* x, const void* y, const void* dy, void* dx, int64_t n, int op, float s,
+               int accumulate, hipStream_t st);
+void binary_fwd(int dt, const void* a, const void* b, void* c, int64_t n, int op, int ndim, const int64_t* shape,
+                const int64_t* sa, const int64_t* sb, int same, hipStream_t st);
+void binary_bwd(int dt, const void* a, const void* b, const void* dc, void* da, void* db, int64_t n, int op,
+                int ndim, const int64_t* shape, const int64_t* sa, const int64_t* sb, int same, hipStream_t st);
+void cast(int dt_in, int dt_out, const void* x, void* y, int64_t n, hipStream_t st);
+void dropout_fwd(int dt, const void* x, void* y, uint8_t* mask, int64_t n, float rate, uint64_t seed,
+                 uint64_t offset, hipStream_t st);
+void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float rate, int accumulate,
+                 hipStream_t st);
+void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, int rows, int cols, int act,
+                  hipStream_t st);
+
+// norm.hip
+void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
+                   void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st);
+void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, int rows, int cols, int accumulate,
+                   hipStream_t st);
+
+// softmax.hip
+void softmax_fwd(int dt, const void* x, void* y, int rows, int cols, float scale, hipStream_t st);
+void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int cols, float scale, int accumulate,
+                 hipStream_t st);
+// Fused softmax + sparse categorical cross-entropy: writes per-row loss (fp32) and dlogits = (p - onehot)*gscale.
+void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
+                          int cols, float gscale, hipStream_t st);
+// Loss on already-normalised probabilities (reference semantics: loss follows a Softmax op)
+void xent_grad(int dt, const void* probs, const int* labels, const void* onehot, void* dprobs, float* loss, int rows,
+               int cols, float gscale, int sparse, hipStream_t st);
+void mse_grad(int dt, const void* pred, const void* label, void* dpred, float* loss, int64_t n, float gscale,
+              hipStream_t st);
+
+// optimizer.hip (flat multi-tensor buffers)
+void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
+                int nesterov, float wd, float gscale, hipStream_t st);
+void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,
+                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st);
+
+// embedding.hip
+void embedding_fwd(int dt, int idx64, const void* idx, const void* table, void* out, int64_t n_out_rows, int bag,
+                   int dim, int64_t num_rows, int aggr_avg, hipStream_t st);
+void embedding_bwd(int dt, int idx64, const void* idx, const void* dout, float* dtable, int64_t n_out_rows, int bag,
+                   int dim, int64_t num_rows, int aggr_avg, hipStream_t st);
+
+// init.hip
+void init_uniform(int dt, void* out, int64_t n, float lo, float hi, uint64_t seed, int64_t offset, hipStream_t st);
+void init_normal(int dt, void* out, int64_t n, float mean, float stdv, uint64_t seed, int64_t offset, hipStream_t st);
+void fill(int dt, void* out, int64_t n, float v, hipStream_t st);
+
+// attention.hip (flash attention, bf16, head_dim 64 or 128)
+// q,k,v,o: [B, H, S, D] contiguous (bf16); lse: [B, H, Sq] fp32
+void flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int Sq, int Sk,
+                    int D, float scale, int causal, hipStream_t st);
+void flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                    float* delta_ws, float* dq_acc, void* dq, void* dk, void* dv, int B, int H, int Sq, int Sk, int D,
+                    float scale, int causal, hipStream_t st);
+
+// reduce.hip
+void reduce_rows(int dt, const void* x, void* y, int64_t outer, int64_t red, int64_t inner, int mean,
+                 hipStream_t st);
+void metrics_classify(int dt, const void* probs, const int* labels, int rows, int cols, float* out /*[3]*/,
+                      hipStream_t st);
+
+}  // namespace ffk

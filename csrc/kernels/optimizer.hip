@@ -1,0 +1,102 @@
+// Fused multi-tensor optimizers over flat parameter arenas.
+// All trainable weights of one dtype live in ONE contiguous fp32 master buffer (plus an optional
+// bf16 compute copy), gradients in ONE fp32 buffer: a single launch updates the whole model and
+// writes the bf16 copy in the same pass (no separate cast kernel).
+// Semantics follow reference src/runtime/optimizer_kernel.cu (sgd_update: momentum/nesterov/
+// weight-decay; adam_update with bias-corrected alpha_t computed on the host, optimizer.cc:371).
+#include "common.h"
+#include "ops.h"
+
+namespace ffk {
+
+__global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ v,
+                           bf16_t* __restrict__ wl, int64_t n, float lr, float momentum, int nesterov, float wd,
+                           float gscale) {
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float* wp = &wv.x;
+    float* gp = &gv.x;
+    float4 vv = make_float4(0, 0, 0, 0);
+    if (momentum > 0.f) vv = reinterpret_cast<float4*>(v)[i];
+    float* vp = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gt = gp[j] * gscale + wd * wp[j];
+      if (momentum > 0.f) {
+        vp[j] = vp[j] * momentum + gt;
+        gt = nesterov ? gt + momentum * vp[j] : vp[j];
+      }
+      wp[j] -= lr * gt;
+    }
+    reinterpret_cast<float4*>(w)[i] = wv;
+    if (momentum > 0.f) reinterpret_cast<float4*>(v)[i] = vv;
+    if (wl) {
+      ushort4 o;
+      o.x = f2bf(wp[0]); o.y = f2bf(wp[1]); o.z = f2bf(wp[2]); o.w = f2bf(wp[3]);
+      reinterpret_cast<ushort4*>(wl)[i] = o;
+    }
+  }
+  for (int64_t i = nv * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gt = g[i] * gscale + wd * w[i];
+    if (momentum > 0.f) {
+      v[i] = v[i] * momentum + gt;
+      gt = nesterov ? gt + momentum * v[i] : v[i];
+    }
+    w[i] -= lr * gt;
+    if (wl) wl[i] = f2bf(w[i]);
+  }
+}
+
+__global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, bf16_t* __restrict__ wl, int64_t n, float alpha_t, float b1,
+                            float b2, float wd, float eps, float gscale) {
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* wp = &wv.x; float* gp = &gv.x; float* mp = &mv.x; float* vp = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gt = gp[j] * gscale + wd * wp[j];
+      mp[j] = b1 * mp[j] + (1.f - b1) * gt;
+      vp[j] = b2 * vp[j] + (1.f - b2) * gt * gt;
+      wp[j] -= alpha_t * mp[j] / (sqrtf(vp[j]) + eps);
+    }
+    reinterpret_cast<float4*>(w)[i] = wv;
+    reinterpret_cast<float4*>(m)[i] = mv;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (wl) {
+      ushort4 o;
+      o.x = f2bf(wp[0]); o.y = f2bf(wp[1]); o.z = f2bf(wp[2]); o.w = f2bf(wp[3]);
+      reinterpret_cast<ushort4*>(wl)[i] = o;
+    }
+  }
+  for (int64_t i = nv * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gt = g[i] * gscale + wd * w[i];
+    m[i] = b1 * m[i] + (1.f - b1) * gt;
+    v[i] = b2 * v[i] + (1.f - b2) * gt * gt;
+    w[i] -= alpha_t * m[i] / (sqrtf(v[i]) + eps);
+    if (wl) wl[i] = f2bf(w[i]);
+  }
+}
+
+void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
+                int nesterov, float wd, float gscale, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(sgd_kernel, dim3(ew_grid(n / 4 + 1, 256)), dim3(256), 0, st, master, grad, mom,
+                     (bf16_t*)param_lowp, n, lr, momentum, nesterov, wd, gscale);
+}
+void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,
+                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(n / 4 + 1, 256)), dim3(256), 0, st, master, grad, m, v,
+                     (bf16_t*)param_lowp, n, alpha_t, beta1, beta2, wd, eps, gscale);
+}
+
+}  // namespace ffk

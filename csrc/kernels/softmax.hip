@@ -1,0 +1,236 @@
+// Row softmax fwd/bwd, fused softmax + sparse cross-entropy, CE/MSE loss gradients, metrics.
+// One wave per row; pass 1 is an online max/sum (Appendix B 'Reduction': avoids the 3x re-read),
+// pass 2 normalises. Replaces reference src/ops/kernels/softmax.cu,
+// src/loss_functions/loss_functions.cu and src/metrics_functions/metrics_functions.cu.
+#include "common.h"
+#include "ops.h"
+
+namespace ffk {
+
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) { m = mn; s = 0.f; return; }
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+template <typename T>
+__device__ __forceinline__ void row_stats(const T* __restrict__ xr, int cols, float scale, int lane, float& m,
+                                          float& s) {
+  m = -INFINITY;
+  s = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float v = Cvt<T>::to_f(xr[c]) * scale;
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+}
+
+template <typename T>
+__global__ void softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int rows, int cols, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const T* xr = x + (int64_t)row * cols;
+    T* yr = y + (int64_t)row * cols;
+    float m, s;
+    row_stats(xr, cols, scale, lane, m, s);
+    const float inv = 1.f / s;
+    for (int c = lane; c < cols; c += 64) yr[c] = Cvt<T>::from_f(__expf(Cvt<T>::to_f(xr[c]) * scale - m) * inv);
+  }
+}
+
+template <typename T>
+__global__ void softmax_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy, T* __restrict__ dx, int rows,
+                                   int cols, float scale, int accumulate) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    float d = 0.f;
+    for (int c = lane; c < cols; c += 64) d += Cvt<T>::to_f(y[base + c]) * Cvt<T>::to_f(dy[base + c]);
+    d = wave_sum(d);
+    for (int c = lane; c < cols; c += 64) {
+      float g = scale * Cvt<T>::to_f(y[base + c]) * (Cvt<T>::to_f(dy[base + c]) - d);
+      if (accumulate) g += Cvt<T>::to_f(dx[base + c]);
+      dx[base + c] = Cvt<T>::from_f(g);
+    }
+  }
+}
+
+template <typename T>
+__global__ void softmax_xent_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
+                                    float* __restrict__ loss, T* __restrict__ dlogits, int rows, int cols,
+                                    float gscale) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const T* xr = logits + (int64_t)row * cols;
+    float m, s;
+    row_stats(xr, cols, 1.f, lane, m, s);
+    const int lab = labels[row];
+    const float lse = m + __logf(s);
+    if (lane == 0 && loss) loss[row] = (lab >= 0 && lab < cols) ? lse - Cvt<T>::to_f(xr[lab]) : 0.f;
+    if (dlogits) {
+      T* dr = dlogits + (int64_t)row * cols;
+      for (int c = lane; c < cols; c += 64) {
+        const float p = __expf(Cvt<T>::to_f(xr[c]) - lse);
+        dr[c] = Cvt<T>::from_f((p - (c == lab ? 1.f : 0.f)) * gscale);
+      }
+    }
+  }
+}
+
+// Reference semantics (src/loss_functions/loss_functions.cu): the model ends in a Softmax op,
+// the loss gradient w.r.t. the softmax INPUT is (p - y) * scale and Softmax::backward passes it
+// through. dprobs here is that gradient.
+template <typename T>
+__global__ void xent_grad_kernel(const T* __restrict__ probs, const int* __restrict__ labels,
+                                 const T* __restrict__ onehot, T* __restrict__ dprobs, float* __restrict__ loss,
+                                 int rows, int cols, float gscale, int sparse) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    float l = 0.f;
+    const int lab = sparse ? labels[row] : -1;
+    for (int c = lane; c < cols; c += 64) {
+      const float p = Cvt<T>::to_f(probs[base + c]);
+      const float t = sparse ? (c == lab ? 1.f : 0.f) : Cvt<T>::to_f(onehot[base + c]);
+      dprobs[base + c] = Cvt<T>::from_f((p - t) * gscale);
+      if (t != 0.f) l -= t * __logf(fmaxf(p, 1e-12f));
+    }
+    l = wave_sum(l);
+    if (lane == 0 && loss) loss[row] = l;
+  }
+}
+
+template <typename T>
+__global__ void mse_grad_kernel(const T* __restrict__ pred, const T* __restrict__ label, T* __restrict__ dpred,
+                                float* __restrict__ loss, int64_t n, float gscale) {
+  __shared__ float red[4];
+  float l = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float d = Cvt<T>::to_f(pred[i]) - Cvt<T>::to_f(label[i]);
+    dpred[i] = Cvt<T>::from_f(d * gscale);
+    l += d * d;
+  }
+  l = block_sum<256>(l, red);
+  if (threadIdx.x == 0 && loss) atomicAdd(loss, l);
+}
+
+// metrics: out[0] += #correct (argmax == label), out[1] += sum CE, out[2] += rows
+template <typename T>
+__global__ void metrics_kernel(const T* __restrict__ probs, const int* __restrict__ labels, int rows, int cols,
+                               float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  float correct = 0.f, ce = 0.f, cnt = 0.f;
+  for (int row = wave; row < rows; row += nwaves) {
+    const int64_t base = (int64_t)row * cols;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < cols; c += 64) {
+      const float v = Cvt<T>::to_f(probs[base + c]);
+      if (v > best) { best = v; bi = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float b2 = __shfl_xor(best, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (b2 > best || (b2 == best && i2 < bi)) { best = b2; bi = i2; }
+    }
+    if (lane == 0) {
+      const int lab = labels[row];
+      correct += (bi == lab) ? 1.f : 0.f;
+      if (lab >= 0 && lab < cols) ce += -__logf(fmaxf(Cvt<T>::to_f(probs[base + lab]), 1e-12f));
+      cnt += 1.f;
+    }
+  }
+  if (lane == 0) {
+    atomicAdd(out + 0, correct);
+    atomicAdd(out + 1, ce);
+    atomicAdd(out + 2, cnt);
+  }
+}
+
+// Sum/mean over the middle axis of an [outer][red][inner] view.
+template <typename T>
+__global__ void reduce_mid_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t outer, int64_t red,
+                                  int64_t inner, int mean) {
+  const int64_t total = outer * inner;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t o = i / inner, in = i % inner;
+    const T* p = x + o * red * inner + in;
+    float s = 0.f;
+    for (int64_t r = 0; r < red; ++r) s += Cvt<T>::to_f(p[r * inner]);
+    if (mean) s /= (float)red;
+    y[i] = Cvt<T>::from_f(s);
+  }
+}
+
+static int row_blocks(int rows) { return std::max(1, std::min((rows + 3) / 4, 8192)); }
+
+#define DT_DISPATCH(dt, ...)                                        \
+  do {                                                              \
+    if (dt == DT_BF16) { using T = bf16_t; __VA_ARGS__; }           \
+    else { using T = float; __VA_ARGS__; }                          \
+  } while (0)
+
+void softmax_fwd(int dt, const void* x, void* y, int rows, int cols, float scale, hipStream_t st) {
+  if (rows == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_fwd_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st, (const T*)x,
+                                     (T*)y, rows, cols, scale));
+}
+void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int cols, float scale, int accumulate,
+                 hipStream_t st) {
+  if (rows == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_bwd_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st, (const T*)y,
+                                     (const T*)dy, (T*)dx, rows, cols, scale, accumulate));
+}
+void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
+                          int cols, float gscale, hipStream_t st) {
+  if (rows == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st,
+                                     (const T*)logits, labels, loss, (T*)dlogits, rows, cols, gscale));
+}
+void xent_grad(int dt, const void* probs, const int* labels, const void* onehot, void* dprobs, float* loss, int rows,
+               int cols, float gscale, int sparse, hipStream_t st) {
+  if (rows == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(xent_grad_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st,
+                                     (const T*)probs, labels, (const T*)onehot, (T*)dprobs, loss, rows, cols, gscale,
+                                     sparse));
+}
+void mse_grad(int dt, const void* pred, const void* label, void* dpred, float* loss, int64_t n, float gscale,
+              hipStream_t st) {
+  if (n == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(mse_grad_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)pred,
+                                     (const T*)label, (T*)dpred, loss, n, gscale));
+}
+void metrics_classify(int dt, const void* probs, const int* labels, int rows, int cols, float* out,
+                      hipStream_t st) {
+  if (rows == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(metrics_kernel<T>, dim3(std::min(row_blocks(rows), 1024)), dim3(256), 0, st,
+                                     (const T*)probs, labels, rows, cols, out));
+}
+void reduce_rows(int dt, const void* x, void* y, int64_t outer, int64_t red, int64_t inner, int mean,
+                 hipStream_t st) {
+  const int64_t total = outer * inner;
+  if (total == 0) return;
+  DT_DISPATCH(dt, hipLaunchKernelGGL(reduce_mid_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
+                                     (T*)y, outer, red, inner, mean));
+}
+
+}  // namespace ffk

@@ -1,0 +1,540 @@
+"""Device-dispatching functional layer over the HIP kernel library.
+
+Every function takes torch tensors. On a HIP device the hand-written gfx950 kernels in
+`flexflow_amd._C` run (and a missing/unbuilt extension is a hard error, never a silent fallback);
+on CPU (unit tests, the `gloo` multi-process tests) an fp32 PyTorch reference of the same math
+runs instead. Plain fp32 GEMMs on the GPU use the vendor BLAS through torch.matmul (library GEMM);
+every bf16 GEMM — the training hot path — is our MFMA kernel with fused epilogues.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+_C = None
+_C_err = None
+
+
+def ext():
+    """The compiled HIP extension; raises loudly if it is not built."""
+    global _C, _C_err
+    if _C is None:
+        try:
+            from flexflow_amd import _C as mod  # noqa: WPS433
+            _C = mod
+        except Exception as e:  # pragma: no cover - exercised on GPU boxes only
+            _C_err = e
+            raise RuntimeError(
+                "flexflow_amd._C (HIP kernels) is not built/loadable; run `python build_ext.py` "
+                f"(original error: {e})") from e
+    return _C
+
+
+def native(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_GELU = 10, 11, 12, 13, 14
+
+
+def act_ref(x, act):
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(x)
+    if act == ACT_TANH:
+        return torch.tanh(x)
+    if act == ACT_GELU:
+        return F.gelu(x)
+    return x
+
+
+def act_grad_ref(z, act):
+    if act == ACT_RELU:
+        return (z > 0).to(z.dtype)
+    if act == ACT_SIGMOID:
+        s = torch.sigmoid(z)
+        return s * (1 - s)
+    if act == ACT_TANH:
+        t = torch.tanh(z)
+        return 1 - t * t
+    if act == ACT_GELU:
+        cdf = 0.5 * (1 + torch.erf(z * 0.7071067811865476))
+        return cdf + z * 0.3989422804014327 * torch.exp(-0.5 * z * z)
+    return torch.ones_like(z)
+
+
+# ----------------------------------------------------------------------------------- GEMM
+def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=None, Z=None, act=ACT_NONE,
+         batch=1, sA=0, sB=0, sC=0, splitk=None):
+    """C = act(alpha*op(A).op(B) + beta*C + bias); raw strided views (see csrc/kernels/gemm.hip)."""
+    if native(C) and A.dtype == torch.bfloat16:
+        X = ext()
+        if splitk is None:
+            splitk = X.gemm_pick_splitk(M, N, K, batch) if batch == 1 else 1
+        ws = None
+        if splitk > 1:
+            ws = torch.empty(M * N * batch * splitk, device=C.device, dtype=torch.float32)
+        X.gemm(A, B, C, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act,
+               splitk, ws)
+        return C
+    # reference / fp32 path (library GEMM on device, plain torch on CPU)
+    Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)
+    Bf = B.as_strided((batch, N, K), (sB, ldb, 1)).transpose(1, 2) if b_k else B.as_strided((batch, K, N), (sB, ldb, 1))
+    cdt = torch.float32
+    r = torch.matmul(Af.to(cdt), Bf.to(cdt)) * alpha
+    Cv = C.as_strided((batch, M, N), (sC, ldc, 1))
+    if beta != 0.0:
+        r = r + beta * Cv.to(cdt)
+    if bias is not None:
+        r = r + bias.to(cdt)
+    if Z is not None:
+        Z.as_strided((batch, M, N), (sC, ldc, 1)).copy_(r)
+    Cv.copy_(act_ref(r, act))
+    return C
+
+
+def linear_fwd(x2d, w, bias, act, save_z):
+    """y = act(x.w^T + b) for x2d [M,K], w [N,K]. Returns (y, z_or_None)."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, device=x2d.device, dtype=x2d.dtype)
+    z = torch.empty_like(y) if (save_z and act != ACT_NONE) else None
+    if native(x2d) and x2d.dtype == torch.bfloat16:
+        gemm(x2d, w, y, M, N, K, True, True, K, K, N, bias=bias, Z=z, act=act)
+        return y, z
+    r = x2d.float() @ w.float().t()
+    if bias is not None:
+        r = r + bias.float()
+    if z is not None:
+        z.copy_(r)
+    y.copy_(act_ref(r, act))
+    return y, z
+
+
+def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True):
+    """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+=). Returns dx (or None)."""
+    M, N = dy2d.shape
+    K = x2d.shape[1]
+    if act != ACT_NONE:
+        dz = bias_act_bwd(dy2d, z, act, db)
+    else:
+        dz = dy2d
+        if db is not None:
+            bias_grad(dz, db)
+    dx = None
+    if native(dy2d) and dy2d.dtype == torch.bfloat16:
+        if need_dx:
+            dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
+            gemm(dz, w, dx, M, K, N, True, False, N, K, K)
+        if dw is not None:
+            gemm(dz, x2d, dw, N, K, M, False, False, N, K, K, beta=1.0)
+        return dx
+    dzf = dz.float()
+    if need_dx:
+        dx = (dzf @ w.float()).to(dy2d.dtype)
+    if dw is not None:
+        dw.add_(dzf.t() @ x2d.float())
+    return dx
+
+
+def bias_grad(dy2d, db):
+    if native(dy2d):
+        ext().bias_act_bwd(dy2d, None, None, db, dy2d.shape[0], dy2d.shape[1], ACT_NONE)
+    else:
+        db.add_(dy2d.float().sum(0))
+
+
+def bias_act_bwd(dy2d, z, act, db):
+    """dz = dy*act'(z); db += colsum(dz)."""
+    if native(dy2d):
+        dz = torch.empty_like(dy2d)
+        ext().bias_act_bwd(dy2d, z, dz, db, dy2d.shape[0], dy2d.shape[1], act)
+        return dz
+    dz = (dy2d.float() * act_grad_ref(z.float(), act)).to(dy2d.dtype)
+    if db is not None:
+        db.add_(dz.float().sum(0))
+    return dz
+
+
+def bmm(a, b, trans_a=False, trans_b=False, out=None):
+    """Batched matmul over the leading dims: a [..., M, K] (or [..., K, M] if trans_a)."""
+    if native(a) and a.dtype == torch.bfloat16 and a.is_contiguous() and b.is_contiguous():
+        batch = int(math.prod(a.shape[:-2]))
+        M = a.shape[-1] if trans_a else a.shape[-2]
+        K = a.shape[-2] if trans_a else a.shape[-1]
+        N = b.shape[-2] if trans_b else b.shape[-1]
+        if out is None:
+            out = torch.empty(*a.shape[:-2], M, N, device=a.device, dtype=a.dtype)
+        gemm(a, b, out, M, N, K, not trans_a, trans_b, a.shape[-1], b.shape[-1], N, batch=batch,
+             sA=a.shape[-1] * a.shape[-2], sB=b.shape[-1] * b.shape[-2], sC=M * N, splitk=1)
+        return out
+    aa = a.transpose(-1, -2) if trans_a else a
+    bb = b.transpose(-1, -2) if trans_b else b
+    r = torch.matmul(aa.float(), bb.float()).to(a.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+# ------------------------------------------------------------------------------ attention
+def attn_supported(x, D):
+    return native(x) and x.dtype == torch.bfloat16 and D in (64, 128)
+
+
+def flash_attn_fwd(q, qs, k, ks, v, vs, o, os_, B, H, Sq, Sk, D, scale, causal):
+    lse = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
+    ext().attn_fwd(q, qs, k, ks, v, vs, o, os_, lse, B, H, Sq, Sk, D, scale, causal)
+    return lse
+
+
+def flash_attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, B, H, Sq, Sk, D, scale,
+                   causal):
+    X = ext()
+    ws = torch.empty(X.attn_bwd_ws(B, H, Sq, Sk, D), device=q.device, dtype=torch.float32)
+    X.attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, ws, B, H, Sq, Sk, D, scale,
+               causal)
+
+
+# ---------------------------------------------------------------------------- layer norm
+def layernorm_fwd(x2d, res2d, gamma, beta, eps, save_sum):
+    """y = LN(x + res). Returns (y, sum_or_x, mean, rstd)."""
+    rows, cols = x2d.shape
+    if native(x2d):
+        y = torch.empty_like(x2d)
+        mean = torch.empty(rows, device=x2d.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        s = torch.empty_like(x2d) if res2d is not None else None
+        ext().layernorm_fwd(x2d, res2d, s, gamma, beta, y, mean, rstd, rows, cols, eps)
+        return y, (s if s is not None else x2d), mean, rstd
+    xs = x2d.float() + (res2d.float() if res2d is not None else 0)
+    mean = xs.mean(-1)
+    var = xs.var(-1, unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    y = (xs - mean[:, None]) * rstd[:, None]
+    if gamma is not None:
+        y = y * gamma.float()
+    if beta is not None:
+        y = y + beta.float()
+    return y.to(x2d.dtype), xs.to(x2d.dtype), mean, rstd
+
+
+def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None):
+    rows, cols = dy2d.shape
+    if native(dy2d):
+        dx = torch.empty_like(dy2d)
+        ext().layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False)
+        return dx
+    xh = (xs2d.float() - mean[:, None]) * rstd[:, None]
+    dy = dy2d.float()
+    g = dy * (gamma.float() if gamma is not None else 1.0)
+    s1 = g.mean(-1, keepdim=True)
+    s2 = (g * xh).mean(-1, keepdim=True)
+    dx = rstd[:, None] * (g - s1 - xh * s2)
+    if dres is not None:
+        dx = dx + dres.float()
+    if dgamma is not None:
+        dgamma.add_((dy * xh).sum(0))
+    if dbeta is not None:
+        dbeta.add_(dy.sum(0))
+    return dx.to(dy2d.dtype)
+
+
+# ----------------------------------------------------------------------------- softmax/loss
+def softmax_fwd(x2d):
+    if native(x2d):
+        y = torch.empty_like(x2d)
+        ext().softmax_fwd(x2d, y, x2d.shape[0], x2d.shape[1], 1.0)
+        return y
+    return torch.softmax(x2d.float(), -1).to(x2d.dtype)
+
+
+def softmax_bwd(y2d, dy2d):
+    if native(y2d):
+        dx = torch.empty_like(dy2d)
+        ext().softmax_bwd(y2d, dy2d, dx, y2d.shape[0], y2d.shape[1], 1.0, False)
+        return dx
+    y = y2d.float()
+    d = dy2d.float()
+    return (y * (d - (d * y).sum(-1, keepdim=True))).to(dy2d.dtype)
+
+
+def xent_grad(probs2d, labels, onehot, gscale, sparse):
+    """(p - y)*gscale and per-row CE; labels int32 [rows] (sparse) or onehot [rows, C]."""
+    rows, cols = probs2d.shape
+    if native(probs2d):
+        d = torch.empty_like(probs2d)
+        loss = torch.empty(rows, device=probs2d.device, dtype=torch.float32)
+        ext().xent_grad(probs2d, labels if sparse else None, None if sparse else onehot, d, loss, rows, cols,
+                        gscale, sparse)
+        return d, loss
+    p = probs2d.float()
+    t = F.one_hot(labels.long(), cols).float() if sparse else onehot.float()
+    d = ((p - t) * gscale).to(probs2d.dtype)
+    loss = -(t * torch.log(p.clamp_min(1e-12))).sum(-1)
+    return d, loss
+
+
+def softmax_xent(logits2d, labels, gscale):
+    rows, cols = logits2d.shape
+    if native(logits2d):
+        d = torch.empty_like(logits2d)
+        loss = torch.empty(rows, device=logits2d.device, dtype=torch.float32)
+        ext().softmax_xent(logits2d, labels, loss, d, rows, cols, gscale)
+        return d, loss
+    lf = logits2d.float()
+    p = torch.softmax(lf, -1)
+    t = F.one_hot(labels.long(), cols).float()
+    return ((p - t) * gscale).to(logits2d.dtype), -(t * torch.log_softmax(lf, -1)).sum(-1)
+
+
+def mse_grad(pred, label, gscale):
+    if native(pred):
+        d = torch.empty_like(pred)
+        loss = torch.zeros(1, device=pred.device, dtype=torch.float32)
+        ext().mse_grad(pred.contiguous(), label.contiguous().to(pred.dtype), d, loss, gscale)
+        return d, loss
+    diff = pred.float() - label.float()
+    return (diff * gscale).to(pred.dtype), (diff * diff).sum().reshape(1)
+
+
+# ------------------------------------------------------------------------------ elementwise
+U = dict(relu=0, sigmoid=1, tanh=2, elu=3, gelu=4, exp=5, sin=6, cos=7, rsqrt=8, pow=9, identity=10,
+         scalar_multiply=11, scalar_add=12, scalar_sub=13, scalar_true_divide=14, scalar_floor_divide=15, log=16,
+         sqrt=17, neg=18, leaky_relu=19)
+
+
+def unary_ref(name, x, s):
+    xf = x.float()
+    r = {
+        "relu": lambda: torch.relu(xf), "sigmoid": lambda: torch.sigmoid(xf), "tanh": lambda: torch.tanh(xf),
+        "elu": lambda: F.elu(xf), "gelu": lambda: F.gelu(xf), "exp": lambda: torch.exp(xf),
+        "sin": lambda: torch.sin(xf), "cos": lambda: torch.cos(xf), "rsqrt": lambda: torch.rsqrt(xf),
+        "pow": lambda: torch.pow(xf, s), "identity": lambda: xf, "scalar_multiply": lambda: xf * s,
+        "scalar_add": lambda: xf + s, "scalar_sub": lambda: xf - s, "scalar_true_divide": lambda: xf / s,
+        "scalar_floor_divide": lambda: torch.floor(xf / s), "log": lambda: torch.log(xf),
+        "sqrt": lambda: torch.sqrt(xf), "neg": lambda: -xf, "leaky_relu": lambda: F.leaky_relu(xf, s),
+    }[name]()
+    return r.to(x.dtype)
+
+
+def unary_fwd(name, x, s=0.0):
+    if native(x) and x.dtype in (torch.bfloat16, torch.float32):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        ext().unary_fwd(xc, y, U[name], float(s))
+        return y
+    return unary_ref(name, x, s)
+
+
+def unary_bwd(name, x, y, dy, s=0.0):
+    if native(x) and x.dtype in (torch.bfloat16, torch.float32):
+        dx = torch.empty_like(dy)
+        ext().unary_bwd(x.contiguous(), y.contiguous(), dy.contiguous(), dx, U[name], float(s), False)
+        return dx
+    xr = x.detach().float().requires_grad_()
+    out = unary_ref(name, xr, s).float() if name != "identity" else xr * 1.0
+    (g,) = torch.autograd.grad(out, xr, dy.float())
+    return g.to(dy.dtype)
+
+
+B = dict(add=0, sub=1, mul=2, div=3, max=4, min=5)
+
+
+def _bcast_desc(a, b, out_shape):
+    nd = len(out_shape)
+
+    def strides(t):
+        shp = [1] * (nd - t.dim()) + list(t.shape)
+        st = [0] * (nd - t.dim()) + list(t.stride())
+        return [0 if shp[i] == 1 and out_shape[i] != 1 else st[i] for i in range(nd)]
+
+    return list(out_shape), strides(a), strides(b)
+
+
+def binary_fwd(name, a, b):
+    out_shape = torch.broadcast_shapes(a.shape, b.shape)
+    if native(a) and a.dtype in (torch.bfloat16, torch.float32) and len(out_shape) <= 6:
+        if b.dtype != a.dtype:
+            b = b.to(a.dtype)
+        c = torch.empty(out_shape, device=a.device, dtype=a.dtype)
+        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape) and a.is_contiguous() and b.is_contiguous()
+        shp, sa, sb = _bcast_desc(a, b, out_shape)
+        ext().binary_fwd(a, b, c, B[name], shp, sa, sb, same)
+        return c
+    af, bf = a.float(), b.float()
+    r = {"add": af + bf, "sub": af - bf, "mul": af * bf, "div": af / bf, "max": torch.maximum(af, bf),
+         "min": torch.minimum(af, bf)}[name]
+    return r.to(a.dtype)
+
+
+def _reduce_to(g, shape):
+    if tuple(g.shape) == tuple(shape):
+        return g
+    nd = g.dim()
+    shp = [1] * (nd - len(shape)) + list(shape)
+    dims = [i for i in range(nd) if shp[i] == 1 and g.shape[i] != 1]
+    r = g.float().sum(dim=dims, keepdim=True) if dims else g.float()
+    return r.reshape(shape).to(g.dtype)
+
+
+def binary_bwd(name, a, b, dc, need_a=True, need_b=True):
+    out_shape = dc.shape
+    if native(dc) and dc.dtype in (torch.bfloat16, torch.float32) and len(out_shape) <= 6:
+        bb = b.to(a.dtype) if b.dtype != a.dtype else b
+        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape) and a.is_contiguous() and b.is_contiguous()
+        shp, sa, sb = _bcast_desc(a, bb, out_shape)
+        da = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_a else None
+        db = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_b else None
+        ext().binary_bwd(a, bb, dc.contiguous(), da, db, B[name], shp, sa, sb, same)
+        return (_reduce_to(da, a.shape) if need_a else None), (_reduce_to(db, b.shape) if need_b else None)
+    ar = a.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_()
+    out = {"add": lambda: ar + br, "sub": lambda: ar - br, "mul": lambda: ar * br, "div": lambda: ar / br,
+           "max": lambda: torch.maximum(ar, br), "min": lambda: torch.minimum(ar, br)}[name]()
+    ga, gb = torch.autograd.grad(out, (ar, br), dc.float())
+    return (ga.to(a.dtype) if need_a else None), (gb.to(b.dtype) if need_b else None)
+
+
+def dropout_fwd(x, rate, seed, offset):
+    if native(x) and x.dtype in (torch.bfloat16, torch.float32):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        mask = torch.empty(xc.numel(), device=x.device, dtype=torch.uint8)
+        ext().dropout_fwd(xc, y, mask, float(rate), int(seed), int(offset))
+        return y, mask
+    g = torch.Generator().manual_seed(int(seed) * 1000003 + int(offset))
+    keep = (torch.rand(x.shape, generator=g) >= rate).to(x.device)
+    return (x * keep / (1 - rate)).to(x.dtype), keep.to(torch.uint8).view(-1)
+
+
+def dropout_bwd(dy, mask, rate):
+    if native(dy):
+        dx = torch.empty_like(dy)
+        ext().dropout_bwd(dy.contiguous(), mask, dx, float(rate), False)
+        return dx
+    return (dy * mask.view(dy.shape).to(dy.dtype) / (1 - rate)).to(dy.dtype)
+
+
+# ----------------------------------------------------------------------------- embedding
+def embedding_fwd(idx, table, bag, avg):
+    dim = table.shape[-1]
+    n = idx.numel() // bag
+    if native(table) and table.dtype in (torch.bfloat16, torch.float32):
+        out = torch.empty(n, dim, device=table.device, dtype=table.dtype)
+        ii = idx.contiguous()
+        if ii.dtype not in (torch.int32, torch.int64):
+            ii = ii.to(torch.int64)
+        ext().embedding_fwd(ii, table, out, n, bag, dim, avg)
+        return out
+    rows = table.float()[idx.long().reshape(n, bag)]
+    r = rows.mean(1) if avg else rows.sum(1)
+    return r.to(table.dtype)
+
+
+def embedding_bwd(idx, dout2d, dtable, bag, avg):
+    dim = dtable.shape[-1]
+    n = idx.numel() // bag
+    if native(dout2d):
+        ii = idx.contiguous()
+        if ii.dtype not in (torch.int32, torch.int64):
+            ii = ii.to(torch.int64)
+        ext().embedding_bwd(ii, dout2d.contiguous(), dtable, n, bag, dim, avg)
+        return
+    g = dout2d.float() / (bag if avg else 1)
+    dtable.index_add_(0, idx.long().reshape(-1), g.repeat_interleave(bag, 0))
+
+
+# ----------------------------------------------------------------------------- optimizers
+def sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale=1.0):
+    if native(master):
+        ext().sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale)
+        return
+    g = grad * gscale + wd * master
+    if momentum > 0:
+        mom.mul_(momentum).add_(g)
+        g = g + momentum * mom if nesterov else mom
+    master.sub_(lr * g)
+    if lowp is not None:
+        lowp.copy_(master)
+
+
+def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0):
+    if native(master):
+        ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale)
+        return
+    g = grad * gscale + wd * master
+    m.mul_(b1).add_((1 - b1) * g)
+    v.mul_(b2).add_((1 - b2) * g * g)
+    master.sub_(alpha_t * m / (v.sqrt() + eps))
+    if lowp is not None:
+        lowp.copy_(master)
+
+
+# ---------------------------------------------------------------------------- initializers
+def _mix64(z):
+    M = (1 << 64) - 1
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9 & M
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EB & M
+    return z ^ (z >> 31)
+
+
+def _u01_ref(seed, idx, stream):
+    # same counter hash as csrc/kernels/init.hip, evaluated with int64 torch ops (wraparound)
+    M = (1 << 64) - 1
+    base = (seed * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019 + stream) & M
+    z = idx.to(torch.int64) * 2
+    z = z + _to_signed(base)
+
+    def xshift(z, s):  # logical shift on 64-bit wrapped values
+        return (z >> s) & ((1 << (64 - s)) - 1)
+
+    z = (z ^ xshift(z, 30)) * _to_signed(0xBF58476D1CE4E5B9)
+    z = (z ^ xshift(z, 27)) * _to_signed(0x94D049BB133111EB)
+    z = z ^ xshift(z, 31)
+    top = xshift(z, 40).to(torch.float64)
+    return ((top + 0.5) / 16777216.0).to(torch.float32)
+
+
+def _to_signed(u):
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def init_uniform(out, lo, hi, seed, offset=0):
+    if native(out):
+        ext().init_uniform(out, lo, hi, int(seed), int(offset))
+        return
+    idx = torch.arange(out.numel(), dtype=torch.int64) + int(offset)
+    out.copy_((lo + (hi - lo) * _u01_ref(int(seed), idx, 0)).view(out.shape))
+
+
+def init_normal(out, mean, std, seed, offset=0):
+    if native(out):
+        ext().init_normal(out, mean, std, int(seed), int(offset))
+        return
+    idx = torch.arange(out.numel(), dtype=torch.int64) + int(offset)
+    a = _u01_ref(int(seed), idx, 0)
+    b = _u01_ref(int(seed), idx, 1)
+    r = torch.sqrt(-2 * torch.log(a)) * torch.cos(6.283185307179586 * b)
+    out.copy_((mean + std * r).view(out.shape))
+
+
+def fill(out, v):
+    if native(out) and out.dtype in (torch.bfloat16, torch.float32):
+        ext().fill(out, float(v))
+    else:
+        out.fill_(v)
+
+
+def metrics_classify(probs2d, labels, acc3):
+    if native(probs2d):
+        ext().metrics_classify(probs2d, labels, probs2d.shape[0], probs2d.shape[1], acc3)
+        return
+    p = probs2d.float()
+    lab = labels.long()
+    acc3[0] += (p.argmax(-1) == lab).float().sum()
+    acc3[1] += -torch.log(p.gather(1, lab[:, None]).clamp_min(1e-12)).sum()
+    acc3[2] += p.shape[0]

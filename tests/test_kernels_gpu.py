@@ -1,0 +1,218 @@
+"""Numerics of the hand-written HIP kernels against plain PyTorch fp32 references (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0, act=10, batch=1, sA=0, sB=0,
+          sC=0, splitk=1, ws=None):
+    lda = A.shape[-1]
+    ldb = B.shape[-1]
+    ldc = C.shape[-1]
+    C_.gemm(A, B, C, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act, splitk, ws)
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024)])
+def test_gemm_layouts(ffC, a_k, b_k, M, N, K):
+    torch.manual_seed(0)
+    Am = torch.randn(M, K, device=DEV).bfloat16()
+    Bn = torch.randn(N, K, device=DEV).bfloat16()
+    A = Am if a_k else Am.t().contiguous()
+    B = Bn if b_k else Bn.t().contiguous()
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _gemm(ffC, A, B, C, M, N, K, a_k, b_k)
+    ref = Am.float() @ Bn.float().t()
+    assert _rel(C, ref) < 1e-2
+
+
+def test_gemm_epilogue_bias_gelu_f32_beta(ffC):
+    torch.manual_seed(1)
+    M, N, K = 384, 512, 256
+    A = torch.randn(M, K, device=DEV).bfloat16()
+    B = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    Z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _gemm(ffC, A, B, C, M, N, K, True, True, bias=bias, Z=Z, act=14)
+    z = A.float() @ B.float().t() + bias
+    assert _rel(Z, z) < 1e-2
+    assert _rel(C, torch.nn.functional.gelu(z)) < 1e-2
+    # fp32 output accumulate (beta=1), alpha scaling
+    C32 = torch.randn(M, N, device=DEV)
+    base = C32.clone()
+    _gemm(ffC, A, B, C32, M, N, K, True, True, alpha=0.5, beta=1.0)
+    assert _rel(C32, base + 0.5 * (A.float() @ B.float().t())) < 1e-4
+
+
+def test_gemm_splitk_and_batch(ffC):
+    torch.manual_seed(2)
+    # wgrad shape: dW[N,K] = dY^T[N,M] X[M,K] with huge reduction dim
+    M, N, K = 256, 192, 8192
+    dY = torch.randn(K, M, device=DEV).bfloat16()  # [tokens][out]  -> A is [K][M] (M contiguous)
+    X = torch.randn(K, N, device=DEV).bfloat16()   # [tokens][in]   -> B is [K][N]
+    ws = torch.empty(M * N * 4, device=DEV)
+    C = torch.zeros(M, N, device=DEV)
+    _gemm(ffC, dY, X, C, M, N, K, False, False, splitk=4, ws=ws)
+    assert _rel(C, dY.float().t() @ X.float()) < 1e-3
+    # strided batch
+    b, M, N, K = 6, 130, 70, 64
+    A = torch.randn(b, M, K, device=DEV).bfloat16()
+    B = torch.randn(b, N, K, device=DEV).bfloat16()
+    C = torch.empty(b, M, N, device=DEV, dtype=torch.bfloat16)
+    _gemm(ffC, A, B, C, M, N, K, True, True, batch=b, sA=M * K, sB=N * K, sC=M * N)
+    assert _rel(C, torch.bmm(A.float(), B.float().transpose(1, 2))) < 1e-2
+
+
+def _attn_ref(q, k, v, scale, causal):
+    s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale
+    if causal:
+        Sq, Sk = s.shape[-2:]
+        mask = torch.ones(Sq, Sk, device=s.device, dtype=torch.bool).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    return torch.einsum("bhqk,bhkd->bhqd", p, v), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("S,D,causal", [(512, 64, False), (200, 64, False), (256, 128, False), (384, 64, True)])
+def test_flash_attention(ffC, S, D, causal):
+    torch.manual_seed(3)
+    B, H = 2, 3
+    q = torch.randn(B, H, S, D, device=DEV).bfloat16()
+    k = torch.randn(B, H, S, D, device=DEV).bfloat16()
+    v = torch.randn(B, H, S, D, device=DEV).bfloat16()
+    o = torch.empty_like(q)
+    lse = torch.empty(B * H * S, device=DEV)
+    st = [H * S * D, S * D, D]
+    scale = 1.0 / math.sqrt(D)
+    ffC.attn_fwd(q, st, k, st, v, st, o, st, lse, B, H, S, S, D, scale, causal)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    ref, ref_lse = _attn_ref(qf, kf, vf, scale, causal)
+    assert _rel(o, ref) < 2e-2
+    assert _rel(lse.view(B, H, S), ref_lse) < 1e-3
+    do = torch.randn_like(q)
+    ref.backward(do.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    ws = torch.empty(ffC.attn_bwd_ws(B, H, S, S, D), device=DEV)
+    ffC.attn_bwd(q, st, k, st, v, st, o, st, do, st, lse, dq, st, dk, st, dv, st, ws, B, H, S, S, D, scale, causal)
+    assert _rel(dv, vf.grad) < 3e-2
+    assert _rel(dk, kf.grad) < 3e-2
+    assert _rel(dq, qf.grad) < 3e-2
+
+
+def test_flash_attention_strided_qkv(ffC):
+    """Q/K/V read straight out of a fused [B,S,3,H,D] projection, O written as [B,S,H,D]."""
+    torch.manual_seed(4)
+    B, S, H, D = 2, 256, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
+    o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=DEV)
+    sq = [S * 3 * H * D, D, 3 * H * D]
+    so = [S * H * D, D, H * D]
+    base = qkv.view(-1)
+    ffC.attn_fwd(base, sq, base[H * D:], sq, base[2 * H * D:], sq, o, so, lse, B, H, S, S, D, 0.125, False)
+    q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3).float() for i in range(3))
+    ref, _ = _attn_ref(q, k, v, 0.125, False)
+    assert _rel(o.permute(0, 2, 1, 3), ref) < 2e-2
+
+
+@pytest.mark.parametrize("cols", [1024, 768, 100])
+def test_layernorm(ffC, cols):
+    torch.manual_seed(5)
+    rows = 300
+    x = torch.randn(rows, cols, device=DEV).bfloat16()
+    r = torch.randn(rows, cols, device=DEV).bfloat16()
+    g = torch.randn(cols, device=DEV).bfloat16()
+    b = torch.randn(cols, device=DEV).bfloat16()
+    y = torch.empty_like(x)
+    s = torch.empty_like(x)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ffC.layernorm_fwd(x, r, s, g, b, y, mean, rstd, rows, cols, 1e-5)
+    xs = (x.float() + r.float()).requires_grad_()
+    gf, bf = g.float().requires_grad_(), b.float().requires_grad_()
+    ref = torch.nn.functional.layer_norm(xs, (cols,), gf, bf, 1e-5)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn_like(x)
+    ref.backward(dy.float())
+    dx = torch.empty_like(x)
+    dg = torch.zeros(cols, device=DEV)
+    db = torch.zeros(cols, device=DEV)
+    ffC.layernorm_bwd(dy, s, g, mean, rstd, dx, None, dg, db, rows, cols, False)
+    assert _rel(dx, xs.grad) < 2e-2
+    assert _rel(dg, gf.grad) < 2e-2
+    assert _rel(db, bf.grad) < 1e-2
+
+
+def test_softmax_and_xent(ffC):
+    torch.manual_seed(6)
+    rows, cols = 257, 1000
+    x = torch.randn(rows, cols, device=DEV)
+    y = torch.empty_like(x)
+    ffC.softmax_fwd(x, y, rows, cols, 1.0)
+    assert _rel(y, torch.softmax(x, -1)) < 1e-5
+    dy = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    ffC.softmax_bwd(y, dy, dx, rows, cols, 1.0, False)
+    xr = x.clone().requires_grad_()
+    torch.softmax(xr, -1).backward(dy)
+    assert _rel(dx, xr.grad) < 1e-4
+    labels = torch.randint(0, cols, (rows,), device=DEV, dtype=torch.int32)
+    loss = torch.empty(rows, device=DEV)
+    dl = torch.empty_like(x)
+    ffC.softmax_xent(x, labels, loss, dl, rows, cols, 1.0 / rows)
+    xr = x.clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(xr, labels.long())
+    ref.backward()
+    assert abs(loss.mean().item() - ref.item()) < 1e-4
+    assert _rel(dl, xr.grad) < 1e-4
+
+
+def test_adam_sgd_embedding_dropout(ffC):
+    torch.manual_seed(7)
+    n = 10001
+    w = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    low = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    w0 = w.clone()
+    ffC.adam_update(w, g, m, v, low, 1e-3, 0.9, 0.999, 0.0, 1e-8, 1.0)
+    mr = 0.1 * g
+    vr = 0.001 * g * g
+    assert _rel(w, w0 - 1e-3 * mr / (vr.sqrt() + 1e-8)) < 1e-6
+    assert _rel(low, w) < 1e-2
+    mom = torch.zeros(n, device=DEV)
+    w1 = w.clone()
+    ffC.sgd_update(w, g, mom, None, 0.1, 0.9, False, 0.0, 1.0)
+    assert _rel(w, w1 - 0.1 * g) < 1e-6
+    # embedding bag sum
+    table = torch.randn(100, 64, device=DEV).bfloat16()
+    idx = torch.randint(0, 100, (32, 3), device=DEV, dtype=torch.int64)
+    out = torch.empty(32, 64, device=DEV, dtype=torch.bfloat16)
+    ffC.embedding_fwd(idx, table, out, 32, 3, 64, False)
+    assert _rel(out, table.float()[idx].sum(1)) < 1e-2
+    dt = torch.zeros(100, 64, device=DEV)
+    dout = torch.randn(32, 64, device=DEV).bfloat16()
+    ffC.embedding_bwd(idx, dout, dt, 32, 3, 64, False)
+    ref = torch.zeros(100, 64, device=DEV).index_add_(0, idx.view(-1), dout.float().repeat_interleave(3, 0))
+    assert _rel(dt, ref) < 1e-5
+    # dropout keeps ~(1-rate) and rescales
+    x = torch.ones(1 << 16, device=DEV)
+    y = torch.empty_like(x)
+    mask = torch.empty(x.numel(), device=DEV, dtype=torch.uint8)
+    ffC.dropout_fwd(x, y, mask, 0.25, 1234, 0)
+    keep = mask.float().mean().item()
+    assert abs(keep - 0.75) < 0.01
+    assert torch.allclose(y[mask.bool()], torch.full_like(y[mask.bool()], 1 / 0.75))
