@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: BERT-Large training throughput (samples/s) under the auto-searched
+parallelization strategy, one process per MI355X (torchrun), bf16 compute, synthetic data.
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Per-GPU batch is fixed (weak scaling): global_batch = batch_per_gpu * N. Every timed step is a
+full training iteration (forward, backward, gradient all-reduce, optimizer update). Rank 0 prints
+ONE JSON line; the step time is the MAX over ranks of the time between two barrier+synchronize
+fences around exactly K steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BASELINE_METRIC = "samples/sec under auto-searched strategy at 1/2/4/8 MI355X; speedup vs DP"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="bert-large", choices=["bert-large", "bert-base", "bert-tiny"])
+    ap.add_argument("--batch-per-gpu", type=int, default=16)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--search", default="unity", help="unity | mcmc | dp")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
+    ap.add_argument("--no-hip-graphs", action="store_true")
+    ap.add_argument("--compare-dp", action="store_true", help="also time pure data parallel (speedup vs DP)")
+    return ap.parse_args()
+
+
+def build(args, search):
+    from flexflow_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+    from flexflow_amd.models.bert import BertConfig, build_bert
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    flags = ["--dtype", args.dtype, "--search", search]
+    if args.no_hip_graphs:
+        flags.append("--no-hip-graphs")
+    cfg = FFConfig(flags)
+    gb = args.batch_per_gpu * world
+    cfg.batch_size = gb
+    bc = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "bert-tiny": BertConfig.tiny}[args.model](args.seq)
+    bc.seq = args.seq
+    bc.max_pos = max(bc.max_pos, args.seq)
+    ff = FFModel(cfg)
+    ids, pos, out = build_bert(ff, gb, bc)
+    opt = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)
+    ff.optimizer = opt
+    ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+    rng = np.random.default_rng(1234)
+    ids.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq), dtype=np.int32))
+    pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (gb, 1)))
+    ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq, 1), dtype=np.int32))
+    return ff, bc, gb
+
+
+def describe(ff, world):
+    """Short parallelism label: dpN when every op is sample-partitioned N ways."""
+    strat = ff.strategy
+    kinds = set()
+    for L in ff.layers:
+        c = strat[L.name]
+        if c.num_parts == 1:
+            kinds.add("single")
+            continue
+        ax = [i for i, d in enumerate(c.degrees) if d > 1]
+        kinds.add("dp" if ax == [0] else "hybrid")
+    if world == 1:
+        return "single"
+    if kinds == {"dp"}:
+        return f"dp{world}"
+    return f"searched-hybrid{world}"
+
+
+def timed(ff, steps, warmup, world):
+    for _ in range(warmup):
+        ff.train_step()
+    sync(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ff.train_step()
+    sync(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def sync(world):
+    if world > 1:
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    ff, bc, gb = build(args, args.search)
+    el = timed(ff, args.steps, args.warmup, world)
+    ms = el / args.steps * 1e3
+    sps = gb * args.steps / el
+    flops = bc.train_flops_per_seq() * gb * args.steps / el
+    res = {
+        "metric": BASELINE_METRIC,
+        "value": round(sps, 3),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (random token ids / labels, random-init weights)",
+        "config": {"model": args.model, "global_batch": gb, "seq_len": bc.seq,
+                   "parallelism": describe(ff, world), "search": (ff.search_report or {}).get("algo"),
+                   "optimizer": args.optimizer, "params": bc.params(), "hidden": bc.hidden, "layers": bc.layers,
+                   "heads": bc.heads, "vocab": bc.vocab},
+        "model_tflops_per_gpu": round(flops / world / 1e12, 2),
+    }
+    if args.compare_dp and world > 1:
+        del ff
+        ff2, _, _ = build(args, "dp")
+        el2 = timed(ff2, args.steps, args.warmup, world)
+        res["dp_samples_per_s"] = round(gb * args.steps / el2, 3)
+        res["speedup_vs_dp"] = round(el2 / el, 4)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

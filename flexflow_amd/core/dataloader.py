@@ -1,0 +1,70 @@
+"""SingleDataLoader (reference include/flexflow/dataloader.h:15-125, src/dataloader/dataloader.cc).
+
+The reference attaches the whole dataset in zero-copy host memory and index-launches a copy
+kernel per GPU shard each iteration. Here each rank keeps the dataset in host memory and, per
+`next_batch`, stages ONLY its own shard of the batch (per the input tensor's layout) into a
+persistent device buffer with an asynchronous pinned-memory H2D copy. When the native data-loader
+ring (flexflow_amd._core.BatchRing) is available the next batch is pre-gathered into pinned memory
+by a background C++ thread while the current step runs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..type import DataType
+
+
+class SingleDataLoader:
+    def __init__(self, ffmodel, input_tensor, full_input, num_samples=None, data_type=None):
+        self.model = ffmodel
+        self.tensor = input_tensor
+        arr = full_input
+        if not isinstance(arr, np.ndarray):
+            arr = np.asarray(arr)
+        if input_tensor.data_type == DataType.DT_INT32 and arr.dtype != np.int32:
+            arr = arr.astype(np.int32)
+        elif input_tensor.data_type == DataType.DT_INT64 and arr.dtype != np.int64:
+            arr = arr.astype(np.int64)
+        elif input_tensor.data_type == DataType.DT_FLOAT and arr.dtype != np.float32:
+            arr = arr.astype(np.float32)
+        bs = input_tensor.dims[0]
+        if arr.ndim == len(input_tensor.dims) - 1:
+            arr = arr.reshape(arr.shape + (1,))
+        self.full = np.ascontiguousarray(arr)
+        self._num_samples = int(num_samples if num_samples is not None else arr.shape[0])
+        self.batch_size = bs
+        self.idx = 0
+        self._ring = None
+        try:
+            from flexflow_amd import _core  # noqa: F401
+            if hasattr(_core, "BatchRing") and self.full.dtype in (np.float32, np.int32, np.int64):
+                self._ring = _core.BatchRing(self.full, bs, 3)
+        except Exception:
+            self._ring = None
+
+    @property
+    def num_samples(self):
+        return self._num_samples
+
+    @num_samples.setter
+    def num_samples(self, v):
+        self._num_samples = int(v)
+
+    def reset(self):
+        self.idx = 0
+        if self._ring is not None:
+            self._ring.reset(0)
+
+    def next_batch(self, ffmodel=None):
+        m = ffmodel or self.model
+        bs = self.batch_size
+        if self.idx + bs > self._num_samples:
+            self.idx = 0
+            if self._ring is not None:
+                self._ring.reset(0)
+        if self._ring is not None:
+            batch = self._ring.next()
+        else:
+            batch = self.full[self.idx:self.idx + bs]
+        m.executor.feed(self.tensor, batch)
+        self.idx += bs

@@ -1,0 +1,76 @@
+"""Layer: a node of the pre-parallelization graph (reference include/flexflow/layer.h:8-63).
+
+Holds op type, attributes (the reference's int/float/vector properties), input/output Tensors and
+weight Parameters. The op semantics live in flexflow_amd.ops (`OPS[op_type]`).
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Any, Dict, List, Optional
+
+from ..type import DataType, OperatorType
+from .tensor import Parameter, Tensor
+
+_layer_guid = itertools.count(1000000)
+
+
+class Layer:
+    def __init__(self, model, op_type: OperatorType, name: Optional[str], inputs: List[Tensor],
+                 attrs: Dict[str, Any]):
+        from ..ops import OPS  # late import (registry)
+        self.model = model
+        self.op_type = op_type
+        self.guid = next(_layer_guid)
+        base = op_type.name[3:].lower()
+        self.name = name or f"{base}_{self.guid - 1000000}"
+        self.inputs = list(inputs)
+        self.attrs = dict(attrs)
+        self.outputs: List[Tensor] = []
+        self.weights: List[Parameter] = []
+        impl_cls = OPS[op_type]
+        out_dims, out_dtypes, wspecs = impl_cls.infer(self.attrs, [t.dims for t in self.inputs],
+                                                      [t.data_type for t in self.inputs])
+        for i, (d, dt) in enumerate(zip(out_dims, out_dtypes)):
+            self.outputs.append(Tensor(d, dt, owner_layer=self, owner_idx=i, name=f"{self.name}:out{i}"))
+        for i, ws in enumerate(wspecs):
+            p = Parameter(ws.dims, ws.dtype, owner_layer=self, owner_idx=i, name=f"{self.name}.{ws.name}",
+                          initializer=ws.init)
+            p.trainable = ws.trainable
+            p.short_name = ws.name
+            self.weights.append(p)
+        self.impl = impl_cls(self)
+
+    # reference Op python API (flexflow_cffi.py Op:57-100)
+    def get_number_parameters(self):
+        return len(self.weights)
+
+    def get_parameter_by_id(self, i):
+        return self.weights[i]
+
+    def get_number_inputs(self):
+        return len(self.inputs)
+
+    def get_input_by_id(self, i):
+        return self.inputs[i]
+
+    def get_number_outputs(self):
+        return len(self.outputs)
+
+    def get_output_by_id(self, i):
+        return self.outputs[i]
+
+    def get_output_tensor(self):
+        return self.outputs[0]
+
+    def get_input_tensor(self):
+        return self.inputs[0]
+
+    def get_weight_tensor(self):
+        return self.weights[0] if self.weights else None
+
+    def get_bias_tensor(self):
+        return self.weights[1] if len(self.weights) > 1 else None
+
+    def __repr__(self):
+        return f"Layer({self.name}, {self.op_type.name}, in={[list(t.dims) for t in self.inputs]}, " \
+               f"out={[list(t.dims) for t in self.outputs]})"

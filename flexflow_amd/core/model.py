@@ -1,0 +1,553 @@
+"""FFModel: the layer-graph builder and training API (reference include/flexflow/model.h:326-958,
+python flexflow_cffi.py FFModel:887-2305).
+
+`compile()` picks a parallelization strategy — imported from a file, data-parallel
+(--only-data-parallel), or searched by the native Unity / MCMC search (flexflow_amd._core) against
+the MI355X cost model — then lowers it to a per-rank Executor. The training loop API
+(forward / zero_gradients / backward / update / compute_metrics, fit / eval) matches the
+reference.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..config import FFConfig
+from ..type import (ActiMode, AggrMode, CompMode, DataType, LossType, MetricsType, OperatorType, PoolType,
+                    RegularizerMode)
+from .layer import Layer
+from .tensor import Parameter, Tensor
+
+
+class PerfMetrics:
+    """reference include/flexflow/metrics_functions.h PerfMetrics."""
+
+    def __init__(self, acc: Optional[np.ndarray] = None, metrics=()):
+        a = acc if acc is not None else np.zeros(8)
+        self.train_all = int(a[3]) if a[3] > 0 else int(a[7])
+        self.train_correct = int(a[1])
+        self.loss = float(a[0])
+        self.cce_loss = float(a[2])
+        self.sparse_cce_loss = float(a[2])
+        self.mse_loss = float(a[4])
+        self.rmse_loss = float(math.sqrt(a[4] / a[6])) if a[6] > 0 else 0.0
+        self.mae_loss = float(a[5])
+        self._n_el = float(a[6])
+        self._n_rows = float(a[7])
+        self.metrics = metrics
+
+    def get_accuracy(self):
+        return 100.0 * self.train_correct / self.train_all if self.train_all else 0.0
+
+    def get_loss(self):
+        return self.loss / self._n_rows if self._n_rows else 0.0
+
+    def __repr__(self):
+        s = [f"loss={self.get_loss():.4f}"]
+        if MetricsType.METRICS_ACCURACY in self.metrics:
+            s.append(f"accuracy: {self.get_accuracy():.2f}% ({self.train_correct} / {self.train_all})")
+        if MetricsType.METRICS_MEAN_SQUARED_ERROR in self.metrics and self._n_el:
+            s.append(f"mse: {self.mse_loss / self._n_el:.4f}")
+        return "[Metrics] " + " ".join(s)
+
+
+def _ensure_dist(config: FFConfig):
+    if config.world_size > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(config.local_rank % torch.cuda.device_count())
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", config.local_rank % torch.cuda.device_count())
+        dist.init_process_group(backend=backend, **kw)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(config.local_rank % torch.cuda.device_count())
+
+
+class FFModel:
+    def __init__(self, ffconfig: Optional[FFConfig] = None):
+        self.config = ffconfig or FFConfig()
+        self.layers: List[Layer] = []
+        self.optimizer = None
+        self.loss_type = None
+        self.metrics = []
+        self.comp_mode = CompMode.TRAINING
+        self.label_tensor: Optional[Tensor] = None
+        self.executor = None
+        self.strategy = None
+        self.search_report = None
+        self._compiled = False
+        self._output = None
+        self._pending_values = {}
+        self.iter_config_seq_length = None
+        self._recompile = None
+        self._step_graph = None
+
+    # ================================================================== graph building
+    def _add(self, op_type, inputs, name=None, **attrs):
+        L = Layer(self, op_type, name, inputs, attrs)
+        self.layers.append(L)
+        return L
+
+    def create_tensor(self, dims, data_type=DataType.DT_FLOAT, create_grad=True, name=None):
+        L = self._add(OperatorType.OP_INPUT, [], name, dims=tuple(dims), data_type=data_type)
+        t = L.outputs[0]
+        t.create_grad = create_grad
+        return t
+
+    def create_constant(self, dims, value, data_type=DataType.DT_FLOAT):
+        t = self.create_tensor(dims, data_type, False)
+        self._pending_values[t.guid] = np.full(dims, value, dtype=np.float32 if data_type == DataType.DT_FLOAT else np.int32)
+        return t
+
+    def map_tensor(self, tensor, parallel_op=None):
+        return tensor
+
+    # ---- element-wise
+    def _unary(self, op, x, name=None, **kw):
+        return self._add(op, [x], name, **kw).outputs[0]
+
+    def exp(self, x, name=None):
+        return self._unary(OperatorType.OP_EXP, x, name)
+
+    def sin(self, x, name=None):
+        return self._unary(OperatorType.OP_SIN, x, name)
+
+    def cos(self, x, name=None):
+        return self._unary(OperatorType.OP_COS, x, name)
+
+    def rsqrt(self, input, name=None):
+        return self._unary(OperatorType.OP_RSQRT, input, name)
+
+    def pow(self, input, exponent, name=None):
+        return self._unary(OperatorType.OP_POW, input, name, scalar=float(exponent))
+
+    def relu(self, input, inplace=True, name=None):
+        return self._unary(OperatorType.OP_RELU, input, name)
+
+    def gelu(self, input, inplace=True, name=None):
+        return self._unary(OperatorType.OP_GELU, input, name)
+
+    def elu(self, input, inplace=True, name=None):
+        return self._unary(OperatorType.OP_ELU, input, name)
+
+    def identity(self, input, name=None):
+        return self._unary(OperatorType.OP_IDENTITY, input, name)
+
+    def sigmoid(self, input, name=None):
+        return self._unary(OperatorType.OP_SIGMOID, input, name)
+
+    def tanh(self, input, name=None):
+        return self._unary(OperatorType.OP_TANH, input, name)
+
+    def scalar_multiply(self, input, scalar, inplace=True, name=None):
+        return self._unary(OperatorType.OP_SCALAR_MULTIPLY, input, name, scalar=float(scalar))
+
+    def scalar_add(self, input, scalar, inplace=True, name=None):
+        return self._unary(OperatorType.OP_SCALAR_ADD, input, name, scalar=float(scalar))
+
+    def scalar_sub(self, input, scalar, inplace=True, name=None):
+        return self._unary(OperatorType.OP_SCALAR_SUB, input, name, scalar=float(scalar))
+
+    def scalar_true_divide(self, input, scalar, inplace=True, name=None):
+        return self._unary(OperatorType.OP_SCALAR_TRUE_DIV, input, name, scalar=float(scalar))
+
+    scalar_truediv = scalar_true_divide
+
+    def scalar_floor_divide(self, input, scalar, name=None):
+        return self._unary(OperatorType.OP_SCALAR_FLOOR_DIV, input, name, scalar=float(scalar))
+
+    def _binary(self, op, x, y, name=None):
+        return self._add(op, [x, y], name).outputs[0]
+
+    def add(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_ADD, x, y, name)
+
+    def subtract(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_SUB, x, y, name)
+
+    def multiply(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_MUL, x, y, name)
+
+    def divide(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_DIV, x, y, name)
+
+    def max(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_MAX, x, y, name)
+
+    def min(self, x, y, inplace_a=False, name=None):
+        return self._binary(OperatorType.OP_EW_MIN, x, y, name)
+
+    def dropout(self, input, rate, seed=0, name=None):
+        return self._unary(OperatorType.OP_DROPOUT, input, name, rate=float(rate), seed=int(seed))
+
+    def cast(self, input, dtype, name=None):
+        return self._add(OperatorType.OP_CAST, [input], name, dtype=dtype).outputs[0]
+
+    # ---- reductions
+    def reduce_sum(self, input, axes, keepdims=False, name=None):
+        return self._add(OperatorType.OP_REDUCE_SUM, [input], name, axes=list(axes), keepdims=keepdims).outputs[0]
+
+    def mean(self, input, dims, keepdims=False, name=None):
+        return self._add(OperatorType.OP_MEAN, [input], name, axes=list(dims), keepdims=keepdims).outputs[0]
+
+    # ---- dense / conv / pool / norm
+    def dense(self, input, out_dim, activation=ActiMode.AC_MODE_NONE, use_bias=True, datatype=DataType.DT_FLOAT,
+              shared_op=None, kernel_initializer=None, bias_initializer=None,
+              kernel_regularizer=None, name=None):
+        L = self._add(OperatorType.OP_LINEAR, [input], name, out_dim=int(out_dim), activation=activation,
+                      use_bias=use_bias, kernel_init=kernel_initializer, bias_init=bias_initializer,
+                      regularizer=kernel_regularizer)
+        self._share(L, shared_op)
+        return L.outputs[0]
+
+    def conv2d(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+               activation=ActiMode.AC_MODE_NONE, groups=1, use_bias=True, shared_op=None, kernel_initializer=None,
+               bias_initializer=None, name=None):
+        L = self._add(OperatorType.OP_CONV2D, [input], name, out_channels=int(out_channels), kernel_h=kernel_h,
+                      kernel_w=kernel_w, stride_h=stride_h, stride_w=stride_w, padding_h=padding_h,
+                      padding_w=padding_w, activation=activation, groups=groups, use_bias=use_bias,
+                      kernel_init=kernel_initializer, bias_init=bias_initializer)
+        self._share(L, shared_op)
+        return L.outputs[0]
+
+    def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+               pool_type=PoolType.POOL_MAX, activation=ActiMode.AC_MODE_NONE, name=None):
+        return self._add(OperatorType.OP_POOL2D, [input], name, kernel_h=kernel_h, kernel_w=kernel_w,
+                         stride_h=stride_h, stride_w=stride_w, padding_h=padding_h, padding_w=padding_w,
+                         pool_type=pool_type, activation=activation).outputs[0]
+
+    def batch_norm(self, input, relu=True, name=None):
+        return self._add(OperatorType.OP_BATCHNORM, [input], name, relu=relu).outputs[0]
+
+    def layer_norm(self, input, axes, elementwise_affine=True, eps=1e-5, name=None):
+        return self._add(OperatorType.OP_LAYERNORM, [input], name, axes=list(axes),
+                         elementwise_affine=elementwise_affine, eps=eps).outputs[0]
+
+    def batch_matmul(self, A, B, a_seq_length_dim=None, b_seq_length_dim=None, name=None):
+        return self._add(OperatorType.OP_BATCHMATMUL, [A, B], name, a_seq_length_dim=a_seq_length_dim,
+                         b_seq_length_dim=b_seq_length_dim).outputs[0]
+
+    def embedding(self, input, num_embeddings, embedding_dim, aggr=AggrMode.AGGR_MODE_NONE, dtype=DataType.DT_FLOAT,
+                  shared_op=None, kernel_initializer=None, name=None):
+        L = self._add(OperatorType.OP_EMBEDDING, [input], name, num_entries=int(num_embeddings),
+                      out_dim=int(embedding_dim), aggr=aggr, data_type=dtype, kernel_init=kernel_initializer)
+        self._share(L, shared_op)
+        return L.outputs[0]
+
+    def multihead_attention(self, query, key, value, embed_dim, num_heads, kdim=0, vdim=0, dropout=0.0, bias=True,
+                            add_bias_kv=False, add_zero_attn=False, kernel_initializer=None, causal=False, name=None):
+        return self._add(OperatorType.OP_MULTIHEAD_ATTENTION, [query, key, value], name, embed_dim=int(embed_dim),
+                         num_heads=int(num_heads), kdim=int(kdim), vdim=int(vdim), dropout=float(dropout), bias=bias,
+                         add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, kernel_init=kernel_initializer,
+                         causal=causal, self_attn=(query is key and key is value)).outputs[0]
+
+    # ---- shape ops
+    def concat(self, tensors, axis, name=None):
+        return self._add(OperatorType.OP_CONCAT, list(tensors), name, axis=int(axis)).outputs[0]
+
+    def split(self, input, sizes, axis, name=None):
+        return list(self._add(OperatorType.OP_SPLIT, [input], name, sizes=sizes, axis=int(axis)).outputs)
+
+    def flat(self, input, name=None):
+        return self._add(OperatorType.OP_FLAT, [input], name).outputs[0]
+
+    def softmax(self, input, axis=-1, name=None):
+        return self._add(OperatorType.OP_SOFTMAX, [input], name, dim=int(axis)).outputs[0]
+
+    def reshape(self, input, shape, name=None):
+        return self._add(OperatorType.OP_RESHAPE, [input], name, shape=tuple(shape)).outputs[0]
+
+    def gather(self, input, index, dim, name=None):
+        return self._add(OperatorType.OP_GATHER, [input, index], name, dim=int(dim)).outputs[0]
+
+    def transpose(self, input, perm, name=None):
+        return self._add(OperatorType.OP_TRANSPOSE, [input], name, perm=tuple(perm)).outputs[0]
+
+    def reverse(self, input, axis, name=None):
+        return self._add(OperatorType.OP_REVERSE, [input], name, axis=int(axis)).outputs[0]
+
+    # ---- mixture of experts
+    def top_k(self, input, k, sorted=False, name=None):
+        return list(self._add(OperatorType.OP_TOPK, [input], name, k=int(k), sorted=sorted).outputs)
+
+    def group_by(self, data, assign, n, alpha, name=None):
+        return list(self._add(OperatorType.OP_GROUP_BY, [data, assign], name, n=int(n), alpha=float(alpha)).outputs)
+
+    def aggregate(self, inputs, n, lambda_bal, name=None):
+        return self._add(OperatorType.OP_AGGREGATE, list(inputs), name, n=int(n),
+                         lambda_bal=float(lambda_bal)).outputs[0]
+
+    def aggregate_spec(self, inputs, n, lambda_bal, name=None):
+        return self._add(OperatorType.OP_AGG_SPEC, list(inputs), name, n=int(n),
+                         lambda_bal=float(lambda_bal)).outputs[0]
+
+    def cache(self, input, num_batches, score_f=None, name=None):
+        L = self._add(OperatorType.OP_CACHE, [input], name, num_batches=int(num_batches))
+        L.attrs["score_f"] = score_f
+        return L.outputs[0]
+
+    def moe(self, input, num_exp, num_select, expert_hidden_size, alpha, lambda_bal):
+        """reference FFModel::moe (src/ops/moe.cc): gate -> top_k -> group_by -> experts -> aggregate."""
+        gate = self.dense(input, num_exp, ActiMode.AC_MODE_RELU)
+        topk_v, topk_i = self.top_k(gate, num_select, False)
+        exp_t = self.group_by(input, topk_i, num_exp, alpha)
+        agg = [self.softmax(topk_v), topk_i, topk_i, gate]
+        for e in exp_t:
+            agg.append(self.softmax(self.dense(e, expert_hidden_size, ActiMode.AC_MODE_RELU)))
+        return self.aggregate(agg, num_exp, lambda_bal)
+
+    def _share(self, L, shared_op):
+        if shared_op is None:
+            return
+        src = shared_op if isinstance(shared_op, Layer) else getattr(shared_op, "owner_layer", None)
+        assert src is not None and len(src.weights) == len(L.weights), "shared_op must have matching weights"
+        for i, w in enumerate(src.weights):
+            assert w.dims == L.weights[i].dims
+        L.weights = list(src.weights)
+        L.attrs["shared_with"] = src.name
+
+    # ================================================================== introspection
+    def get_layers(self):
+        return {i: L for i, L in enumerate(self.layers) if L.op_type != OperatorType.OP_INPUT}
+
+    def _non_input_layers(self):
+        return [L for L in self.layers if L.op_type != OperatorType.OP_INPUT]
+
+    def get_layer_by_id(self, layer_id):
+        return self._non_input_layers()[layer_id]
+
+    def get_last_layer(self):
+        return self._non_input_layers()[-1]
+
+    def get_layer_by_name(self, layer_name):
+        for L in self.layers:
+            if L.name == layer_name:
+                return L
+        return None
+
+    def get_tensor_by_id(self, id):
+        for L in self.layers:
+            for t in L.outputs:
+                if t.guid == id:
+                    return t
+        return None
+
+    def print_layers(self, id=-1):
+        for i, L in enumerate(self._non_input_layers()):
+            if id in (-1, i):
+                cfg = self.strategy.get(L.name) if self.strategy else None
+                print(f"layer[{i}] {L} cfg={cfg}")
+
+    def output_tensor(self):
+        if self._output is not None:
+            return self._output
+        for L in reversed(self.layers):
+            if L.op_type != OperatorType.OP_INPUT:
+                return L.outputs[0]
+        return None
+
+    def set_output(self, t):
+        self._output = t
+
+    # ================================================================== compile
+    def compile(self, optimizer=None, loss_type=None, metrics=None, comp_mode=None):
+        cfg = self.config
+        if optimizer is not None:
+            self.optimizer = optimizer
+        if comp_mode is not None:
+            self.comp_mode = comp_mode
+        self.loss_type = loss_type
+        self.metrics = list(metrics or [])
+        _ensure_dist(cfg)
+        out = self.output_tensor()
+        if loss_type is not None and out is not None:
+            if loss_type == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
+                lab_dims = tuple(out.dims[:-1]) + (1,)
+                self.label_tensor = Tensor(lab_dims, DataType.DT_INT32, name="label")
+            else:
+                self.label_tensor = Tensor(out.dims, out.data_type, name="label")
+        from ..pcg.search import choose_strategy
+        self.strategy, self.search_report = choose_strategy(self)
+        from ..runtime.executor import Executor
+        training = self.comp_mode == CompMode.TRAINING
+        self.executor = Executor(self, self.strategy, loss_type, self.metrics, training=training)
+        self.executor.init_weights(cfg.seed)
+        if self.optimizer is not None and training:
+            self.executor.init_optimizer(self.optimizer)
+        for guid, v in self._pending_values.items():
+            t = self._find_tensor(guid)
+            if t is not None:
+                self.executor.feed(t, v)
+        for L in self.layers:
+            for t in L.outputs:
+                if t._attached is not None:
+                    self.executor.feed(t, t._attached)
+        self._compiled = True
+        if cfg.export_strategy_file and cfg.rank == 0:
+            from ..pcg.strategy import save_strategy
+            save_strategy(cfg.export_strategy_file, self.strategy, cfg.num_devices,
+                          extra={"search": self.search_report})
+
+    def _find_tensor(self, guid):
+        for L in self.layers:
+            for t in L.outputs:
+                if t.guid == guid:
+                    return t
+        if self.label_tensor is not None and self.label_tensor.guid == guid:
+            return self.label_tensor
+        return None
+
+    def init_layers(self):
+        """Weights are initialised at compile (reference init_operators)."""
+        return None
+
+    init_operators = init_layers
+
+    def prefetch(self):
+        return None
+
+    # ================================================================== training loop
+    def forward(self, seq_length=None):
+        if seq_length is not None:
+            self.iter_config_seq_length = seq_length
+        self.executor.forward()
+
+    def zero_gradients(self):
+        self.executor.zero_gradients()
+
+    def backward(self, seq_length=None):
+        self.executor.backward()
+
+    def update(self):
+        self.executor.update(self.optimizer)
+
+    def compute_metrics(self):
+        return None  # metrics accumulate on device during backward; folded lazily
+
+    def reset_metrics(self):
+        self.executor.reset_metrics()
+
+    def get_perf_metrics(self):
+        return PerfMetrics(self.executor.metrics_snapshot(), self.metrics)
+
+    def set_optimizer(self, optimizer):
+        self.optimizer = optimizer
+        if self.executor is not None:
+            self.executor.init_optimizer(optimizer)
+
+    def train_step(self):
+        """One full iteration (forward, zero_gradients, backward, update) — the unit captured by
+        hipGraphs in runtime/graph.py."""
+        from ..runtime.graph import run_train_step
+        run_train_step(self)
+
+    def recompile_on_condition(self, r):
+        """reference FFModel::recompile_on_condition (model.cc:2422-2426)."""
+        self._recompile = r
+        if r.trigger():
+            r.alter()
+
+    def fit(self, x=None, y=None, batch_size=None, epochs=1):
+        """x, y: SingleDataLoader (or lists of them) as in the reference; numpy arrays are wrapped."""
+        from .dataloader import SingleDataLoader
+        xs = x if isinstance(x, (list, tuple)) else [x]
+        if not isinstance(xs[0], SingleDataLoader):
+            inputs = [L.outputs[0] for L in self.layers if L.op_type == OperatorType.OP_INPUT]
+            xs = [SingleDataLoader(self, t, a) for t, a in zip(inputs, xs)]
+        if y is not None and not isinstance(y, SingleDataLoader):
+            y = SingleDataLoader(self, self.label_tensor, y)
+        bs = batch_size or self.config.batch_size
+        num_samples = xs[0].num_samples
+        iters = num_samples // bs
+        ts = time.perf_counter()
+        for ep in range(epochs):
+            for d in xs:
+                d.reset()
+            if y is not None:
+                y.reset()
+            self.reset_metrics()
+            for it in range(iters):
+                for d in xs:
+                    d.next_batch(self)
+                if y is not None:
+                    y.next_batch(self)
+                self.train_step()
+            if self.config.rank == 0 and self.metrics:
+                pm = self.get_perf_metrics()
+                print(f"epoch {ep}: {pm}", flush=True)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        el = time.perf_counter() - ts
+        if self.config.rank == 0:
+            print(f"ELAPSED TIME = {el:.4f}s, THROUGHPUT = {num_samples * epochs / max(el, 1e-9):.2f} samples/s",
+                  flush=True)
+
+    def eval(self, x=None, y=None, batch_size=None):
+        from .dataloader import SingleDataLoader
+        xs = x if isinstance(x, (list, tuple)) else [x]
+        if not isinstance(xs[0], SingleDataLoader):
+            inputs = [L.outputs[0] for L in self.layers if L.op_type == OperatorType.OP_INPUT]
+            xs = [SingleDataLoader(self, t, a) for t, a in zip(inputs, xs)]
+        if y is not None and not isinstance(y, SingleDataLoader):
+            y = SingleDataLoader(self, self.label_tensor, y)
+        bs = batch_size or self.config.batch_size
+        iters = xs[0].num_samples // bs
+        for d in xs:
+            d.reset()
+        if y is not None:
+            y.reset()
+        self.reset_metrics()
+        for it in range(iters):
+            for d in xs:
+                d.next_batch(self)
+            if y is not None:
+                y.next_batch(self)
+            self.executor.forward(training=False)
+            self.executor.compute_loss_grad()
+        pm = self.get_perf_metrics()
+        if self.config.rank == 0:
+            print(f"eval: {pm}", flush=True)
+        return pm
+
+    # ================================================================== data access
+    def create_data_loader(self, batch_tensor, full_array):
+        from .dataloader import SingleDataLoader
+        return SingleDataLoader(self, batch_tensor, full_array)
+
+    def _set_tensor_value(self, t, arr):
+        if isinstance(t, Parameter):
+            return self._set_weight_value(t, arr)
+        if not self._compiled:
+            self._pending_values[t.guid] = np.asarray(arr)
+            return
+        self.executor.feed(t, np.asarray(arr))
+
+    def _get_tensor_value(self, t):
+        v = self.executor.get_value(t)
+        return (v.float() if v.is_floating_point() else v).detach().cpu().numpy().copy()
+
+    def _get_tensor_grad(self, t):
+        if isinstance(t, Parameter):
+            return self.executor.get_weight_grad(t).detach().cpu().numpy().copy()
+        raise NotImplementedError("activation gradients are not retained")
+
+    def _set_weight_value(self, w, arr):
+        self.executor.set_weight(w, np.asarray(arr))
+
+    def _get_weight_value(self, w):
+        return self.executor.get_weight(w).float().detach().cpu().numpy().copy()
+
+    @property
+    def ffconfig(self):
+        return self.config
+
+    def get_output_tensor(self, ffmodel=None, data_type=None):
+        return self._get_tensor_value(self.output_tensor())

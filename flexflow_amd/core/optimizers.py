@@ -1,0 +1,79 @@
+"""SGD and Adam (reference include/flexflow/optimizer.h:15-120, src/runtime/optimizer.cc:23-610,
+optimizer_kernel.cu).
+
+The reference launches one update task per weight (with a NCCL all-reduce inside each). Here
+every weight shard of a replica group lives in one flat fp32 arena, so an update is ONE fused HIP
+kernel per arena (multi-tensor apply) that also refreshes the bf16 compute copy.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import kernels as K
+
+
+class Optimizer:
+    def __init__(self, ffmodel=None, lr=0.01):
+        self.lr = lr
+        self.ffmodel = ffmodel
+        self.state = {}
+
+    def set_learning_rate(self, learning_rate):
+        self.lr = learning_rate
+
+    def init_state(self, arena):
+        pass
+
+    def next(self):
+        pass
+
+    def step(self, arena):
+        raise NotImplementedError
+
+
+class SGDOptimizer(Optimizer):
+    def __init__(self, ffmodel=None, lr=0.01, momentum=0.0, nesterov=False, weight_decay=0.0):
+        super().__init__(ffmodel, lr)
+        self.momentum = momentum
+        self.nesterov = nesterov
+        self.weight_decay = weight_decay
+
+    def init_state(self, arena):
+        if self.momentum > 0:
+            self.state[id(arena)] = torch.zeros_like(arena.master)
+
+    def step(self, arena):
+        K.sgd_update(arena.master, arena.grad, self.state.get(id(arena)), arena.lowp, self.lr, self.momentum,
+                     self.nesterov, self.weight_decay)
+
+
+class AdamOptimizer(Optimizer):
+    def __init__(self, ffmodel=None, alpha=0.001, beta1=0.9, beta2=0.999, weight_decay=0.0, epsilon=1e-8):
+        super().__init__(ffmodel, alpha)
+        self.alpha = alpha
+        self.beta1, self.beta2 = beta1, beta2
+        self.weight_decay = weight_decay
+        self.epsilon = epsilon
+        self.beta1_t = 1.0
+        self.beta2_t = 1.0
+        self.alpha_t = alpha
+
+    def set_learning_rate(self, learning_rate):
+        self.alpha = learning_rate
+        self.lr = learning_rate
+
+    def init_state(self, arena):
+        self.state[id(arena)] = (torch.zeros_like(arena.master), torch.zeros_like(arena.master))
+
+    def next(self):
+        # reference optimizer.cc:371-376
+        self.beta1_t *= self.beta1
+        self.beta2_t *= self.beta2
+        self.alpha_t = self.alpha * math.sqrt(1 - self.beta2_t) / (1 - self.beta1_t)
+
+    def step(self, arena):
+        m, v = self.state[id(arena)]
+        K.adam_update(arena.master, arena.grad, m, v, arena.lowp, self.alpha_t, self.beta1, self.beta2,
+                      self.weight_decay, self.epsilon)

@@ -1,0 +1,217 @@
+"""Conv2D and Pool2D (NCHW), reference src/ops/conv_2d.cc, src/ops/pool_2d.cc (cuDNN).
+
+Parallel axes: N (sample), C_out (parameter; conv only), H and W (attribute parallelism: each part
+computes an output row/col block and reads its input block plus a halo of the receptive field,
+provided by the edge transfer), and for conv a C_in reduction axis with partial-sum outputs.
+Attribute parallelism requires stride-aligned blocks (checked in supports_axis).
+
+Math: MIOpen through torch.nn.functional for now (groups, dilation-free, as the reference).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import kernels as K
+from ..type import ActiMode, OperatorType, PoolType
+from .base import OpImpl, WeightSpec, register
+
+
+def _out_size(i, k, s, p):
+    return (i + 2 * p - k) // s + 1
+
+
+class _Spatial(OpImpl):
+    def _kp(self):
+        a = self.attrs
+        return a["kernel_h"], a["kernel_w"], a["stride_h"], a["stride_w"], a["padding_h"], a["padding_w"]
+
+    def input_halo(self, idx, degrees):
+        if idx != 0:
+            return None
+        kh, kw, sh, sw, ph, pw = self._kp()
+        return (0, 0, kh if degrees[2] > 1 else 0, kw if degrees[3] > 1 else 0)
+
+    def _spatial_ok(self, axis):
+        kh, kw, sh, sw, ph, pw = self._kp()
+        ih, iw = self.layer.inputs[0].dims[2:4]
+        oh, ow = self.layer.outputs[0].dims[2:4]
+        if axis == 2:
+            return ih == oh * sh and kh - 1 == 2 * ph  # 'same'-style tiling, block-aligned input
+        if axis == 3:
+            return iw == ow * sw and kw - 1 == 2 * pw
+        return True
+
+    def _local_input(self, ctx, x, axis_base=2):
+        """Crop the halo'd input block to exactly what this output block needs (+ zero pad at edges)."""
+        kh, kw, sh, sw, ph, pw = self._kp()
+        pads = [pw, pw, ph, ph]
+        if ctx.degree(2) == 1 and ctx.degree(3) == 1:
+            return x, (ph, pw)
+        ih, iw = self.layer.inputs[0].dims[2:4]
+        # region bookkeeping supplied by the executor
+        reg = ctx.extra["in_region0"]
+        out_reg = ctx.extra["out_region"]
+        res = []
+        for d, (k, s, p, full) in zip((2, 3), ((kh, sh, ph, ih), (kw, sw, pw, iw))):
+            olo, ohi = out_reg[d]
+            need_lo, need_hi = olo * s - p, (ohi - 1) * s - p + k
+            have_lo, have_hi = reg[d]
+            lo_pad = max(0, have_lo - need_lo) if need_lo < 0 else 0
+            hi_pad = max(0, need_hi - have_hi) if need_hi > full else 0
+            a = max(need_lo, have_lo) - have_lo
+            b = min(need_hi, have_hi) - have_lo
+            res.append((a, b, lo_pad, hi_pad))
+        (a2, b2, lp2, hp2), (a3, b3, lp3, hp3) = res
+        xc = x[:, :, a2:b2, a3:b3]
+        xc = F.pad(xc, (lp3, hp3, lp2, hp2))
+        return xc, (0, 0)
+
+
+@register(OperatorType.OP_CONV2D)
+class Conv2D(_Spatial):
+    op_type = OperatorType.OP_CONV2D
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        n, c, h, w = in_dims[0]
+        oh = _out_size(h, attrs["kernel_h"], attrs["stride_h"], attrs["padding_h"])
+        ow = _out_size(w, attrs["kernel_w"], attrs["stride_w"], attrs["padding_w"])
+        g = attrs.get("groups", 1)
+        ws = [WeightSpec("kernel", (attrs["out_channels"], c // g, attrs["kernel_h"], attrs["kernel_w"]),
+                         in_dtypes[0], attrs.get("kernel_init"))]
+        if attrs.get("use_bias", True):
+            ws.append(WeightSpec("bias", (attrs["out_channels"],), in_dtypes[0], attrs.get("bias_init")))
+        return [(n, attrs["out_channels"], oh, ow)], [in_dtypes[0]], ws
+
+    def extra_axis_sizes(self):
+        return [self.layer.inputs[0].dims[1]]
+
+    def axis_kinds(self):
+        return ["sample", "parameter", "attribute", "attribute", "parameter"]
+
+    def supports_axis(self, axis):
+        if self.attrs.get("groups", 1) != 1 and axis in (1, 4):
+            return False
+        if axis == 4:
+            return self.attrs.get("activation", ActiMode.AC_MODE_NONE) == ActiMode.AC_MODE_NONE
+        return self._spatial_ok(axis)
+
+    def input_maps(self):
+        return [(0, 4, 2, 3)]
+
+    def weight_maps(self):
+        m = [(1, 4, None, None)]
+        if len(self.layer.weights) > 1:
+            m.append((1,))
+        return m
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        w = ws[0]
+        b = ws[1] if len(ws) > 1 else None
+        if b is not None and ctx.degree(4) > 1 and ctx.coord(4) != 0:
+            b = None
+        kh, kw, sh, sw, ph, pw = self._kp()
+        xc, pad = self._local_input(ctx, x)
+        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE).value
+        xr = xc.detach().requires_grad_(ctx.training)
+        wr = w.detach().requires_grad_(ctx.training)
+        br = b.detach().requires_grad_(ctx.training) if b is not None else None
+        with torch.enable_grad() if ctx.training else torch.no_grad():
+            z = F.conv2d(xr, wr, br, (sh, sw), pad, 1, self.attrs.get("groups", 1))
+            y = K.act_ref(z, act)
+        if ctx.training:
+            ctx.saved.update(xr=xr, wr=wr, br=br, y=y, x_shape=x.shape)
+        return [y.detach()]
+
+    def backward(self, ctx, douts):
+        s = ctx.saved
+        xr, wr, br, y = s.pop("xr"), s.pop("wr"), s.pop("br"), s.pop("y")
+        x_shape = s.pop("x_shape")
+        need = [xr, wr] + ([br] if br is not None else [])
+        grads = torch.autograd.grad(y, need, douts[0].to(y.dtype))
+        if ctx.wgrads:
+            ctx.wgrads[0].add_(grads[1].float())
+            if br is not None and len(ctx.wgrads) > 1:
+                ctx.wgrads[1].add_(grads[2].float())
+        dx = grads[0]
+        if tuple(dx.shape) != tuple(x_shape):  # attribute-parallel: scatter crop back into halo'd block
+            full = torch.zeros(x_shape, dtype=dx.dtype, device=dx.device)
+            full = self._uncrop(ctx, full, dx)
+            dx = full
+        return [dx]
+
+    def _uncrop(self, ctx, full, dxc):
+        kh, kw, sh, sw, ph, pw = self._kp()
+        ih, iw = self.layer.inputs[0].dims[2:4]
+        reg = ctx.extra["in_region0"]
+        out_reg = ctx.extra["out_region"]
+        sl = []
+        for d, (k, s_, p, fullsz) in zip((2, 3), ((kh, sh, ph, ih), (kw, sw, pw, iw))):
+            olo, ohi = out_reg[d]
+            need_lo, need_hi = olo * s_ - p, (ohi - 1) * s_ - p + k
+            have_lo, have_hi = reg[d]
+            a = max(need_lo, have_lo) - have_lo
+            b = min(need_hi, have_hi) - have_lo
+            lo_pad = (have_lo - need_lo) if need_lo < have_lo else 0
+            sl.append((a, b, lo_pad))
+        (a2, b2, l2), (a3, b3, l3) = sl
+        full[:, :, a2:b2, a3:b3] += dxc[:, :, l2:l2 + (b2 - a2), l3:l3 + (b3 - a3)]
+        return full
+
+    def flops(self, in_shapes, out_shapes, w_shapes):
+        w = w_shapes[0]
+        return 2.0 * math.prod(out_shapes[0]) * w[1] * w[2] * w[3]
+
+    def uses_mfma(self):
+        return True
+
+
+@register(OperatorType.OP_POOL2D)
+class Pool2D(_Spatial):
+    op_type = OperatorType.OP_POOL2D
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        n, c, h, w = in_dims[0]
+        oh = _out_size(h, attrs["kernel_h"], attrs["stride_h"], attrs["padding_h"])
+        ow = _out_size(w, attrs["kernel_w"], attrs["stride_w"], attrs["padding_w"])
+        return [(n, c, oh, ow)], [in_dtypes[0]], []
+
+    def axis_kinds(self):
+        return ["sample", "attribute", "attribute", "attribute"]
+
+    def supports_axis(self, axis):
+        return self._spatial_ok(axis)
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        kh, kw, sh, sw, ph, pw = self._kp()
+        xc, pad = self._local_input(ctx, x)
+        xr = xc.detach().requires_grad_(ctx.training)
+        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE).value
+        with torch.enable_grad() if ctx.training else torch.no_grad():
+            if self.attrs.get("pool_type", PoolType.POOL_MAX) == PoolType.POOL_MAX:
+                xp = F.pad(xr, (pad[1], pad[1], pad[0], pad[0]), value=float("-inf")) if any(pad) else xr
+                y = F.max_pool2d(xp, (kh, kw), (sh, sw))
+            else:
+                y = F.avg_pool2d(xr, (kh, kw), (sh, sw), pad, count_include_pad=True)
+            y = K.act_ref(y, act)
+        if ctx.training:
+            ctx.saved.update(xr=xr, y=y, x_shape=x.shape)
+        return [y.detach()]
+
+    def backward(self, ctx, douts):
+        s = ctx.saved
+        xr, y, x_shape = s.pop("xr"), s.pop("y"), s.pop("x_shape")
+        (dx,) = torch.autograd.grad(y, (xr,), douts[0].to(y.dtype))
+        if tuple(dx.shape) != tuple(x_shape):
+            full = torch.zeros(x_shape, dtype=dx.dtype, device=dx.device)
+            dx = Conv2D._uncrop(self, ctx, full, dx)
+        return [dx]
+
+    def flops(self, in_shapes, out_shapes, w_shapes):
+        return float(math.prod(out_shapes[0]) * self.attrs["kernel_h"] * self.attrs["kernel_w"])

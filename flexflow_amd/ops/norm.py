@@ -1,0 +1,123 @@
+"""LayerNorm and BatchNorm.
+
+LayerNorm normalises over the trailing `axes` (reference src/ops/layer_norm.cc; the reference HIP
+build has its fast path disabled, layer_norm.cpp:46-52). Normalised dims cannot be partitioned;
+every other dim can. Runs on csrc/kernels/norm.hip (one wave per row, row kept in VGPRs).
+
+BatchNorm (NCHW, reference src/ops/batch_norm.cc) normalises per channel over N,H,W with
+per-shard statistics when the batch is partitioned — the reference's cuDNN per-partition
+semantics. It has no hand kernel yet: MIOpen via torch does the math.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import kernels as K
+from ..type import DataType, OperatorType
+from .base import OpImpl, WeightSpec, register
+
+
+@register(OperatorType.OP_LAYERNORM)
+class LayerNorm(OpImpl):
+    op_type = OperatorType.OP_LAYERNORM
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        d = in_dims[0]
+        axes = sorted(a % len(d) for a in attrs["axes"])
+        attrs["axes"] = axes
+        ws = []
+        if attrs.get("elementwise_affine", True):
+            nd = tuple(d[a] for a in axes)
+            from ..core.initializers import ConstantInitializer, ZeroInitializer
+            ws = [WeightSpec("gamma", nd, in_dtypes[0], ConstantInitializer(1.0)),
+                  WeightSpec("beta", nd, in_dtypes[0], ZeroInitializer())]
+        return [d], [in_dtypes[0]], ws
+
+    def axis_kinds(self):
+        kinds = super().axis_kinds()
+        for a in self.attrs["axes"]:
+            kinds[a] = "none"
+        return kinds
+
+    def supports_axis(self, axis):
+        return axis not in self.attrs["axes"]
+
+    def weight_maps(self):
+        return [tuple([None] * len(w.dims)) for w in self.layer.weights]
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        nrm = int(math.prod(x.shape[a] for a in self.attrs["axes"]))
+        assert self.attrs["axes"] == list(range(x.dim() - len(self.attrs["axes"]), x.dim())), \
+            "LayerNorm axes must be trailing"
+        x2 = x.reshape(-1, nrm)
+        g = ws[0].reshape(-1) if ws else None
+        b = ws[1].reshape(-1) if ws else None
+        y, xs_, mean, rstd = K.layernorm_fwd(x2, None, g, b, float(self.attrs.get("eps", 1e-5)), False)
+        if ctx.training:
+            ctx.saved.update(x=xs_, mean=mean, rstd=rstd, g=g)
+        return [y.reshape(x.shape)]
+
+    def backward(self, ctx, douts):
+        dy = douts[0]
+        s = ctx.saved
+        x2 = s.pop("x")
+        dg = ctx.wgrads[0].reshape(-1) if ctx.wgrads else None
+        db = ctx.wgrads[1].reshape(-1) if ctx.wgrads else None
+        dx = K.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, s.pop("g"), s.pop("mean"), s.pop("rstd"), dg, db)
+        return [dx.reshape(dy.shape)]
+
+    def flops(self, in_shapes, out_shapes, w_shapes):
+        return 8.0 * math.prod(out_shapes[0])
+
+
+@register(OperatorType.OP_BATCHNORM)
+class BatchNorm(OpImpl):
+    op_type = OperatorType.OP_BATCHNORM
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        d = in_dims[0]
+        from ..core.initializers import ConstantInitializer, ZeroInitializer
+        c = d[1]
+        ws = [WeightSpec("scale", (c,), in_dtypes[0], ConstantInitializer(1.0)),
+              WeightSpec("bias", (c,), in_dtypes[0], ZeroInitializer())]
+        return [d], [in_dtypes[0]], ws
+
+    def axis_kinds(self):
+        # N (sample) and C (parameter) partitionable; spatial dims need cross-shard statistics
+        return ["sample", "parameter"] + ["none"] * (len(self.layer.outputs[0].dims) - 2)
+
+    def supports_axis(self, axis):
+        return axis in (0, 1)
+
+    def weight_maps(self):
+        return [(1,), (1,)]
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        xr = x.detach().float().requires_grad_(ctx.training)
+        g = ws[0].detach().float().requires_grad_(ctx.training)
+        b = ws[1].detach().float().requires_grad_(ctx.training)
+        rm = ctx.extra.setdefault("running_mean", torch.zeros(x.shape[1], device=x.device))
+        rv = ctx.extra.setdefault("running_var", torch.ones(x.shape[1], device=x.device))
+        with torch.enable_grad():
+            y = F.batch_norm(xr, rm, rv, g, b, training=ctx.training, momentum=0.1, eps=1e-5)
+            if self.attrs.get("relu", True):
+                y = torch.relu(y)
+        if ctx.training:
+            ctx.saved.update(xr=xr, g=g, b=b, y=y)
+        return [y.detach().to(x.dtype)]
+
+    def backward(self, ctx, douts):
+        s = ctx.saved
+        xr, g, b, y = s.pop("xr"), s.pop("g"), s.pop("b"), s.pop("y")
+        dx, dg, db = torch.autograd.grad(y, (xr, g, b), douts[0].float())
+        if ctx.wgrads:
+            ctx.wgrads[0].add_(dg)
+            ctx.wgrads[1].add_(db)
+        return [dx.to(douts[0].dtype)]

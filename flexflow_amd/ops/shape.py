@@ -1,0 +1,287 @@
+"""Shape / data-movement ops: input, noop, flat, reshape, transpose, concat, split, reverse, gather.
+
+Reference: src/ops/{noop,flat,reshape,transpose,concat,split,reverse,gather}.cc. These are
+layout-only on the local shard; which dims may be partitioned follows from which dims survive the
+op unchanged (e.g. Reshape/Flat keep the batch dim, Concat/Split/Reverse/Softmax-like ops keep
+every dim except the one they act on).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import kernels as K
+from ..type import DataType, OperatorType
+from .base import OpImpl, register
+
+
+@register(OperatorType.OP_INPUT)
+class Input(OpImpl):
+    op_type = OperatorType.OP_INPUT
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        return [tuple(attrs["dims"])], [attrs["data_type"]], []
+
+    def forward(self, ctx, xs, ws):  # value injected by the executor
+        raise RuntimeError("input op is fed by the executor")
+
+    def backward(self, ctx, douts):
+        return []
+
+
+@register(OperatorType.OP_NOOP)
+class NoOp(OpImpl):
+    op_type = OperatorType.OP_NOOP
+
+    def forward(self, ctx, xs, ws):
+        return [xs[0]]
+
+    def backward(self, ctx, douts):
+        return [douts[0]]
+
+    def flops(self, *a):
+        return 0.0
+
+
+def _batch_only_kinds(n):
+    return ["sample"] + ["none"] * (n - 1)
+
+
+@register(OperatorType.OP_FLAT)
+class Flat(OpImpl):
+    op_type = OperatorType.OP_FLAT
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        d = in_dims[0]
+        return [(d[0], int(math.prod(d[1:])))], [in_dtypes[0]], []
+
+    def axis_kinds(self):
+        return _batch_only_kinds(2)
+
+    def supports_axis(self, axis):
+        return axis == 0
+
+    def input_maps(self):
+        return [(0,) + (None,) * (len(self.layer.inputs[0].dims) - 1)]
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        ctx.saved["shape"] = x.shape
+        return [x.reshape(x.shape[0], -1)]
+
+    def backward(self, ctx, douts):
+        return [douts[0].reshape(ctx.saved.pop("shape"))]
+
+    def flops(self, *a):
+        return 0.0
+
+
+@register(OperatorType.OP_RESHAPE)
+class Reshape(OpImpl):
+    op_type = OperatorType.OP_RESHAPE
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        shape = list(attrs["shape"])
+        n = math.prod(in_dims[0])
+        if -1 in shape:
+            i = shape.index(-1)
+            shape[i] = n // -math.prod(shape)
+        assert math.prod(shape) == n, (shape, in_dims[0])
+        attrs["shape"] = tuple(shape)
+        return [tuple(shape)], [in_dtypes[0]], []
+
+    def _keeps_batch(self):
+        i, o = self.layer.inputs[0].dims, self.layer.outputs[0].dims
+        return i[0] == o[0]
+
+    def axis_kinds(self):
+        k = _batch_only_kinds(len(self.layer.outputs[0].dims))
+        if not self._keeps_batch():
+            k[0] = "none"
+        return k
+
+    def supports_axis(self, axis):
+        return axis == 0 and self._keeps_batch()
+
+    def input_maps(self):
+        return [(0,) + (None,) * (len(self.layer.inputs[0].dims) - 1)]
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0]
+        ctx.saved["shape"] = x.shape
+        shp = list(self.attrs["shape"])
+        shp[0] = x.shape[0] if self._keeps_batch() else shp[0]
+        return [x.reshape(shp)]
+
+    def backward(self, ctx, douts):
+        return [douts[0].reshape(ctx.saved.pop("shape"))]
+
+    def flops(self, *a):
+        return 0.0
+
+
+@register(OperatorType.OP_TRANSPOSE)
+class Transpose(OpImpl):
+    op_type = OperatorType.OP_TRANSPOSE
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        perm = tuple(attrs["perm"])
+        return [tuple(in_dims[0][p] for p in perm)], [in_dtypes[0]], []
+
+    def input_maps(self):
+        perm = self.attrs["perm"]
+        inv = [0] * len(perm)
+        for o, i in enumerate(perm):
+            inv[i] = o
+        return [tuple(inv)]
+
+    def forward(self, ctx, xs, ws):
+        return [xs[0].permute(*self.attrs["perm"]).contiguous()]
+
+    def backward(self, ctx, douts):
+        perm = self.attrs["perm"]
+        inv = [0] * len(perm)
+        for o, i in enumerate(perm):
+            inv[i] = o
+        return [douts[0].permute(*inv).contiguous()]
+
+
+@register(OperatorType.OP_CONCAT)
+class Concat(OpImpl):
+    op_type = OperatorType.OP_CONCAT
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        ax = attrs["axis"] % len(in_dims[0])
+        attrs["axis"] = ax
+        out = list(in_dims[0])
+        out[ax] = sum(d[ax] for d in in_dims)
+        return [tuple(out)], [in_dtypes[0]], []
+
+    def axis_kinds(self):
+        k = super().axis_kinds()
+        k[self.attrs["axis"]] = "none"
+        return k
+
+    def supports_axis(self, axis):
+        return axis != self.attrs["axis"]
+
+    def input_maps(self):
+        n = len(self.layer.outputs[0].dims)
+        return [tuple(range(n)) for _ in self.layer.inputs]
+
+    def forward(self, ctx, xs, ws):
+        ctx.saved["sizes"] = [x.shape[self.attrs["axis"]] for x in xs]
+        return [torch.cat(xs, self.attrs["axis"])]
+
+    def backward(self, ctx, douts):
+        return list(torch.split(douts[0], ctx.saved.pop("sizes"), self.attrs["axis"]))
+
+
+@register(OperatorType.OP_SPLIT)
+class Split(OpImpl):
+    op_type = OperatorType.OP_SPLIT
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        d = in_dims[0]
+        ax = attrs["axis"] % len(d)
+        attrs["axis"] = ax
+        sizes = attrs["sizes"]
+        if isinstance(sizes, int):
+            assert d[ax] % sizes == 0
+            sizes = [d[ax] // sizes] * sizes
+        attrs["sizes"] = list(sizes)
+        outs = []
+        for s in sizes:
+            o = list(d)
+            o[ax] = s
+            outs.append(tuple(o))
+        return outs, [in_dtypes[0]] * len(outs), []
+
+    def axis_kinds(self):
+        k = super().axis_kinds()
+        k[self.attrs["axis"]] = "none"
+        return k
+
+    def supports_axis(self, axis):
+        return axis != self.attrs["axis"]
+
+    def output_maps(self):
+        n = len(self.layer.outputs[0].dims)
+        return [tuple(range(n)) for _ in self.layer.outputs]
+
+    def forward(self, ctx, xs, ws):
+        return [t.contiguous() for t in torch.split(xs[0], self.attrs["sizes"], self.attrs["axis"])]
+
+    def backward(self, ctx, douts):
+        like = [d for d in douts if d is not None][0]
+        parts = []
+        for d, s in zip(douts, self.attrs["sizes"]):
+            if d is None:
+                shp = list(like.shape)
+                shp[self.attrs["axis"]] = s
+                d = torch.zeros(shp, dtype=like.dtype, device=like.device)
+            parts.append(d)
+        return [torch.cat(parts, self.attrs["axis"])]
+
+
+@register(OperatorType.OP_REVERSE)
+class Reverse(OpImpl):
+    op_type = OperatorType.OP_REVERSE
+
+    def axis_kinds(self):
+        k = super().axis_kinds()
+        k[self.attrs["axis"] % len(k)] = "none"
+        return k
+
+    def supports_axis(self, axis):
+        return axis != self.attrs["axis"] % len(self.layer.outputs[0].dims)
+
+    def forward(self, ctx, xs, ws):
+        return [torch.flip(xs[0], [self.attrs["axis"]])]
+
+    def backward(self, ctx, douts):
+        return [torch.flip(douts[0], [self.attrs["axis"]])]
+
+
+@register(OperatorType.OP_GATHER)
+class Gather(OpImpl):
+    """torch.gather semantics along `dim` (reference src/ops/gather.cc)."""
+    op_type = OperatorType.OP_GATHER
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        return [tuple(in_dims[1])], [in_dtypes[0]], []
+
+    def axis_kinds(self):
+        k = _batch_only_kinds(len(self.layer.outputs[0].dims))
+        if self.attrs["dim"] % len(k) == 0:
+            k[0] = "none"
+        return k
+
+    def supports_axis(self, axis):
+        return axis == 0 and self.attrs["dim"] % len(self.layer.outputs[0].dims) != 0
+
+    def input_maps(self):
+        n = len(self.layer.outputs[0].dims)
+        return [(0,) + (None,) * (len(self.layer.inputs[0].dims) - 1), (0,) + (None,) * (n - 1)]
+
+    def forward(self, ctx, xs, ws):
+        x, idx = xs
+        ctx.saved.update(shape=x.shape, idx=idx)
+        return [torch.gather(x, self.attrs["dim"], idx.long())]
+
+    def backward(self, ctx, douts):
+        shp, idx = ctx.saved.pop("shape"), ctx.saved.pop("idx")
+        dx = torch.zeros(shp, dtype=torch.float32, device=douts[0].device)
+        dx.scatter_add_(self.attrs["dim"], idx.long(), douts[0].float())
+        return [dx.to(douts[0].dtype), None]
+
+    def needs_input_grad(self, i):
+        return i == 0

@@ -1,0 +1,372 @@
+"""Explicit data movement between sharded layouts over RCCL (torch.distributed 'nccl') or gloo.
+
+This replaces the reference's implicit Legion/Realm DMA between logical-region partitions and its
+parallel-op kernels (src/parallel_ops/{partition,combine,replicate,reduction}.cc,
+src/parallel_ops/kernels/*.cu) with explicit collectives chosen per edge:
+
+    identity          same layout                                    (no-op)
+    local slice       replicated -> partitioned on the same devices  (Repartition, no comm)
+    all_gather        partitioned -> replicated                      (Combine / Replicate)
+    reduce_scatter    partial    -> partitioned                      (Reduction + Repartition)
+    all_reduce        partial    -> replicated                       (Reduction + Replicate)
+    generic P2P       anything else (placement changes, halos, uneven device sets):
+                      batched isend/irecv of exactly the overlapping blocks.
+
+and the weight-gradient synchronisation (reference: one ncclAllReduce per weight followed by an
+execution fence, src/runtime/optimizer_kernel.cu:88-94 / optimizer.cc:193) with bucketed
+all-reduces over flat fp32 gradient arenas, issued asynchronously as soon as a bucket's last
+gradient is produced so they overlap the rest of the backward pass.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .layout import Layout, TransferItem, plan_transfer, rel_slices
+
+
+def _slices(region, within):
+    return rel_slices(region, within)
+
+
+class Communicator:
+    """Owns the SPMD process-group registry. Groups are created collectively (every rank calls
+    `ensure_groups` with the same ordered list) as required by torch.distributed.new_group."""
+
+    def __init__(self, rank: int = 0, world: int = 1):
+        self.rank = rank
+        self.world = world
+        self.groups: Dict[tuple, object] = {}
+        self.backend = dist.get_backend() if (dist.is_available() and dist.is_initialized()) else None
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1 and self.backend is not None
+
+    def ensure_groups(self, rank_sets: Sequence[Sequence[int]]):
+        for rs in rank_sets:
+            key = tuple(sorted(set(rs)))
+            if len(key) <= 1 or key in self.groups:
+                continue
+            if len(key) == self.world:
+                self.groups[key] = dist.group.WORLD
+            else:
+                self.groups[key] = dist.new_group(list(key))
+
+    def group(self, ranks) -> object:
+        key = tuple(sorted(set(ranks)))
+        if len(key) == self.world:
+            return dist.group.WORLD
+        g = self.groups.get(key)
+        if g is None:
+            raise RuntimeError(f"process group {key} was not created at compile time")
+        return g
+
+    @property
+    def is_nccl(self):
+        return self.backend == "nccl"
+
+
+def _find_split_dim(a: Layout, b: Layout, factor: int) -> Optional[int]:
+    """dim d where b.degrees[d] == a.degrees[d]*factor and all other degrees equal."""
+    cand = None
+    for d, (x, y) in enumerate(zip(a.degrees, b.degrees)):
+        if x == y:
+            continue
+        if y == x * factor and cand is None:
+            cand = d
+        else:
+            return None
+    return cand
+
+
+class Transfer:
+    """A planned layout conversion for one tensor edge, executed by every rank (SPMD)."""
+
+    def __init__(self, src: Layout, dst: Layout, src_partial: bool, rank: int, elem_dtype=None):
+        self.src, self.dst, self.sp = src, dst, src_partial
+        self.rank = rank
+        self.kind = "generic"
+        self.dim = None
+        self.group_ranks: tuple = ()
+        self._classify()
+        self.items: Optional[list[TransferItem]] = None
+        if self.kind == "generic":
+            self.items = plan_transfer(src, dst, src_partial)
+
+    # ------------------------------------------------------------------ classification
+    def _classify(self):
+        S, D, sp = self.src, self.dst, self.sp
+        same_blocks = S.degrees == D.degrees
+        if not sp and same_blocks and S.replicas == D.replicas and S.devices == D.devices and S.halo == D.halo:
+            self.kind = "identity"
+            return
+        if S.halo or D.halo:
+            return
+        if sp and same_blocks and S.replicas == D.replicas:
+            ok = all(set(S.replica_group(b)) == set(D.replica_group(b)) for b in S.blocks())
+            if ok:
+                self.kind = "all_reduce"
+                return
+        if sp and D.replicas == 1 and S.replicas > 1:
+            d = _find_split_dim(S, D, S.replicas)
+            if d is not None and self._subblock_devices_match(S, D, d, S.replicas):
+                self.kind, self.dim = "reduce_scatter", d
+                return
+        if not sp and S.replicas == 1 and D.replicas > 1:
+            d = _find_split_dim(D, S, D.replicas)
+            if d is not None and self._subblock_devices_match(D, S, d, D.replicas):
+                self.kind, self.dim = "all_gather", d
+                return
+        if not sp and S.replicas > 1 and D.replicas == 1:
+            d = _find_split_dim(S, D, S.replicas)
+            if d is not None and self._subblock_devices_match(S, D, d, S.replicas, subset=True):
+                self.kind, self.dim = "local_slice", d
+                return
+
+    @staticmethod
+    def _subblock_devices_match(coarse: Layout, fine: Layout, d: int, k: int, subset=False) -> bool:
+        """Each coarse block's replica devices == devices of its k fine sub-blocks along dim d."""
+        for blk in coarse.blocks():
+            rep_devs = set(coarse.replica_group(blk))
+            sub = []
+            for j in range(k):
+                fb = list(blk)
+                fb[d] = blk[d] * k + j
+                sub.append(fine.devices[fine.part_index(fb, 0)])
+            if subset:
+                if not set(sub) <= rep_devs or len(set(sub)) != k:
+                    return False
+            elif set(sub) != rep_devs or len(rep_devs) != k:
+                return False
+        return True
+
+    def rank_sets(self) -> list[tuple]:
+        """Process groups this transfer needs (for collective creation at compile time)."""
+        out = []
+        if self.kind == "all_reduce":
+            for b in self.src.blocks():
+                out.append(tuple(sorted(self.src.replica_group(b))))
+        elif self.kind == "reduce_scatter":
+            for b in self.src.blocks():
+                out.append(tuple(sorted(self.src.replica_group(b))))
+        elif self.kind == "all_gather":
+            for b in self.dst.blocks():
+                out.append(tuple(sorted(self.dst.replica_group(b))))
+        return out
+
+    def bytes_moved(self, elem_bytes: int) -> int:
+        """Bytes sent by this rank (cost accounting / tracing)."""
+        S = self.src
+        loc = S.parts_on(self.rank)
+        if not loc:
+            return 0
+        n = 1
+        for s in S.local_shape(loc[0]):
+            n *= s
+        if self.kind in ("identity", "local_slice"):
+            return 0
+        if self.kind == "all_reduce":
+            r = S.replicas
+            return int(2 * (r - 1) / r * n * elem_bytes)
+        if self.kind == "reduce_scatter":
+            r = S.replicas
+            return int((r - 1) / r * n * elem_bytes)
+        if self.kind == "all_gather":
+            return int((self.dst.replicas - 1) * n * elem_bytes)
+        tot = 0
+        for it in self.items or []:
+            if S.devices[it.src_part] == self.rank and self.dst.devices[it.dst_part] != self.rank:
+                m = 1
+                for lo, hi in it.region:
+                    m *= hi - lo
+                tot += m * elem_bytes
+        return tot
+
+    # ------------------------------------------------------------------ execution
+    def run(self, comm: Communicator, x: Optional[torch.Tensor], like: Optional[torch.Tensor] = None):
+        """x: this rank's src part (or None). Returns this rank's dst part (or None)."""
+        S, D, r = self.src, self.dst, self.rank
+        dparts = D.parts_on(r)
+        sparts = S.parts_on(r)
+        if self.kind == "identity":
+            return x
+        if self.kind == "local_slice":
+            if not dparts:
+                return None
+            q = dparts[0]
+            return x[_slices(D.region(q), S.region(sparts[0]))].contiguous()
+        if self.kind == "all_reduce":
+            if x is None:
+                return None
+            grp = tuple(sorted(S.replica_group(S.coords(sparts[0])[0])))
+            y = x.contiguous().clone() if not x.is_contiguous() else x
+            if len(grp) > 1:
+                dist.all_reduce(y, group=comm.group(grp))
+            return y
+        if self.kind == "reduce_scatter":
+            if x is None:
+                return None
+            return self._reduce_scatter(comm, x)
+        if self.kind == "all_gather":
+            return self._all_gather(comm, x) if (x is not None or dparts) else None
+        return self._generic(comm, x, like)
+
+    def _reduce_scatter(self, comm, x):
+        S, D, d, r = self.src, self.dst, self.dim, self.rank
+        blk, _ = S.coords(S.parts_on(r)[0])
+        k = S.replicas
+        grp = sorted(S.replica_group(blk))
+        # order of fine sub-blocks by group rank
+        sub_dev = []
+        for j in range(k):
+            fb = list(blk)
+            fb[d] = blk[d] * k + j
+            sub_dev.append(D.devices[D.part_index(fb, 0)])
+        xm = x.movedim(d, 0)
+        chunks = list(xm.chunk(k, 0))
+        order = [sub_dev.index(g) for g in grp]  # chunk for group-rank i
+        inp = torch.cat([chunks[j] for j in order], 0).contiguous() if order != list(range(k)) else xm.contiguous()
+        out_shape = list(inp.shape)
+        out_shape[0] //= k
+        out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
+        g = comm.group(grp)
+        if comm.is_nccl:
+            dist.reduce_scatter_tensor(out, inp, group=g)
+        else:  # gloo: no reduce_scatter; all_reduce then keep own chunk
+            tmp = inp.clone()
+            dist.all_reduce(tmp, group=g)
+            out.copy_(tmp.chunk(k, 0)[grp.index(r)])
+        return out.movedim(0, d).contiguous()
+
+    def _all_gather(self, comm, x):
+        S, D, d, r = self.src, self.dst, self.dim, self.rank
+        k = D.replicas
+        qblk, _ = D.coords(D.parts_on(r)[0])
+        grp = sorted(D.replica_group(qblk))
+        sub_dev = []
+        for j in range(k):
+            fb = list(qblk)
+            fb[d] = qblk[d] * k + j
+            sub_dev.append(S.devices[S.part_index(fb, 0)])
+        xm = x.movedim(d, 0).contiguous()
+        g = comm.group(grp)
+        if comm.is_nccl:
+            out = torch.empty((k * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
+            dist.all_gather_into_tensor(out, xm, group=g)
+            chunks = list(out.chunk(k, 0))
+        else:
+            chunks = [torch.empty_like(xm) for _ in range(k)]
+            dist.all_gather(chunks, xm, group=g)
+        # chunks[i] came from group-rank i == device grp[i]; reorder to dim order
+        ordered = [chunks[grp.index(dev)] for dev in sub_dev]
+        return torch.cat(ordered, 0).movedim(0, d).contiguous()
+
+    def _generic(self, comm, x, like):
+        S, D, r = self.src, self.dst, self.rank
+        dparts = D.parts_on(r)
+        sparts = S.parts_on(r)
+        ref = x if x is not None else like
+        out = None
+        if dparts:
+            q = dparts[0]
+            out = torch.zeros(D.local_shape(q), dtype=ref.dtype, device=ref.device)
+        ops = []
+        pending = []
+        for it in self.items:
+            sd, dd = S.devices[it.src_part], D.devices[it.dst_part]
+            if sd != r and dd != r:
+                continue
+            if sd == r and dd == r:
+                src_view = x[_slices(it.region, S.region(it.src_part))]
+                dst_view = out[_slices(it.region, D.region(it.dst_part))]
+                if it.reduce:
+                    dst_view.add_(src_view)
+                else:
+                    dst_view.copy_(src_view)
+            elif sd == r:
+                buf = x[_slices(it.region, S.region(it.src_part))].contiguous()
+                ops.append(dist.P2POp(dist.isend, buf, dd))
+                pending.append(("send", buf, None, None))
+            else:
+                shp = tuple(hi - lo for lo, hi in it.region)
+                buf = torch.empty(shp, dtype=ref.dtype, device=ref.device)
+                ops.append(dist.P2POp(dist.irecv, buf, sd))
+                pending.append(("recv", buf, it, None))
+        if ops:
+            reqs = dist.batch_isend_irecv(ops)
+            for q in reqs:
+                q.wait()
+        for kind, buf, it, _ in pending:
+            if kind == "recv":
+                dst_view = out[_slices(it.region, D.region(it.dst_part))]
+                if it.reduce:
+                    dst_view.add_(buf)
+                else:
+                    dst_view.copy_(buf)
+        return out
+
+
+class GradBucketer:
+    """Bucketed, backward-overlapped gradient all-reduce over flat fp32 arenas.
+
+    Each arena holds the gradients of all weight shards that share one replica group (e.g. every
+    data-parallel weight); buckets are contiguous slices in reverse forward order so the first
+    bucket completes early in the backward pass. Bucket size is chosen for xGMI ring all-reduce
+    (config.grad_bucket_mb, default 64 MiB: few, large collectives).
+    """
+
+    def __init__(self, comm: Communicator, bucket_bytes: int):
+        self.comm = comm
+        self.bucket_bytes = bucket_bytes
+        self.arenas = []  # (group_ranks, flat_grad, [buckets]) ; bucket = dict(lo, hi, params:set, ready:set)
+        self.param_bucket = {}
+        self.handles = []
+
+    def add_arena(self, group_ranks, flat, segments):
+        """segments: list of (param_key, lo, hi) in gradient-completion order."""
+        buckets = []
+        cur = None
+        for key, lo, hi in segments:
+            if cur is None or (cur["hi"] - cur["lo"]) * 4 >= self.bucket_bytes:
+                cur = dict(lo=lo, hi=hi, params=set(), ready=set(), flat=flat, group=group_ranks)
+                buckets.append(cur)
+            cur["lo"] = min(cur["lo"], lo)
+            cur["hi"] = max(cur["hi"], hi)
+            cur["params"].add(key)
+            self.param_bucket[key] = cur
+        self.arenas.append((group_ranks, flat, buckets))
+
+    def reset(self):
+        for _, _, buckets in self.arenas:
+            for b in buckets:
+                b["ready"] = set()
+        self.handles = []
+
+    def mark_ready(self, key):
+        b = self.param_bucket.get(key)
+        if b is None:
+            return
+        b["ready"].add(key)
+        if len(b["ready"]) == len(b["params"]):
+            self._launch(b)
+
+    def _launch(self, b):
+        if len(b["group"]) <= 1 or not self.comm.distributed:
+            return
+        view = b["flat"][b["lo"]:b["hi"]]
+        h = dist.all_reduce(view, group=self.comm.group(b["group"]), async_op=True)
+        self.handles.append(h)
+
+    def flush(self):
+        for _, _, buckets in self.arenas:
+            for b in buckets:
+                if len(b["ready"]) != len(b["params"]):
+                    self._launch(b)
+                    b["ready"] = set(b["params"])
+        for h in self.handles:
+            h.wait()
+        self.handles = []

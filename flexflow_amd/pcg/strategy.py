@@ -1,0 +1,192 @@
+"""Parallelization strategies: per-op parallel configs, their tensor layouts, and strategy files.
+
+An `OpConfig` assigns a degree to every parallel axis of an op (its output dims + op-specific
+reduction axes, see ops/base.py) and a device for every part — the reference's
+ParallelConfig/MachineView pair (include/flexflow/machine_view.h, parallel_tensor.h). From it the
+layouts of every input requirement, weight shard and output follow mechanically
+(`op_layouts`), which is what both the executor and the cost model consume.
+
+Strategy files are JSON (`{"version": 1, "num_devices": N, "ops": {layer_name: {"degrees": [...],
+"devices": [...]}}}`), written by `--export-strategy` and read by `--import-strategy` — the
+reference parses these flags but never uses them (model.cc:2812-2815); here they round-trip.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from ..parallel.layout import Layout
+from ..type import OperatorType
+
+
+@dataclass(frozen=True)
+class OpConfig:
+    degrees: Tuple[int, ...]
+    devices: Tuple[int, ...]
+
+    @property
+    def num_parts(self) -> int:
+        return int(math.prod(self.degrees))
+
+    def coords(self, p: int) -> Tuple[int, ...]:
+        cs = []
+        for d in reversed(self.degrees):
+            cs.append(p % d)
+            p //= d
+        return tuple(reversed(cs))
+
+    def part(self, coords: Sequence[int]) -> int:
+        p = 0
+        for c, d in zip(coords, self.degrees):
+            p = p * d + c
+        return p
+
+    def to_json(self):
+        return {"degrees": list(self.degrees), "devices": list(self.devices)}
+
+    @staticmethod
+    def from_json(d):
+        return OpConfig(tuple(d["degrees"]), tuple(d["devices"]))
+
+
+def tensor_layout(shape, dim_axes, cfg: OpConfig, partial_axes=(), halo=None) -> Layout:
+    """Layout of a tensor whose dim i is partitioned along op axis dim_axes[i] (None = whole).
+    Op axes with degree > 1 that the tensor does not map become its replica dims (in axis order)."""
+    nax = len(cfg.degrees)
+    mapped = [a for a in dim_axes if a is not None]
+    degrees = tuple(cfg.degrees[a] if a is not None else 1 for a in dim_axes)
+    rep_axes = [a for a in range(nax) if a not in mapped and cfg.degrees[a] > 1]
+    replicas = int(math.prod(cfg.degrees[a] for a in rep_axes)) if rep_axes else 1
+    nblocks = int(math.prod(degrees))
+    devices = [0] * (nblocks * replicas)
+    for p in range(cfg.num_parts):
+        c = cfg.coords(p)
+        block = [c[a] if a is not None else 0 for a in dim_axes]
+        r = 0
+        for a in rep_axes:
+            r = r * cfg.degrees[a] + c[a]
+        b = 0
+        for bc, d in zip(block, degrees):
+            b = b * d + bc
+        devices[b * replicas + r] = cfg.devices[p]
+    partial = bool(partial_axes) and any(cfg.degrees[a] > 1 for a in partial_axes)
+    if partial:
+        assert set(rep_axes) <= set(partial_axes), "outputs may only be replicated over partial-sum axes"
+    return Layout(tuple(shape), degrees, replicas, tuple(devices), partial, halo)
+
+
+@dataclass
+class OpLayouts:
+    inputs: List[Layout]
+    weights: List[Layout]
+    outputs: List[Layout]
+
+
+def op_layouts(layer, cfg: OpConfig) -> OpLayouts:
+    impl = layer.impl
+    ins = []
+    for i, (t, m) in enumerate(zip(layer.inputs, impl.input_maps())):
+        halo = impl.input_halo(i, cfg.degrees) if len(cfg.degrees) > 0 else None
+        if halo is not None and not any(halo):
+            halo = None
+        ins.append(tensor_layout(t.dims, m, cfg, halo=halo))
+    ws = [tensor_layout(w.dims, m, cfg) for w, m in zip(layer.weights, impl.weight_maps())]
+    pax = impl.partial_axes()
+    outs = [tensor_layout(o.dims, m, cfg, partial_axes=pax) for o, m in zip(layer.outputs, impl.output_maps())]
+    return OpLayouts(ins, ws, outs)
+
+
+def valid_config(layer, cfg: OpConfig) -> bool:
+    impl = layer.impl
+    sizes = impl.axis_sizes()
+    if len(cfg.degrees) != len(sizes) or len(cfg.devices) != cfg.num_parts:
+        return False
+    if len(set(cfg.devices)) != len(cfg.devices):
+        return False
+    kinds = impl.axis_kinds()
+    for a, (d, s) in enumerate(zip(cfg.degrees, sizes)):
+        if d == 1:
+            continue
+        if s % d != 0 or kinds[a] == "none" or not impl.supports_axis(a):
+            return False
+    # every tensor dim must divide
+    try:
+        op_layouts(layer, cfg)
+    except AssertionError:
+        return False
+    return True
+
+
+def divisors(n: int) -> List[int]:
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute", "parameter"),
+                      max_configs: int = 64, contiguous_starts: bool = True) -> List[OpConfig]:
+    """Candidate parallelizations of one op: degree combos over its allowed axes whose product
+    divides the device count, placed on aligned contiguous device blocks (reference
+    register_all_machine_views: 1-D views `i | N`, graph.cc:2329-2360)."""
+    impl = layer.impl
+    sizes = impl.axis_sizes()
+    kinds = impl.axis_kinds()
+    axes = [a for a, k in enumerate(kinds) if k in allow_kinds and impl.supports_axis(a)]
+    out: List[OpConfig] = []
+    degs = [1] * len(sizes)
+
+    def rec(i, prod):
+        if i == len(axes):
+            P = prod
+            starts = range(0, num_devices, P) if contiguous_starts else [0]
+            for st in starts:
+                if st + P > num_devices:
+                    continue
+                cfg = OpConfig(tuple(degs), tuple(range(st, st + P)))
+                if valid_config(layer, cfg):
+                    out.append(cfg)
+            return
+        a = axes[i]
+        for d in divisors(num_devices // prod):
+            if sizes[a] % d:
+                continue
+            degs[a] = d
+            rec(i + 1, prod * d)
+        degs[a] = 1
+
+    rec(0, 1)
+    # prefer configs using more devices first; cap the list
+    out.sort(key=lambda c: (-c.num_parts, c.devices[0], c.degrees))
+    return out[:max_configs]
+
+
+def data_parallel_config(layer, num_devices: int) -> OpConfig:
+    """Reference --only-data-parallel: partition the sample dim over all devices when legal,
+    otherwise run the op on device 0 (degree 1)."""
+    sizes = layer.impl.axis_sizes()
+    n = len(sizes)
+    for d in sorted(divisors(num_devices), reverse=True):
+        degs = [1] * n
+        degs[0] = d
+        cfg = OpConfig(tuple(degs), tuple(range(d)))
+        if layer.impl.axis_kinds()[0] == "sample" and valid_config(layer, cfg):
+            return cfg
+    return OpConfig(tuple([1] * n), (0,))
+
+
+def data_parallel_strategy(layers, num_devices: int) -> Dict[str, OpConfig]:
+    return {l.name: data_parallel_config(l, num_devices) for l in layers}
+
+
+def save_strategy(path: str, strategy: Dict[str, OpConfig], num_devices: int, extra: Optional[dict] = None):
+    doc = {"version": 1, "num_devices": num_devices, "ops": {k: v.to_json() for k, v in strategy.items()}}
+    if extra:
+        doc.update(extra)
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+def load_strategy(path: str) -> Tuple[Dict[str, OpConfig], int]:
+    with open(path) as f:
+        doc = json.load(f)
+    return {k: OpConfig.from_json(v) for k, v in doc["ops"].items()}, int(doc.get("num_devices", 1))

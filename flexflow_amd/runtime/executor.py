@@ -1,0 +1,495 @@
+"""Per-rank SPMD executor (replaces the reference's Legion index-task launches, mapper and
+region-based data movement: FFModel::forward/backward/update, model.cc:2401-2474, and
+FFMapper, src/mapper/mapper.cc).
+
+Every rank runs the same program: for each op in topological order, the edge transfers that
+bring its inputs into the layouts its parallel config requires (collectives over RCCL), then —
+iff the rank owns a part of the op — the op's HIP kernels on its local shards. The backward pass
+mirrors it with the dual transfers; weight gradients land in flat fp32 arenas whose buckets are
+all-reduced asynchronously as they complete (overlapping the rest of the backward), and `update`
+applies one fused optimizer kernel per arena.
+
+Static, step-invariant structure (layouts, transfers, process groups, weight arenas, input
+staging buffers) is built once in `__init__`, so a whole forward+backward step can be captured
+into a hipGraph (runtime/graph.py) when the strategy has no in-step collectives.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import kernels as K
+from ..ops import OpCtx, torch_dtype
+from ..parallel.comm import Communicator, GradBucketer, Transfer
+from ..parallel.layout import Layout, rel_slices
+from ..pcg.strategy import OpConfig, op_layouts
+from ..type import DataType, LossType, MetricsType, OperatorType
+
+
+class WeightArena:
+    """Flat storage for all local weight shards sharing one replica (gradient-sync) group."""
+
+    def __init__(self, group: tuple, device, lowp_dtype):
+        self.group = group
+        self.device = device
+        self.lowp_dtype = lowp_dtype
+        self.entries = []  # (param, offset, numel, shape)
+        self.size = 0
+        self.master = self.grad = self.lowp = None
+
+    def add(self, param, shape):
+        n = int(math.prod(shape))
+        # 16-byte align every shard so vector kernels / GEMM operand loads stay aligned
+        self.entries.append((param, self.size, n, tuple(shape)))
+        self.size += (n + 7) // 8 * 8
+
+    def materialize(self):
+        self.master = torch.zeros(max(self.size, 8), dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros_like(self.master)
+        if self.lowp_dtype is not None:
+            self.lowp = torch.zeros(max(self.size, 8), dtype=self.lowp_dtype, device=self.device)
+
+    def views(self, i):
+        _, off, n, shape = self.entries[i]
+        m = self.master[off:off + n].view(shape)
+        g = self.grad[off:off + n].view(shape)
+        c = self.lowp[off:off + n].view(shape) if self.lowp is not None else m
+        return m, g, c
+
+
+def _device_for(config):
+    if torch.cuda.is_available():
+        return torch.device("cuda", config.local_rank % max(1, torch.cuda.device_count()))
+    return torch.device("cpu")
+
+
+class Executor:
+    def __init__(self, model, strategy: Dict[str, OpConfig], loss_type: Optional[LossType], metrics, training=True):
+        self.model = model
+        cfg = model.config
+        self.config = cfg
+        self.rank, self.world = cfg.rank, cfg.world_size
+        self.device = _device_for(cfg)
+        self.training = training
+        self.cdt = DataType.DT_BF16 if cfg.compute_dtype == DataType.DT_BF16 else DataType.DT_FLOAT
+        self.ctorch = torch.bfloat16 if self.cdt == DataType.DT_BF16 else torch.float32
+        self.layers = list(model.layers)
+        self.strategy = strategy
+        self.loss_type = loss_type
+        self.metrics = list(metrics or [])
+        self.step_idx = 0
+        self.comm = Communicator(self.rank, self.world)
+
+        self.lay = {L.name: op_layouts(L, strategy[L.name]) for L in self.layers}
+        self.local: Dict[str, bool] = {}
+        self.ctx: Dict[str, OpCtx] = {}
+        for L in self.layers:
+            scfg = strategy[L.name]
+            mine = [p for p, d in enumerate(scfg.devices) if d == self.rank]
+            self.local[L.name] = bool(mine)
+            if mine:
+                self.ctx[L.name] = OpCtx(layer=L, part_coords=scfg.coords(mine[0]), degrees=scfg.degrees,
+                                         compute_dtype=self.cdt, training=training, seed=cfg.seed)
+        self.producer_layout: Dict[int, Layout] = {}
+        for L in self.layers:
+            for o, lo in zip(L.outputs, self.lay[L.name].outputs):
+                self.producer_layout[o.guid] = lo
+
+        # model output / loss plumbing
+        self.output_tensor = model.output_tensor()
+        self._build_grad_reachability()
+        self._build_transfers()
+        self._alloc_weights()
+        self._setup_loss()
+        self.values: Dict[int, Optional[torch.Tensor]] = {}
+        self.inputs: Dict[int, torch.Tensor] = {}
+        self._metric_acc = torch.zeros(8, dtype=torch.float32, device=self.device)
+        self.last_loss = None
+        self.comm.ensure_groups(self._rank_sets)
+
+    # ------------------------------------------------------------------ static analysis
+    def _build_grad_reachability(self):
+        need = {self.output_tensor.guid} if self.output_tensor is not None else set()
+        self.layer_bwd: Dict[str, bool] = {}
+        for L in reversed(self.layers):
+            nb = any(o.guid in need for o in L.outputs) and L.op_type != OperatorType.OP_INPUT
+            self.layer_bwd[L.name] = nb and self.training
+            if nb:
+                for j, t in enumerate(L.inputs):
+                    if L.impl.needs_input_grad(j) and t.data_type in (DataType.DT_FLOAT, DataType.DT_HALF,
+                                                                        DataType.DT_DOUBLE, DataType.DT_BF16):
+                        need.add(t.guid)
+        self.tensor_needs_grad = need
+        # a grad only has to flow into an input whose producer (or its ancestors) owns weights
+        has_w = set()
+        for L in self.layers:
+            if L.weights or any(t.guid in has_w for t in L.inputs):
+                for o in L.outputs:
+                    has_w.add(o.guid)
+        self.grad_useful = has_w
+
+    def _build_transfers(self):
+        self.fwd_tx: Dict[Tuple[str, int], Transfer] = {}
+        self.bwd_tx: Dict[Tuple[str, int], Transfer] = {}
+        self.in_grad: Dict[Tuple[str, int], bool] = {}
+        rank_sets = []
+        for L in self.layers:
+            if L.op_type == OperatorType.OP_INPUT:
+                continue
+            for j, t in enumerate(L.inputs):
+                src = self.producer_layout[t.guid]
+                dst = self.lay[L.name].inputs[j]
+                tx = Transfer(src, dst, src.partial, self.rank)
+                self.fwd_tx[(L.name, j)] = tx
+                rank_sets += tx.rank_sets()
+                ig = (self.layer_bwd[L.name] and t.guid in self.tensor_needs_grad and t.guid in self.grad_useful
+                      and L.impl.needs_input_grad(j))
+                self.in_grad[(L.name, j)] = ig
+                if ig:
+                    btx = Transfer(dst.with_(partial=False), src.with_(partial=False),
+                                   dst.replicas > 1 or dst.halo is not None, self.rank)
+                    self.bwd_tx[(L.name, j)] = btx
+                    rank_sets += btx.rank_sets()
+            if L.name in self.ctx:
+                # first Linear-like ops whose input needs no grad skip the dgrad GEMM
+                self.ctx[L.name].extra["need_dx0"] = bool(L.inputs) and self.in_grad.get((L.name, 0), False)
+                lo = self.lay[L.name]
+                if lo.inputs:
+                    p = lo.inputs[0].parts_on(self.rank)
+                    if p:
+                        self.ctx[L.name].extra["in_region0"] = lo.inputs[0].region(p[0])
+                if lo.outputs:
+                    p = lo.outputs[0].parts_on(self.rank)
+                    if p:
+                        self.ctx[L.name].extra["out_region"] = lo.outputs[0].region(p[0])
+        self._rank_sets = rank_sets
+
+    def _alloc_weights(self):
+        lowp = torch.bfloat16 if self.cdt == DataType.DT_BF16 else None
+        self.arenas: Dict[tuple, WeightArena] = {}
+        self.weight_loc: Dict[int, Tuple[WeightArena, int]] = {}
+        self.weight_layout: Dict[int, Layout] = {}
+        self.weight_users: Dict[int, int] = {}
+        for L in self.layers:
+            for w in L.weights:
+                if self.layer_bwd.get(L.name) and self.local.get(L.name):
+                    self.weight_users[w.guid] = self.weight_users.get(w.guid, 0) + 1
+        for L in reversed(self.layers):  # backward completion order
+            for w, wl in zip(L.weights, self.lay[L.name].weights):
+                if w.guid in self.weight_layout:  # shared weight (shared_op): allocated once
+                    assert self.weight_layout[w.guid].key() == wl.key(), "shared weights need equal layouts"
+                    continue
+                self.weight_layout[w.guid] = wl
+                parts = wl.parts_on(self.rank)
+                if not parts:
+                    continue
+                p = parts[0]
+                grp = tuple(sorted(wl.replica_group(wl.coords(p)[0])))
+                ar = self.arenas.setdefault(grp, WeightArena(grp, self.device, lowp))
+                ar.add(w, wl.local_shape(p))
+                self.weight_loc[w.guid] = (ar, len(ar.entries) - 1)
+        for ar in self.arenas.values():
+            ar.materialize()
+        self._rank_sets += [g for g in self.arenas.keys()]
+        bucket_bytes = int(self.config.grad_bucket_mb * (1 << 20))
+        self.bucketer = GradBucketer(self.comm, bucket_bytes)
+        for grp, ar in self.arenas.items():
+            segs = [(w.guid, off, off + n) for (w, off, n, _) in ar.entries]
+            self.bucketer.add_arena(grp, ar.grad, segs)
+        for L in self.layers:
+            if L.name in self.ctx:
+                self.ctx[L.name].wgrads = [self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]
+                                           if w.guid in self.weight_loc else None for w in L.weights]
+
+    def init_weights(self, seed_base: int):
+        """Deterministic global init, each rank keeping its shard."""
+        from ..core.initializers import default_initializer
+        for L in self.layers:
+            for i, w in enumerate(L.weights):
+                if w.guid not in self.weight_loc:
+                    continue
+                ar, idx = self.weight_loc[w.guid]
+                m, _, c = ar.views(idx)
+                init = w.initializer or default_initializer(getattr(w, "short_name", w.name), seed_base + w.guid)
+                full = torch.empty(w.dims, dtype=torch.float32, device=self.device)
+                init.fill_full(full, w.dims)
+                wl = self.weight_layout[w.guid]
+                p = wl.parts_on(self.rank)[0]
+                m.copy_(full[rel_slices(wl.region(p), tuple((0, s) for s in w.dims))])
+                if c is not m:
+                    c.copy_(m)
+
+    def weight_tensor(self, w):
+        ar, idx = self.weight_loc[w.guid]
+        return ar.views(idx)[2]
+
+    # ------------------------------------------------------------------ loss
+    def _setup_loss(self):
+        self.loss_layout = None
+        self.label_layout = None
+        out = self.output_tensor
+        if out is None or self.loss_type is None:
+            return
+        pl = self.producer_layout[out.guid]
+        d0 = pl.degrees[0]
+        devs = []
+        for b in range(d0):
+            blk = [b] + [0] * (pl.ndim - 1)
+            devs.append(pl.devices[pl.part_index(blk, 0)])
+        self.loss_layout = Layout(pl.shape, (d0,) + (1,) * (pl.ndim - 1), 1, tuple(devs))
+        lab = self.model.label_tensor
+        self.label_layout = Layout(tuple(lab.dims), (d0,) + (1,) * (len(lab.dims) - 1), 1, tuple(devs))
+        self.loss_fwd_tx = Transfer(pl, self.loss_layout, pl.partial, self.rank)
+        self.loss_bwd_tx = Transfer(self.loss_layout, pl.with_(partial=False), False, self.rank)
+        self._rank_sets += self.loss_fwd_tx.rank_sets() + self.loss_bwd_tx.rank_sets()
+        owner = out.owner_layer
+        self.softmax_fused = (owner.op_type == OperatorType.OP_SOFTMAX and self.loss_type in (
+            LossType.LOSS_CATEGORICAL_CROSSENTROPY, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY))
+        if self.softmax_fused and owner.name in self.ctx:
+            self.ctx[owner.name].extra["loss_fused"] = True
+
+    # ------------------------------------------------------------------ inputs
+    def input_layout(self, t) -> Layout:
+        if t.guid in self.producer_layout:
+            return self.producer_layout[t.guid]
+        if self.model.label_tensor is not None and t.guid == self.model.label_tensor.guid:
+            return self.label_layout
+        raise KeyError(t)
+
+    def feed(self, t, value):
+        """Stage the global value of an input/label tensor: keep this rank's shard in a persistent
+        device buffer (stable address for graph replay)."""
+        lay = self.input_layout(t)
+        parts = lay.parts_on(self.rank)
+        if not parts:
+            return
+        reg = lay.region(parts[0])
+        full = tuple((0, s) for s in lay.shape)
+        if isinstance(value, np.ndarray):
+            src = torch.from_numpy(np.ascontiguousarray(value[rel_slices(reg, full)]))
+        else:
+            src = value[rel_slices(reg, full)]
+        is_float = t.data_type in (DataType.DT_FLOAT, DataType.DT_HALF, DataType.DT_DOUBLE, DataType.DT_BF16)
+        dt = self.ctorch if is_float else torch_dtype(t.data_type)
+        buf = self.inputs.get(t.guid)
+        if buf is None or tuple(buf.shape) != tuple(src.shape) or buf.dtype != dt:
+            buf = torch.empty(tuple(src.shape), dtype=dt, device=self.device)
+            self.inputs[t.guid] = buf
+        if src.device.type == "cpu" and self.device.type == "cuda":
+            src = src.pin_memory() if not src.is_pinned() else src
+            buf.copy_(src.to(dt) if src.dtype != dt and not is_float else src, non_blocking=True)
+        else:
+            buf.copy_(src)
+
+    # ------------------------------------------------------------------ execution
+    def _like(self, t):
+        is_float = t.data_type in (DataType.DT_FLOAT, DataType.DT_HALF, DataType.DT_DOUBLE, DataType.DT_BF16)
+        return torch.empty(0, dtype=self.ctorch if is_float else torch_dtype(t.data_type), device=self.device)
+
+    def forward(self, training: Optional[bool] = None):
+        tr = self.training if training is None else training
+        vals = self.values
+        for L in self.layers:
+            if L.op_type == OperatorType.OP_INPUT:
+                o = L.outputs[0]
+                vals[o.guid] = self.inputs.get(o.guid) if self.local[L.name] else None
+                continue
+            xs, cache = [], {}
+            for j, t in enumerate(L.inputs):
+                key = (t.guid, self.lay[L.name].inputs[j].key())
+                if key not in cache:
+                    cache[key] = self.fwd_tx[(L.name, j)].run(self.comm, vals.get(t.guid), self._like(t))
+                xs.append(cache[key])
+            if self.local[L.name]:
+                ctx = self.ctx[L.name]
+                ctx.training = tr
+                ctx.step = self.step_idx
+                ws = [self.weight_tensor(w) for w in L.weights]
+                outs = L.impl.forward(ctx, xs, ws)
+                for o, v in zip(L.outputs, outs):
+                    vals[o.guid] = v
+            else:
+                for o in L.outputs:
+                    vals[o.guid] = None
+
+    def compute_loss_grad(self):
+        """Loss gradient w.r.t. the model output (reference Loss::backward, scale 1/batch or
+        2/volume for MSE-avg), seeded in the producer's layout."""
+        out = self.output_tensor
+        v = self.loss_fwd_tx.run(self.comm, self.values.get(out.guid), self._like(out))
+        g = None
+        if v is not None:
+            lt = self.loss_type
+            B = out.dims[0]
+            lab = self.inputs.get(self.model.label_tensor.guid)
+            rows = v.reshape(v.shape[0], -1) if lt != LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY else \
+                v.reshape(-1, v.shape[-1])
+            if lt == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
+                labels = lab.reshape(-1).to(torch.int32)
+                if self.softmax_fused:
+                    g, lrow = K.xent_grad(rows.contiguous(), labels, None, 1.0 / B, True)
+                else:
+                    g, lrow = K.softmax_xent(rows.contiguous(), labels, 1.0 / B)
+                self._metric_acc[0] += lrow.sum()
+            elif lt == LossType.LOSS_CATEGORICAL_CROSSENTROPY:
+                oh = lab.reshape(rows.shape).to(rows.dtype)
+                if self.softmax_fused:
+                    g, lrow = K.xent_grad(rows.contiguous(), None, oh, 1.0 / B, False)
+                else:
+                    g = ((torch.softmax(rows.float(), -1) - oh.float()) / B).to(rows.dtype)
+                    lrow = -(oh.float() * torch.log_softmax(rows.float(), -1)).sum(-1)
+                self._metric_acc[0] += lrow.sum()
+            elif lt in (LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE, LossType.LOSS_MEAN_SQUARED_ERROR_SUM_REDUCE):
+                vol = math.prod(out.dims)
+                sc = 2.0 / vol if lt == LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE else 1.0 / B
+                g, l2 = K.mse_grad(v.contiguous(), lab.reshape(v.shape), sc)
+                self._metric_acc[0] += l2.sum()
+            else:  # identity
+                g = torch.full_like(v, 1.0 / B)
+                self._metric_acc[0] += v.float().sum()
+            g = g.reshape(v.shape)
+            self._metric_acc[7] += v.shape[0]
+            self._accumulate_metrics(v, lab)
+        return self.loss_bwd_tx.run(self.comm, g, self._like(out))
+
+    def _accumulate_metrics(self, v, lab):
+        mets = set(self.metrics)
+        if not mets:
+            return
+        lt = self.loss_type
+        if MetricsType.METRICS_ACCURACY in mets or MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY in mets \
+                or MetricsType.METRICS_CATEGORICAL_CROSSENTROPY in mets:
+            rows = v.reshape(-1, v.shape[-1])
+            if lt == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
+                labels = lab.reshape(-1).to(torch.int32)
+            elif lab.shape[-1] == v.shape[-1] and v.shape[-1] > 1:
+                labels = lab.reshape(rows.shape).float().argmax(-1).to(torch.int32)
+            else:
+                labels = None
+            if labels is not None and rows.shape[0] == labels.shape[0]:
+                probs = rows if self.softmax_fused else torch.softmax(rows.float(), -1).to(rows.dtype)
+                acc3 = torch.zeros(3, dtype=torch.float32, device=v.device)
+                K.metrics_classify(probs.contiguous(), labels, acc3)
+                self._metric_acc[1] += acc3[0]
+                self._metric_acc[2] += acc3[1]
+                self._metric_acc[3] += acc3[2]
+        if MetricsType.METRICS_MEAN_SQUARED_ERROR in mets or MetricsType.METRICS_ROOT_MEAN_SQUARED_ERROR in mets \
+                or MetricsType.METRICS_MEAN_ABSOLUTE_ERROR in mets:
+            if lab.numel() == v.numel():
+                d = v.float() - lab.reshape(v.shape).float()
+                self._metric_acc[4] += (d * d).sum()
+                self._metric_acc[5] += d.abs().sum()
+                self._metric_acc[6] += d.numel()
+
+    def backward(self):
+        self.bucketer.reset()
+        self._wdone = {}
+        grads: Dict[int, torch.Tensor] = {}
+        if self.output_tensor is not None and self.loss_type is not None:
+            g = self.compute_loss_grad()
+            if g is not None:
+                grads[self.output_tensor.guid] = g
+        for L in reversed(self.layers):
+            if not self.layer_bwd.get(L.name):
+                continue
+            dxs = None
+            if self.local[L.name]:
+                douts = [grads.pop(o.guid, None) for o in L.outputs]
+                if any(d is not None for d in douts):
+                    ref = [d for d in douts if d is not None][0]
+                    vals = [self.values.get(o.guid) for o in L.outputs]
+                    douts = [d if d is not None else (torch.zeros_like(v) if v is not None else None)
+                             for d, v in zip(douts, vals)]
+                    dxs = L.impl.backward(self.ctx[L.name], douts)
+                for w in L.weights:
+                    self._wdone[w.guid] = self._wdone.get(w.guid, 0) + 1
+                    if self._wdone[w.guid] == self.weight_users.get(w.guid, 1):
+                        self.bucketer.mark_ready(w.guid)
+            pending = {}
+            for j, t in enumerate(L.inputs):
+                if not self.in_grad.get((L.name, j)):
+                    continue
+                key = (t.guid, self.lay[L.name].inputs[j].key())
+                gj = dxs[j] if dxs is not None and j < len(dxs) else None
+                if key in pending:
+                    if gj is not None:
+                        prev = pending[key][2]
+                        pending[key][2] = gj if prev is None else prev + gj
+                else:
+                    pending[key] = [t, j, gj]
+            for key, (t, j, gj) in pending.items():
+                gp = self.bwd_tx[(L.name, j)].run(self.comm, gj, self._like(t))
+                if gp is not None:
+                    prev = grads.get(t.guid)
+                    grads[t.guid] = gp if prev is None else prev + gp
+
+    def zero_gradients(self):
+        for ar in self.arenas.values():
+            ar.grad.zero_()
+
+    def update(self, optimizer):
+        self.bucketer.flush()
+        optimizer.next()
+        for ar in self.arenas.values():
+            if ar.size:
+                optimizer.step(ar)
+        self.step_idx += 1
+
+    def init_optimizer(self, optimizer):
+        for ar in self.arenas.values():
+            optimizer.init_state(ar)
+
+    # ------------------------------------------------------------------ value access
+    def gather_full(self, t, local: Optional[torch.Tensor], layout: Layout) -> torch.Tensor:
+        """Full logical value on every rank (for get_tensor / get_weights)."""
+        if not self.comm.distributed:
+            assert layout.num_parts == 1 or layout.device_set() == (self.rank,), layout
+            return local
+        dst = Layout(layout.shape, (1,) * layout.ndim, self.world, tuple(range(self.world)))
+        tx = Transfer(layout, dst, layout.partial, self.rank)
+        self.comm.ensure_groups(tx.rank_sets())
+        return tx.run(self.comm, local, self._like(t))
+
+    def get_value(self, t):
+        if self.model.label_tensor is not None and t.guid == self.model.label_tensor.guid:
+            return self.gather_full(t, self.inputs.get(t.guid), self.label_layout)
+        lay = self.producer_layout[t.guid]
+        return self.gather_full(t, self.values.get(t.guid), lay)
+
+    def get_weight(self, w):
+        loc = self.weight_tensor(w) if w.guid in self.weight_loc else None
+        if loc is not None and w.guid in self.weight_loc:
+            loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[0]
+        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False))
+
+    def get_weight_grad(self, w):
+        loc = None
+        if w.guid in self.weight_loc:
+            loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]
+        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False))
+
+    def set_weight(self, w, value: np.ndarray):
+        if w.guid not in self.weight_loc:
+            return
+        ar, idx = self.weight_loc[w.guid]
+        m, _, c = ar.views(idx)
+        wl = self.weight_layout[w.guid]
+        p = wl.parts_on(self.rank)[0]
+        sl = rel_slices(wl.region(p), tuple((0, s) for s in w.dims))
+        m.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(value, dtype=np.float32)[sl])))
+        if c is not m:
+            c.copy_(m)
+
+    def metrics_snapshot(self) -> np.ndarray:
+        acc = self._metric_acc.clone()
+        if self.comm.distributed:
+            dist.all_reduce(acc)
+        return acc.cpu().numpy()
+
+    def reset_metrics(self):
+        self._metric_acc.zero_()
