@@ -111,7 +111,14 @@ void bias_act_bwd(Tensor dy, optional<Tensor> z, optional<Tensor> dz, optional<T
                   int64_t cols, int64_t act) {
   TORCH_CHECK(dy.numel() == rows * cols);
   if (dbias.has_value() && dbias->defined()) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->numel() >= cols);
-  ffk::bias_act_bwd(dtcode(dy), dy.data_ptr(), ptr(z), ptr(dz), ptr<float>(dbias), rows, cols, act, cur_stream());
+  Tensor ws;
+  float* wsp = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    ws = at::empty({(int64_t)ffk::bias_act_bwd_chunks(rows, cols) * cols}, dy.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  ffk::bias_act_bwd(dtcode(dy), dy.data_ptr(), ptr(z), ptr(dz), ptr<float>(dbias), wsp, rows, cols, act,
+                    cur_stream());
 }
 void layernorm_fwd(Tensor x, optional<Tensor> res, optional<Tensor> sum_out, optional<Tensor> gamma,
                    optional<Tensor> beta, Tensor y, Tensor mean, Tensor rstd, int64_t rows, int64_t cols,
@@ -124,9 +131,10 @@ void layernorm_bwd(Tensor dy, Tensor x, optional<Tensor> gamma, Tensor mean, Ten
                    optional<Tensor> dres, optional<Tensor> dgamma, optional<Tensor> dbeta, int64_t rows,
                    int64_t cols, bool acc) {
   TORCH_CHECK(dy.numel() == rows * cols && dx.numel() == rows * cols);
+  Tensor ws = at::empty({2 * (int64_t)ffk::layernorm_bwd_waves(rows) * cols}, dy.options().dtype(at::kFloat));
   ffk::layernorm_bwd(dtcode(dy), dy.data_ptr(), x.data_ptr(), ptr(gamma), mean.data_ptr<float>(),
-                     rstd.data_ptr<float>(), dx.data_ptr(), ptr(dres), ptr<float>(dgamma), ptr<float>(dbeta), rows,
-                     cols, acc, cur_stream());
+                     rstd.data_ptr<float>(), dx.data_ptr(), ptr(dres), ptr<float>(dgamma), ptr<float>(dbeta),
+                     ws.data_ptr<float>(), rows, cols, acc, cur_stream());
 }
 void softmax_fwd(Tensor x, Tensor y, int64_t rows, int64_t cols, double scale) {
   TORCH_CHECK(x.numel() == rows * cols);

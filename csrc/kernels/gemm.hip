@@ -33,7 +33,11 @@ __device__ __forceinline__ int swz_mn(int row) {  // 256-B row image, T10 (b)
   return ((row & 3) << 2) | ((row >> 2) & 3);
 }
 
-template <bool KCONT, int ROWS>
+// ALIGNED: rows of the contiguous dim start 16-B aligned and its extent is a multiple of 8, so a
+// whole 8-element chunk is in or out of bounds and loads as one dwordx4. Otherwise (e.g. a 30522-
+// wide vocab projection) each element is bounds-checked and loaded as a 16-bit value — only the
+// operand that needs it pays, the MFMA/LDS pipeline is unchanged.
+template <bool KCONT, int ROWS, bool ALIGNED = true>
 struct Stager {
   // ROWS = 128 (the M or N extent of the tile)
   uint4 r[4];
@@ -47,12 +51,31 @@ struct Stager {
       if (KCONT) { mn = id >> 3; kk = (id & 7) * 8; }
       else { kk = id >> 4; mn = (id & 15) * 8; }
       const int gm = mn0 + mn, gk = k0 + kk;
-      bool ok = KCONT ? (gm < mn_lim && gk < k_lim) : (gk < k_lim && gm < mn_lim);
-      if (ok) {
-        const bf16_t* p = KCONT ? g + (int64_t)gm * ld + gk : g + (int64_t)gk * ld + gm;
-        r[i] = *reinterpret_cast<const uint4*>(p);
+      if (ALIGNED) {
+        bool ok = KCONT ? (gm < mn_lim && gk < k_lim) : (gk < k_lim && gm < mn_lim);
+        if (ok) {
+          const bf16_t* p = KCONT ? g + (int64_t)gm * ld + gk : g + (int64_t)gk * ld + gm;
+          r[i] = *reinterpret_cast<const uint4*>(p);
+        } else {
+          r[i] = make_uint4(0, 0, 0, 0);
+        }
       } else {
-        r[i] = make_uint4(0, 0, 0, 0);
+        uint16_t e[8];
+        if (KCONT) {
+          const bool rok = gm < mn_lim;
+          const bf16_t* p = g + (int64_t)gm * ld;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = (rok && gk + j < k_lim) ? p[gk + j] : (uint16_t)0;
+        } else {
+          const bool kok = gk < k_lim;
+          const bf16_t* p = g + (int64_t)gk * ld;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = (kok && gm + j < mn_lim) ? p[gm + j] : (uint16_t)0;
+        }
+        r[i].x = e[0] | ((uint32_t)e[1] << 16);
+        r[i].y = e[2] | ((uint32_t)e[3] << 16);
+        r[i].z = e[4] | ((uint32_t)e[5] << 16);
+        r[i].w = e[6] | ((uint32_t)e[7] << 16);
       }
     }
   }
@@ -117,7 +140,7 @@ __device__ __forceinline__ void tile_coords(int bid, int tm, int tn, int& tile_m
 
 // OUT_MODE: 0 = bf16 output with full epilogue, 1 = fp32 output with full epilogue,
 //           2 = fp32 split-K partial (alpha only, no beta/bias/act)
-template <bool A_K, bool B_K, int OUT_MODE>
+template <bool A_K, bool B_K, int OUT_MODE, bool A_AL = true, bool B_AL = true>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -135,8 +158,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs p) {
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  Stager<A_K, BM> sa;
-  Stager<B_K, BN> sb;
+  Stager<A_K, BM, A_AL> sa;
+  Stager<B_K, BN, B_AL> sb;
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -302,16 +325,19 @@ __global__ void gemm_fallback_kernel(GemmArgs p, bool a_k, bool b_k) {
 }
 
 template <bool AK, bool BK_, int MODE>
-static void launch_tiled(const GemmArgs& p, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<AK, BK_, MODE>), grid, dim3(NT), 0, s, p);
+static void launch_tiled(const GemmArgs& p, dim3 grid, hipStream_t s, bool a_al, bool b_al) {
+  if (a_al && b_al) hipLaunchKernelGGL((gemm_kernel<AK, BK_, MODE, true, true>), grid, dim3(NT), 0, s, p);
+  else if (!a_al && b_al) hipLaunchKernelGGL((gemm_kernel<AK, BK_, MODE, false, true>), grid, dim3(NT), 0, s, p);
+  else if (a_al && !b_al) hipLaunchKernelGGL((gemm_kernel<AK, BK_, MODE, true, false>), grid, dim3(NT), 0, s, p);
+  else hipLaunchKernelGGL((gemm_kernel<AK, BK_, MODE, false, false>), grid, dim3(NT), 0, s, p);
 }
 
 template <int MODE>
-static void dispatch_layout(const GemmArgs& p, dim3 grid, hipStream_t s) {
-  if (p.a_kcontig && p.b_kcontig) launch_tiled<true, true, MODE>(p, grid, s);
-  else if (p.a_kcontig && !p.b_kcontig) launch_tiled<true, false, MODE>(p, grid, s);
-  else if (!p.a_kcontig && p.b_kcontig) launch_tiled<false, true, MODE>(p, grid, s);
-  else launch_tiled<false, false, MODE>(p, grid, s);
+static void dispatch_layout(const GemmArgs& p, dim3 grid, hipStream_t s, bool a_al, bool b_al) {
+  if (p.a_kcontig && p.b_kcontig) launch_tiled<true, true, MODE>(p, grid, s, a_al, b_al);
+  else if (p.a_kcontig && !p.b_kcontig) launch_tiled<true, false, MODE>(p, grid, s, a_al, b_al);
+  else if (!p.a_kcontig && p.b_kcontig) launch_tiled<false, true, MODE>(p, grid, s, a_al, b_al);
+  else launch_tiled<false, false, MODE>(p, grid, s, a_al, b_al);
 }
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
@@ -331,15 +357,15 @@ int gemm_pick_splitk(int M, int N, int K, int batch) {
 
 void gemm_bf16(GemmArgs p, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0 || p.batch <= 0) return;
-  // Tiled path preconditions: 16-B aligned rows of the contiguous dimension.
-  bool ok = aligned16(p.A) && aligned16(p.B) && (p.lda % 8 == 0) && (p.ldb % 8 == 0) &&
-            (p.sA % 8 == 0) && (p.sB % 8 == 0);
-  ok = ok && (p.a_kcontig ? (p.K % 8 == 0) : (p.M % 8 == 0));
-  ok = ok && (p.b_kcontig ? (p.K % 8 == 0) : (p.N % 8 == 0));
+  // 16-B aligned chunks of the contiguous dim for the vector staging path, per operand
+  const bool a_al = aligned16(p.A) && (p.lda % 8 == 0) && (p.sA % 8 == 0) &&
+                    (p.a_kcontig ? (p.K % 8 == 0) : (p.M % 8 == 0));
+  const bool b_al = aligned16(p.B) && (p.ldb % 8 == 0) && (p.sB % 8 == 0) &&
+                    (p.b_kcontig ? (p.K % 8 == 0) : (p.N % 8 == 0));
   const int osz = p.out_f32 ? 4 : 2;
   p.vec_ok = ((p.ldc % 4) == 0) && ((p.sC % 4) == 0) && (((uintptr_t)p.C) % (4 * osz) == 0) &&
              (p.Z == nullptr || ((uintptr_t)p.Z % 8) == 0);
-  if (!ok) {
+  if (p.M * (int64_t)p.N * p.K < 64 * 64 * 64 && !(a_al && b_al)) {
     dim3 grid((p.N + 15) / 16, (p.M + 15) / 16, p.batch);
     if (p.out_f32) hipLaunchKernelGGL(gemm_fallback_kernel<float>, grid, dim3(16, 16), 0, stream, p, p.a_kcontig, p.b_kcontig);
     else hipLaunchKernelGGL(gemm_fallback_kernel<bf16_t>, grid, dim3(16, 16), 0, stream, p, p.a_kcontig, p.b_kcontig);
@@ -349,7 +375,7 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   if (p.splitk > 1 && p.ws != nullptr) {
     p.kchunk = ((p.K + p.splitk - 1) / p.splitk + BK - 1) / BK * BK;
     dim3 grid(tm * tn, p.batch * p.splitk);
-    dispatch_layout<2>(p, grid, stream);
+    dispatch_layout<2>(p, grid, stream, a_al, b_al);
     const int64_t total = (int64_t)p.M * p.N * p.batch;
     if (p.out_f32) hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
     else hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
@@ -358,8 +384,8 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   p.splitk = 1;
   p.kchunk = p.K;
   dim3 grid(tm * tn, p.batch);
-  if (p.out_f32) dispatch_layout<1>(p, grid, stream);
-  else dispatch_layout<0>(p, grid, stream);
+  if (p.out_f32) dispatch_layout<1>(p, grid, stream, a_al, b_al);
+  else dispatch_layout<0>(p, grid, stream, a_al, b_al);
 }
 
 }  // namespace ffk

@@ -107,8 +107,8 @@ template <typename T, int NCH>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const T* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                     const T* __restrict__ dres_in, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, int rows, int cols, int accumulate) {
+                                                     const T* __restrict__ dres_in, float* __restrict__ pgam,
+                                                     float* __restrict__ pbet, int rows, int cols, int accumulate) {
   constexpr int V = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -170,14 +170,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
+  // per-wave partial column sums -> plain-stored slab rows (reduced by col_reduce_add)
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * V;
     if (col < cols) {
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        if (dgamma) atomicAdd(dgamma + col + j, pg[c][j]);
-        if (dbeta) atomicAdd(dbeta + col + j, pb[c][j]);
+      for (int j = 0; j < V; j += 4) {  // V fp32 partials = V/4 16-B stores
+        if (pgam) store16(pgam + (int64_t)wave * cols + col + j, &pg[c][j]);
+        if (pbet) store16(pbet + (int64_t)wave * cols + col + j, &pb[c][j]);
       }
     }
   }
@@ -245,9 +246,11 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 #undef LNF
 }
 
+int layernorm_bwd_waves(int rows) { return 4 * std::max(1, std::min((rows + 63) / 64, 1024)); }
+
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
-                   void* dx, const void* dres_in, float* dgamma, float* dbeta, int rows, int cols, int accumulate,
-                   hipStream_t st) {
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
+                   int accumulate, hipStream_t st) {
   if (rows == 0) return;
   const int esz = dt == DT_BF16 ? 2 : 4;
   const int V = 16 / esz;
@@ -256,8 +259,12 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   const int nch = (cols + 64 * V - 1) / (64 * V);
   // ~16 rows per wave keeps the dgamma/dbeta atomics small while filling the chip
   const int blocks = std::max(1, std::min((rows + 63) / 64, 1024));
-#define LNB(T, N) hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x, \
-                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, dgamma, dbeta, rows, cols, accumulate)
+  const int nw = 4 * blocks;
+  float* pg = dgamma ? ws : nullptr;
+  float* pb = dbeta ? ws + (int64_t)nw * cols : nullptr;
+  bool used_slab = false;
+#define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x, \
+                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, rows, cols, accumulate); } while (0)
   if (dt == DT_BF16) {
     using T = bf16_t;
     if (vec && nch <= 1) LNB(T, 1); else if (vec && nch <= 2) LNB(T, 2); else if (vec && nch <= 4) LNB(T, 4);
@@ -270,6 +277,10 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
                             (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, dgamma, dbeta, rows, cols, accumulate);
   }
 #undef LNB
+  if (used_slab) {
+    if (dgamma) col_reduce_add(pg, dgamma, nw, cols, st);
+    if (dbeta) col_reduce_add(pb, dbeta, nw, cols, st);
+  }
 }
 
 }  // namespace ffk

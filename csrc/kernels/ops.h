@@ -29,15 +29,20 @@ void dropout_fwd(int dt, const void* x, void* y, uint8_t* mask, int64_t n, float
                  uint64_t offset, hipStream_t st);
 void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float rate, int accumulate,
                  hipStream_t st);
-void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, int rows, int cols, int act,
-                  hipStream_t st);
+// dbias += colsum(dz); ws: fp32 slab of bias_act_bwd_chunks(rows, cols) * cols floats
+void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
+                  int act, hipStream_t st);
+int bias_act_bwd_chunks(int rows, int cols);
+void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st);
 
 // norm.hip
 void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st);
+// ws: fp32 slab of 2 * layernorm_bwd_waves(rows) * cols floats (dgamma / dbeta partials)
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
-                   void* dx, const void* dres_in, float* dgamma, float* dbeta, int rows, int cols, int accumulate,
-                   hipStream_t st);
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
+                   int accumulate, hipStream_t st);
+int layernorm_bwd_waves(int rows);
 
 // softmax.hip
 void softmax_fwd(int dt, const void* x, void* y, int rows, int cols, float scale, hipStream_t st);

@@ -430,8 +430,10 @@ def embedding_fwd(idx, table, bag, avg):
             ii = ii.to(torch.int64)
         ext().embedding_fwd(ii, table, out, n, bag, dim, avg)
         return out
-    rows = table.float()[idx.long().reshape(n, bag)]
-    r = rows.mean(1) if avg else rows.sum(1)
+    ii = idx.long().reshape(n, bag)
+    valid = (ii >= 0) & (ii < table.shape[0])  # ids owned by another vocab shard contribute 0
+    rows = table.float()[ii.clamp(0, table.shape[0] - 1)] * valid[..., None]
+    r = rows.sum(1) / bag if avg else rows.sum(1)
     return r.to(table.dtype)
 
 
@@ -445,7 +447,9 @@ def embedding_bwd(idx, dout2d, dtable, bag, avg):
         ext().embedding_bwd(ii, dout2d.contiguous(), dtable, n, bag, dim, avg)
         return
     g = dout2d.float() / (bag if avg else 1)
-    dtable.index_add_(0, idx.long().reshape(-1), g.repeat_interleave(bag, 0))
+    ii = idx.long().reshape(-1)
+    valid = (ii >= 0) & (ii < dtable.shape[0])
+    dtable.index_add_(0, ii[valid], g.repeat_interleave(bag, 0)[valid])
 
 
 # ----------------------------------------------------------------------------- optimizers

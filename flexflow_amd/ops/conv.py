@@ -38,10 +38,12 @@ class _Spatial(OpImpl):
         kh, kw, sh, sw, ph, pw = self._kp()
         ih, iw = self.layer.inputs[0].dims[2:4]
         oh, ow = self.layer.outputs[0].dims[2:4]
+        # block-aligned tiling: output block [a, b) reads input block [a*s, b*s) plus a halo of at
+        # most k rows on each side (the input layout's halo)
         if axis == 2:
-            return ih == oh * sh and kh - 1 == 2 * ph  # 'same'-style tiling, block-aligned input
+            return ih == oh * sh and ph < kh
         if axis == 3:
-            return iw == ow * sw and kw - 1 == 2 * pw
+            return iw == ow * sw and pw < kw
         return True
 
     def _local_input(self, ctx, x, axis_base=2):

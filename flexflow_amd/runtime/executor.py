@@ -209,13 +209,18 @@ class Executor:
     def init_weights(self, seed_base: int):
         """Deterministic global init, each rank keeping its shard."""
         from ..core.initializers import default_initializer
-        for L in self.layers:
+        done = set()
+        for li, L in enumerate(self.layers):
             for i, w in enumerate(L.weights):
-                if w.guid not in self.weight_loc:
+                if w.guid not in self.weight_loc or w.guid in done:
                     continue
+                done.add(w.guid)
                 ar, idx = self.weight_loc[w.guid]
                 m, _, c = ar.views(idx)
-                init = w.initializer or default_initializer(getattr(w, "short_name", w.name), seed_base + w.guid)
+                # model-local seed (layer position, weight slot): identical in every process and
+                # independent of how many models were built before
+                init = w.initializer or default_initializer(getattr(w, "short_name", w.name),
+                                                            seed_base + 1009 * li + i)
                 full = torch.empty(w.dims, dtype=torch.float32, device=self.device)
                 init.fill_full(full, w.dims)
                 wl = self.weight_layout[w.guid]

@@ -24,7 +24,8 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
+                                   (130, 258, 4099)])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -54,6 +55,19 @@ def test_gemm_epilogue_bias_gelu_f32_beta(ffC):
     base = C32.clone()
     _gemm(ffC, A, B, C32, M, N, K, True, True, alpha=0.5, beta=1.0)
     assert _rel(C32, base + 0.5 * (A.float() @ B.float().t())) < 1e-4
+
+
+def test_gemm_unaligned_splitk(ffC):
+    """vocab-projection-like shapes: odd N / K handled by the element-staged MFMA path (not the
+    scalar fallback) including split-K wgrad."""
+    torch.manual_seed(9)
+    T, V, H = 512, 1002, 256
+    dz = torch.randn(T, V, device=DEV).bfloat16()
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    dW = torch.zeros(V, H, device=DEV)
+    ws = torch.empty(V * H * 4, device=DEV)
+    _gemm(ffC, dz, x, dW, V, H, T, False, False, beta=1.0, splitk=4, ws=ws)
+    assert _rel(dW, dz.float().t() @ x.float()) < 1e-3
 
 
 def test_gemm_splitk_and_batch(ffC):
