@@ -152,6 +152,10 @@ def main():
         res["speedup_vs_dp"] = round(el2 / el, 4)
     if rank == 0:
         print(json.dumps(res), flush=True)
+        if os.environ.get("FF_TUNE_LOG"):
+            from flexflow_amd import kernels as K
+            with open(os.environ["FF_TUNE_LOG"], "w") as f:
+                json.dump(K.TUNE_LOG, f, indent=1)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

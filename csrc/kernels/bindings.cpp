@@ -32,7 +32,8 @@ T* ptr(const optional<Tensor>& t) {
 
 void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> Z, int64_t M, int64_t N,
           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t batch,
-          bool a_k, bool b_k, double alpha, double beta, int64_t act, int64_t splitk, optional<Tensor> ws) {
+          bool a_k, bool b_k, double alpha, double beta, int64_t act, int64_t splitk, optional<Tensor> ws,
+          bool big) {
   check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A/B must be bf16");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm: C must be bf16/fp32");
@@ -58,6 +59,9 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
   p.alpha = alpha; p.beta = beta; p.act = act;
   p.a_kcontig = a_k; p.b_kcontig = b_k;
   p.out_f32 = C.scalar_type() == at::kFloat;
+  p.a_bytes = A.numel() * 2;
+  p.b_bytes = B.numel() * 2;
+  p.allow_big = big;
   p.splitk = 1;
   if (splitk > 1 && ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->numel() * ws->element_size() >= ffk::gemm_workspace_bytes(M, N, K, batch, splitk),
@@ -253,7 +257,10 @@ void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "flexflow_amd HIP/CDNA4 kernels (gfx950)";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("Z"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
+        py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
+        py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("big") = true);
   m.def("gemm_pick_splitk", &gemm_pick_splitk);
   m.def("unary_fwd", &unary_fwd);
   m.def("unary_bwd", &unary_bwd);

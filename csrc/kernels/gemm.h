@@ -23,10 +23,13 @@ struct GemmArgs {
   bool vec_ok = false;
   int splitk = 1;
   int kchunk = 0;
+  int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
+  bool allow_big = true;
 };
 
 void gemm_bf16(GemmArgs p, hipStream_t stream);
 int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk);
 int gemm_pick_splitk(int M, int N, int K, int batch);
+bool gemm_big_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 
 }  // namespace ffk

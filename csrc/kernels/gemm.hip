@@ -348,11 +348,19 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 }
 
 int gemm_pick_splitk(int M, int N, int K, int batch) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
+  // tile count of the kernel that will run (256x128 DMA kernel when K % 64 == 0)
+  const bool big = (K % 64 == 0);
+  const int tiles = big ? ((M + 255) / 256) * ((N + 127) / 128) * batch
+                        : ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
   if (tiles >= 256 || K < 1024) return 1;
-  int s = 1;
-  while (tiles * s * 2 <= 512 && (K / (s * 2)) >= 512) s *= 2;
-  return s;
+  // minimise (waves of 256 CUs) / split, with a small charge per split for the fp32 slab reduce
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 8 && K / s >= 512; ++s) {
+    const double cost = (double)((tiles * s + 255) / 256) / s + 0.03 * s;
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
+  }
+  return best;
 }
 
 void gemm_bf16(GemmArgs p, hipStream_t stream) {
@@ -375,7 +383,8 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   if (p.splitk > 1 && p.ws != nullptr) {
     p.kchunk = ((p.K + p.splitk - 1) / p.splitk + BK - 1) / BK * BK;
     dim3 grid(tm * tn, p.batch * p.splitk);
-    dispatch_layout<2>(p, grid, stream, a_al, b_al);
+    if (!(p.allow_big && a_al && b_al && p.a_bytes > 0 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)))
+      dispatch_layout<2>(p, grid, stream, a_al, b_al);
     const int64_t total = (int64_t)p.M * p.N * p.batch;
     if (p.out_f32) hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
     else hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
@@ -383,6 +392,7 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   }
   p.splitk = 1;
   p.kchunk = p.K;
+  if (p.allow_big && a_al && b_al && p.a_bytes > 0 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)) return;
   dim3 grid(tm * tn, p.batch);
   if (p.out_f32) dispatch_layout<1>(p, grid, stream, a_al, b_al);
   else dispatch_layout<0>(p, grid, stream, a_al, b_al);

@@ -246,7 +246,7 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 #undef LNF
 }
 
-int layernorm_bwd_waves(int rows) { return 4 * std::max(1, std::min((rows + 63) / 64, 1024)); }
+int layernorm_bwd_waves(int rows) { return 4 * std::max(1, std::min((rows + 15) / 16, 1024)); }
 
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
@@ -257,8 +257,8 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   const bool vec = (cols % V == 0) && a16(x) && a16(dy) && a16(dx) && (!dres_in || a16(dres_in)) &&
                    (!gamma || a16(gamma));
   const int nch = (cols + 64 * V - 1) / (64 * V);
-  // ~16 rows per wave keeps the dgamma/dbeta atomics small while filling the chip
-  const int blocks = std::max(1, std::min((rows + 63) / 64, 1024));
+  // ~4 rows per wave: enough waves in flight to cover HBM latency, slab partials stay small
+  const int blocks = std::max(1, std::min((rows + 15) / 16, 1024));
   const int nw = 4 * blocks;
   float* pg = dgamma ? ws : nullptr;
   float* pb = dbeta ? ws + (int64_t)nw * cols : nullptr;

@@ -367,6 +367,13 @@ class FFModel:
         self.loss_type = loss_type
         self.metrics = list(metrics or [])
         _ensure_dist(cfg)
+        self.subst_report = None
+        if os.environ.get("FF_NO_SUBST", "0") != "1":
+            try:
+                from ..pcg.substitutions import optimize_graph
+                self.subst_report = optimize_graph(self)
+            except ImportError:  # native core not built: run the graph as written
+                self.subst_report = {"skipped": "native core unavailable"}
         out = self.output_tensor()
         if loss_type is not None and out is not None:
             if loss_type == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:

@@ -67,18 +67,107 @@ def act_grad_ref(z, act):
 
 
 # ----------------------------------------------------------------------------------- GEMM
+import os as _os
+
+_TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
+_tuned: dict = {}
+TUNE_LOG: list = []
+
+
+def _views(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC):
+    Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)
+    Bf = B.as_strided((batch, N, K), (sB, ldb, 1)).transpose(1, 2) if b_k else B.as_strided((batch, K, N), (sB, ldb, 1))
+    Cv = C.as_strided((batch, M, N), (sC, ldc, 1))
+    return Af, Bf, Cv
+
+
+def _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC):
+    """Plain GEMM on the vendor library (hipBLASLt via torch): bf16 in, bf16 or fp32 out, optional
+    bias, beta-accumulate. Only offered for calls without a fused activation epilogue."""
+    Af, Bf, Cv = _views(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC)
+    if batch == 1 and alpha == 1.0 and beta == 0.0 and Cv[0].is_contiguous():
+        a2, b2, c2 = Af[0], Bf[0], Cv[0]
+        if C.dtype == torch.float32:  # bf16 x bf16 -> fp32 straight into C (weight-gradient arena)
+            torch.mm(a2, b2, out_dtype=torch.float32, out=c2)
+        elif bias is not None:
+            torch.addmm(bias.to(a2.dtype), a2, b2, out=c2)
+        else:
+            torch.mm(a2, b2, out=c2)
+        return
+    if batch == 1:
+        a2, b2 = Af[0], Bf[0]
+        if C.dtype == torch.float32:
+            r = torch.mm(a2, b2, out_dtype=torch.float32)
+        elif bias is not None:
+            r = torch.addmm(bias.to(a2.dtype), a2, b2)
+            bias = None
+        else:
+            r = torch.mm(a2, b2)
+        r = r.unsqueeze(0)
+    else:
+        r = torch.bmm(Af, Bf)
+    if alpha != 1.0:
+        r = r * alpha
+    if bias is not None:
+        r = r + bias.to(r.dtype)
+    if beta != 0.0:
+        Cv.add_(r.to(Cv.dtype)) if beta == 1.0 else Cv.mul_(beta).add_(r.to(Cv.dtype))
+    else:
+        Cv.copy_(r)
+
+
+def _time(fn, reps=3):
+    fn()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        fn()
+    en.record()
+    en.synchronize()
+    return st.elapsed_time(en) / reps
+
+
 def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=None, Z=None, act=ACT_NONE,
          batch=1, sA=0, sB=0, sC=0, splitk=None):
-    """C = act(alpha*op(A).op(B) + beta*C + bias); raw strided views (see csrc/kernels/gemm.hip)."""
+    """C = act(alpha*op(A).op(B) + beta*C + bias); raw strided views (see csrc/kernels/gemm.hip).
+
+    On the device, each call site (shape, layouts, epilogue) is autotuned once, outside graph
+    capture, among our 256x128 LDS-DMA MFMA kernel, our 128x128 MFMA kernel and — for plain GEMMs
+    without a fused activation / pre-activation store — the vendor library GEMM."""
     if native(C) and A.dtype == torch.bfloat16:
         X = ext()
         if splitk is None:
             splitk = X.gemm_pick_splitk(M, N, K, batch) if batch == 1 else 1
-        ws = None
-        if splitk > 1:
-            ws = torch.empty(M * N * batch * splitk, device=C.device, dtype=torch.float32)
-        X.gemm(A, B, C, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act,
-               splitk, ws)
+
+        def ours(big, out=C):
+            ws = None
+            if splitk > 1:
+                ws = torch.empty(M * N * batch * splitk, device=C.device, dtype=torch.float32)
+            X.gemm(A, B, out, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act,
+                   splitk, ws, big)
+
+        key = (M, N, K, a_k, b_k, lda, ldb, ldc, batch, C.dtype, bias is not None, Z is not None, act,
+               beta != 0.0, splitk)
+        choice = _tuned.get(key)
+        if choice is None:
+            plain = act == ACT_NONE and Z is None and sC in (0, M * N) and ldc == N
+            if not _TUNE or torch.cuda.is_current_stream_capturing():
+                choice = "big"
+            else:
+                scratch = torch.zeros_like(C)
+                cands = {"big": lambda: ours(True, scratch), "128": lambda: ours(False, scratch)}
+                if plain:
+                    cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
+                                                     bias, batch, sA, sB, sC)
+                times = {k: _time(f) for k, f in cands.items()}
+                choice = min(times, key=times.get)
+                TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
+                                 "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
+            _tuned[key] = choice
+        if choice == "lib":
+            _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC)
+        else:
+            ours(choice == "big")
         return C
     # reference / fp32 path (library GEMM on device, plain torch on CPU)
     Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)
@@ -114,8 +203,9 @@ def linear_fwd(x2d, w, bias, act, save_z):
     return y, z
 
 
-def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True):
-    """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+=). Returns dx (or None)."""
+def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0):
+    """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+= ; dw_beta=0 overwrites dw
+    when the executor knows this op is the weight's only user). Returns dx (or None)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     if act != ACT_NONE:
@@ -130,13 +220,16 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True):
             dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
             gemm(dz, w, dx, M, K, N, True, False, N, K, K)
         if dw is not None:
-            gemm(dz, x2d, dw, N, K, M, False, False, N, K, K, beta=1.0)
+            gemm(dz, x2d, dw, N, K, M, False, False, N, K, K, beta=dw_beta)
         return dx
     dzf = dz.float()
     if need_dx:
         dx = (dzf @ w.float()).to(dy2d.dtype)
     if dw is not None:
-        dw.add_(dzf.t() @ x2d.float())
+        if dw_beta == 0.0:
+            dw.copy_(dzf.t() @ x2d.float())
+        else:
+            dw.add_(dzf.t() @ x2d.float())
     return dx
 
 

@@ -169,8 +169,9 @@ class MultiHeadAttention(OpImpl):
         o2 = o.view(B * Sq, Hl * vd)
         dwo = gw("o_weight")
         dbo = gw("o_bias") if s["has_bo"] else None
+        wb = 0.0 if ctx.extra.get("wgrad_overwrite") else 1.0
         do2 = K.linear_bwd(dy2, o2, s["wo"], None, K.ACT_NONE,
-                           dwo.view(E, Hl * vd) if dwo is not None else None, dbo)
+                           dwo.view(E, Hl * vd) if dwo is not None else None, dbo, dw_beta=wb)
         do = do2.view(B, Sq, Hl, vd)
         scale, causal = s["scale"], s["causal"]
         qs, ks, vs, os_ = s["qs"], s["ks"], s["vs"], s["os"]
@@ -202,7 +203,7 @@ class MultiHeadAttention(OpImpl):
             db = gw("qkv_bias")
             dx2 = K.linear_bwd(dqkv, s["x2"], s["wqkv"], None, K.ACT_NONE,
                                dw.view(3 * Hl * kd, -1) if dw is not None else None,
-                               db.view(-1) if db is not None else None)
+                               db.view(-1) if db is not None else None, dw_beta=wb)
             dx = dx2.view(B, Sq, -1)
             ctx.saved.clear()
             return [dx, None, None]  # all three inputs are the same tensor: gradient once
@@ -213,7 +214,7 @@ class MultiHeadAttention(OpImpl):
             x2 = s[f"x_{name}"]
             dx2 = K.linear_bwd(g.view(B * S_, Hl * d), x2, s[f"w_{name}"], None, K.ACT_NONE,
                                dw.view(Hl * d, -1) if dw is not None else None,
-                               db.view(-1) if db is not None else None)
+                               db.view(-1) if db is not None else None, dw_beta=wb)
             grads.append(dx2.view(B, S_, -1))
         ctx.saved.clear()
         return grads

@@ -50,14 +50,18 @@ class LayerNorm(OpImpl):
         return [tuple([None] * len(w.dims)) for w in self.layer.weights]
 
     def forward(self, ctx, xs, ws):
+        # 2 inputs = residual-fused LayerNorm(x + res), produced by the fuse_add_layernorm
+        # substitution: one kernel reads x and res and writes y (+ the sum kept for backward)
         x = xs[0]
+        res = xs[1] if len(xs) > 1 else None
         nrm = int(math.prod(x.shape[a] for a in self.attrs["axes"]))
         assert self.attrs["axes"] == list(range(x.dim() - len(self.attrs["axes"]), x.dim())), \
             "LayerNorm axes must be trailing"
         x2 = x.reshape(-1, nrm)
+        r2 = res.reshape(-1, nrm).contiguous() if res is not None else None
         g = ws[0].reshape(-1) if ws else None
         b = ws[1].reshape(-1) if ws else None
-        y, xs_, mean, rstd = K.layernorm_fwd(x2, None, g, b, float(self.attrs.get("eps", 1e-5)), False)
+        y, xs_, mean, rstd = K.layernorm_fwd(x2.contiguous(), r2, g, b, float(self.attrs.get("eps", 1e-5)), False)
         if ctx.training:
             ctx.saved.update(x=xs_, mean=mean, rstd=rstd, g=g)
         return [y.reshape(x.shape)]
@@ -69,7 +73,8 @@ class LayerNorm(OpImpl):
         dg = ctx.wgrads[0].reshape(-1) if ctx.wgrads else None
         db = ctx.wgrads[1].reshape(-1) if ctx.wgrads else None
         dx = K.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, s.pop("g"), s.pop("mean"), s.pop("rstd"), dg, db)
-        return [dx.reshape(dy.shape)]
+        dx = dx.reshape(dy.shape)
+        return [dx, dx] if len(self.layer.inputs) > 1 else [dx]
 
     def flops(self, in_shapes, out_shapes, w_shapes):
         return 8.0 * math.prod(out_shapes[0])

@@ -32,6 +32,13 @@ class Softmax(OpImpl):
 
     def forward(self, ctx, xs, ws):
         x = xs[0]
+        if ctx.training and ctx.extra.get("loss_fused") and self.dim == x.dim() - 1:
+            # The loss consumes the LOGITS (fused softmax + cross-entropy kernel), so the
+            # [tokens x classes] probability tensor is never written; probabilities are produced
+            # on demand if the user reads this tensor (executor.get_value).
+            ctx.extra["emitted_logits"] = True
+            return [x]
+        ctx.extra["emitted_logits"] = False
         xm = x.movedim(self.dim, -1) if self.dim != x.dim() - 1 else x
         shp = xm.shape
         y = K.softmax_fwd(xm.reshape(-1, shp[-1]).contiguous()).reshape(shp)
@@ -42,10 +49,11 @@ class Softmax(OpImpl):
         return [y]
 
     def backward(self, ctx, douts):
-        y = ctx.saved.pop("y")
         dy = douts[0]
         if ctx.extra.get("loss_fused"):
+            ctx.saved.pop("y", None)
             return [dy]
+        y = ctx.saved.pop("y")
         if self.dim != y.dim() - 1:
             ym, dym = y.movedim(self.dim, -1), dy.movedim(self.dim, -1)
             shp = ym.shape

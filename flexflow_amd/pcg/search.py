@@ -50,11 +50,20 @@ def choose_strategy(model):
         report["algo"] = "data_parallel"
         return data_parallel_strategy(layers, n), report
     try:
+        from flexflow_amd import _core  # noqa: F401
         from .unity import search as native_search
     except ImportError:
         native_search = None
     if native_search is None:
-        report["algo"] = "data_parallel(fallback)"
+        report["algo"] = "data_parallel(fallback: native core not built)"
         return data_parallel_strategy(layers, n), report
+    distributed = dist.is_available() and dist.is_initialized() and cfg.world_size > 1
+    if distributed and cfg.rank != 0:
+        # rank 0 searches (its measured costs decide); everyone else receives the result
+        obj = [None, None]
+        dist.broadcast_object_list(obj, src=0)
+        return {k: OpConfig.from_json(v) for k, v in obj[0].items()}, obj[1]
     strat, report = native_search(model, algo)
-    return _broadcast_strategy(model, strat), report
+    if distributed:
+        dist.broadcast_object_list([{k: v.to_json() for k, v in strat.items()}, report], src=0)
+    return strat, report

@@ -203,6 +203,8 @@ class Executor:
             self.bucketer.add_arena(grp, ar.grad, segs)
         for L in self.layers:
             if L.name in self.ctx:
+                self.ctx[L.name].extra["wgrad_overwrite"] = bool(L.weights) and all(
+                    self.weight_users.get(w.guid, 1) == 1 for w in L.weights)
                 self.ctx[L.name].wgrads = [self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]
                                            if w.guid in self.weight_loc else None for w in L.weights]
 
@@ -257,6 +259,12 @@ class Executor:
             LossType.LOSS_CATEGORICAL_CROSSENTROPY, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY))
         if self.softmax_fused and owner.name in self.ctx:
             self.ctx[owner.name].extra["loss_fused"] = True
+        self._softmax_last_dim = self.softmax_fused and (owner.attrs.get("dim", -1) % len(out.dims) == len(out.dims) - 1)
+        self._fwd_training = self.training
+
+    def _softmax_emitted_logits(self) -> bool:
+        """The fused softmax emits raw logits in training forwards (see ops/softmax.py)."""
+        return self._softmax_last_dim and self._fwd_training
 
     # ------------------------------------------------------------------ inputs
     def input_layout(self, t) -> Layout:
@@ -298,6 +306,7 @@ class Executor:
 
     def forward(self, training: Optional[bool] = None):
         tr = self.training if training is None else training
+        self._fwd_training = tr
         vals = self.values
         for L in self.layers:
             if L.op_type == OperatorType.OP_INPUT:
@@ -334,13 +343,15 @@ class Executor:
             lab = self.inputs.get(self.model.label_tensor.guid)
             rows = v.reshape(v.shape[0], -1) if lt != LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY else \
                 v.reshape(-1, v.shape[-1])
+            logits = not self.softmax_fused or self._softmax_emitted_logits()
             if lt == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY:
                 labels = lab.reshape(-1).to(torch.int32)
-                if self.softmax_fused:
+                if not logits:
                     g, lrow = K.xent_grad(rows.contiguous(), labels, None, 1.0 / B, True)
-                else:
+                else:  # fused softmax + cross-entropy straight from the logits
                     g, lrow = K.softmax_xent(rows.contiguous(), labels, 1.0 / B)
                 self._metric_acc[0] += lrow.sum()
+                self._lrow = lrow
             elif lt == LossType.LOSS_CATEGORICAL_CROSSENTROPY:
                 oh = lab.reshape(rows.shape).to(rows.dtype)
                 if self.softmax_fused:
@@ -377,12 +388,16 @@ class Executor:
             else:
                 labels = None
             if labels is not None and rows.shape[0] == labels.shape[0]:
-                probs = rows if self.softmax_fused else torch.softmax(rows.float(), -1).to(rows.dtype)
+                have_probs = self.softmax_fused and not self._softmax_emitted_logits()
                 acc3 = torch.zeros(3, dtype=torch.float32, device=v.device)
-                K.metrics_classify(probs.contiguous(), labels, acc3)
+                # argmax of logits == argmax of probabilities: accuracy needs no softmax pass
+                K.metrics_classify(rows.contiguous(), labels, acc3)
                 self._metric_acc[1] += acc3[0]
-                self._metric_acc[2] += acc3[1]
                 self._metric_acc[3] += acc3[2]
+                if have_probs:
+                    self._metric_acc[2] += acc3[1]
+                elif lt == LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY and getattr(self, "_lrow", None) is not None:
+                    self._metric_acc[2] += self._lrow.sum()
         if MetricsType.METRICS_MEAN_SQUARED_ERROR in mets or MetricsType.METRICS_ROOT_MEAN_SQUARED_ERROR in mets \
                 or MetricsType.METRICS_MEAN_ABSOLUTE_ERROR in mets:
             if lab.numel() == v.numel():
@@ -464,7 +479,11 @@ class Executor:
         if self.model.label_tensor is not None and t.guid == self.model.label_tensor.guid:
             return self.gather_full(t, self.inputs.get(t.guid), self.label_layout)
         lay = self.producer_layout[t.guid]
-        return self.gather_full(t, self.values.get(t.guid), lay)
+        full = self.gather_full(t, self.values.get(t.guid), lay)
+        if (self.output_tensor is not None and t.guid == self.output_tensor.guid and self.softmax_fused
+                and self._softmax_emitted_logits()):
+            full = torch.softmax(full.float(), -1).to(full.dtype)  # probabilities on demand
+        return full
 
     def get_weight(self, w):
         loc = self.weight_tensor(w) if w.guid in self.weight_loc else None

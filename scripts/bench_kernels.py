@@ -41,7 +41,10 @@ def gemm_case(M, N, K, a_k, b_k, out_f32=False, act=10, splitk=1):
     lda, ldb = A.shape[1], B.shape[1]
 
     def mine():
-        _C.gemm(A, B, C, None, None, M, N, K, lda, ldb, N, 0, 0, 0, 1, a_k, b_k, 1.0, 0.0, act, splitk, ws)
+        _C.gemm(A, B, C, None, None, M, N, K, lda, ldb, N, 0, 0, 0, 1, a_k, b_k, 1.0, 0.0, act, splitk, ws, True)
+
+    def mine128():
+        _C.gemm(A, B, C, None, None, M, N, K, lda, ldb, N, 0, 0, 0, 1, a_k, b_k, 1.0, 0.0, act, splitk, ws, False)
 
     At = A if a_k else A.t()
     Bt = B.t() if b_k else B
@@ -50,11 +53,12 @@ def gemm_case(M, N, K, a_k, b_k, out_f32=False, act=10, splitk=1):
         torch.matmul(At, Bt)
 
     t_m = timeit(mine)
+    t_s = timeit(mine128)
     t_l = timeit(lib)
     fl = 2.0 * M * N * K
     return {"op": "gemm", "M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "splitk": splitk,
             "ours_ms": round(t_m, 4), "lib_ms": round(t_l, 4), "ours_tflops": round(fl / t_m / 1e9, 1),
-            "lib_tflops": round(fl / t_l / 1e9, 1)}
+            "ours128_tflops": round(fl / t_s / 1e9, 1), "lib_tflops": round(fl / t_l / 1e9, 1)}
 
 
 def attn_case(B, H, S, D):
@@ -112,7 +116,7 @@ def main():
         cases = cases[:3]
     for c in cases:
         print(json.dumps(gemm_case(*c)), flush=True)
-    for c in [(3072, 1024, T, False, False), (1024, 1024, T, False, False)]:
+    for c in [(3072, 1024, T, False, False), (1024, 1024, T, False, False), (4096, 1024, T, False, False)]:
         sk = _C.gemm_pick_splitk(c[0], c[1], c[2], 1)
         print(json.dumps(gemm_case(*c, splitk=max(sk, 2))), flush=True)
     print(json.dumps(attn_case(T // 512, 16, 512, 64)), flush=True)

@@ -17,7 +17,7 @@ for step in "$@"; do
   case $step in
     tests) run tests 600 python -m pytest tests -m gpu -x -q ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    bench) run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    bench) FF_TUNE_LOG=$OUT/tune.json run bench 600 python bench.py --steps 10 --warmup 3 ;;
     microbench) run microbench 400 python scripts/bench_kernels.py ;;
     prof) cd /tmp && export TMPDIR=/tmp && run prof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-hip-graphs; cd - >/dev/null ;;
   esac

@@ -25,7 +25,7 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
-                                   (130, 258, 4099)])
+                                   (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -68,6 +68,28 @@ def test_gemm_unaligned_splitk(ffC):
     ws = torch.empty(V * H * 4, device=DEV)
     _gemm(ffC, dz, x, dW, V, H, T, False, False, beta=1.0, splitk=4, ws=ws)
     assert _rel(dW, dz.float().t() @ x.float()) < 1e-3
+
+
+def test_gemm_big_splitk_bias(ffC):
+    """256x128 LDS-DMA kernel: split-K wgrad and fused bias/GELU epilogue at >=128 tiles."""
+    torch.manual_seed(10)
+    M, N, K = 1024, 1024, 8192
+    dY = torch.randn(K, M, device=DEV).bfloat16()
+    X = torch.randn(K, N, device=DEV).bfloat16()
+    ws = torch.empty(M * N * 8, device=DEV)
+    C = torch.zeros(M, N, device=DEV)
+    _gemm(ffC, dY, X, C, M, N, K, False, False, beta=1.0, splitk=8, ws=ws)
+    assert _rel(C, dY.float().t() @ X.float()) < 1e-3
+    M, N, K = 4096, 2048, 512
+    A = torch.randn(M, K, device=DEV).bfloat16()
+    B = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    Cb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    Z = torch.empty_like(Cb)
+    _gemm(ffC, A, B, Cb, M, N, K, True, True, bias=bias, Z=Z, act=14)
+    z = A.float() @ B.float().t() + bias
+    assert _rel(Z, z) < 1e-2
+    assert _rel(Cb, torch.nn.functional.gelu(z)) < 1e-2
 
 
 def test_gemm_splitk_and_batch(ffC):
