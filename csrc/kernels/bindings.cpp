@@ -148,10 +148,11 @@ void softmax_bwd(Tensor y, Tensor dy, Tensor dx, int64_t rows, int64_t cols, dou
   ffk::softmax_bwd(dtcode(y), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), rows, cols, scale, acc, cur_stream());
 }
 void softmax_xent(Tensor logits, Tensor labels, optional<Tensor> loss, optional<Tensor> dlogits, int64_t rows,
-                  int64_t cols, double gscale) {
+                  int64_t cols, double gscale, optional<Tensor> acc3) {
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= rows);
+  TORCH_CHECK(!acc3 || (acc3->scalar_type() == at::kFloat && acc3->numel() >= 3));
   ffk::softmax_xent_fwd_bwd(dtcode(logits), logits.data_ptr(), labels.data_ptr<int>(), ptr<float>(loss),
-                            ptr(dlogits), rows, cols, gscale, cur_stream());
+                            ptr(dlogits), rows, cols, gscale, ptr<float>(acc3), cur_stream());
 }
 void xent_grad(Tensor probs, optional<Tensor> labels, optional<Tensor> onehot, Tensor dprobs, optional<Tensor> loss,
                int64_t rows, int64_t cols, double gscale, bool sparse) {
@@ -274,7 +275,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
-  m.def("softmax_xent", &softmax_xent);
+  m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("loss"), py::arg("dlogits"),
+        py::arg("rows"), py::arg("cols"), py::arg("gscale"), py::arg("acc3") = py::none());
   m.def("xent_grad", &xent_grad);
   m.def("mse_grad", &mse_grad);
   m.def("metrics_classify", &metrics_classify);

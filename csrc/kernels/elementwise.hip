@@ -236,60 +236,97 @@ __global__ void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 
 // Fused activation-backward + bias-gradient for Linear/Conv epilogues:
 //   dz[r][c] = dy[r][c] * act'(z[r][c]);   part[y][c] = sum_{r in chunk y} dz[r][c]
-// Each thread owns 8 consecutive columns (16 B of bf16) and walks one row chunk; the per-chunk
-// column sums go to a plain-stored fp32 slab (no same-address atomics: every block would hit the
-// same N words — the contended pattern MI355X_MICROARCH 'Global float atomics' prices at 14x),
-// then col_reduce_add folds the slab into dbias.
-template <typename T>
-__global__ void bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z, T* __restrict__ dz,
-                                    float* __restrict__ part, int rows, int cols, int act, int rows_per_block) {
-  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (c0 >= cols) return;
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
+// A block = 4 waves x 512 columns (each lane 8 consecutive columns = one 16-B load per row, a wave
+// reads 1 KiB contiguous per row); the waves interleave rows, 4 rows in flight per wave, and fold
+// their sums through LDS so the fp32 slab has one row per block.  The slab is folded by
+// col_reduce_add with <= 32 adders per address (the full-rate regime of MI355X_MICROARCH
+// 'Global float atomics'; all blocks into one row is 14x slower, hence no direct atomics).
+constexpr int BAB_COLS = 512;
+template <typename T, bool ACT>
+__global__ void __launch_bounds__(256) bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z,
+                                                           T* __restrict__ dz, float* __restrict__ part, int rows,
+                                                           int cols, int act, int rpb) {
+  __shared__ float red[4][BAB_COLS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * BAB_COLS + lane * 8;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool vec = (c0 + 8 <= cols) && ((cols & 7) == 0) && sizeof(T) == 2;
-  for (int r = r0; r < r1; ++r) {
-    const int64_t base = (int64_t)r * cols + c0;
-    float g[8], zz[8];
+  if (c0 < cols) {
+    const bool vec = sizeof(T) == 2 && (cols & 7) == 0;
+    int r = r0 + w;
     if (vec) {
-      load16(dy + base, g);
-      if (act != ACT_NONE) load16(z + base, zz);
+      // U rows in flight per wave (U x 16 B per lane, plus z when ACT): the whole block's rows are
+      // requested before the first add, which is what hides HBM latency on these short kernels
+      constexpr int U = ACT ? 4 : 8;
+      for (; r + 4 * (U - 1) < r1; r += 4 * U) {
+        float g[U][8], zz[ACT ? U : 1][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          load16(dy + (int64_t)(r + 4 * u) * cols + c0, g[u]);
+          if (ACT) load16(z + (int64_t)(r + 4 * u) * cols + c0, zz[ACT ? u : 0]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (ACT) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[u][j] *= act_grad(act, zz[ACT ? u : 0][j]);
+            if (dz) store16(dz + (int64_t)(r + 4 * u) * cols + c0, g[u]);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += g[u][j];
+        }
+      }
+      for (; r < r1; r += 4) {
+        float g[8], zz[8];
+        load16(dy + (int64_t)r * cols + c0, g);
+        if (ACT) {
+          load16(z + (int64_t)r * cols + c0, zz);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] *= act_grad(act, zz[j]);
+          if (dz) store16(dz + (int64_t)r * cols + c0, g);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += g[j];
+      }
     } else {
-      for (int j = 0; j < 8; ++j) {
-        g[j] = (c0 + j < cols) ? Cvt<T>::to_f(dy[base + j]) : 0.f;
-        zz[j] = (act != ACT_NONE && c0 + j < cols) ? Cvt<T>::to_f(z[base + j]) : 0.f;
+      for (; r < r1; r += 4) {
+        const int64_t base = (int64_t)r * cols + c0;
+        for (int j = 0; j < 8 && c0 + j < cols; ++j) {
+          float g = Cvt<T>::to_f(dy[base + j]);
+          if (ACT) {
+            g *= act_grad(act, Cvt<T>::to_f(z[base + j]));
+            if (dz) dz[base + j] = Cvt<T>::from_f(g);
+          }
+          acc[j] += g;
+        }
       }
     }
-    if (act != ACT_NONE) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] *= act_grad(act, zz[j]);
-      if (dz) {
-        if (vec) store16(dz + base, g);
-        else for (int j = 0; j < 8; ++j) if (c0 + j < cols) dz[base + j] = Cvt<T>::from_f(g[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += g[j];
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = acc[j];
+  __syncthreads();
   if (part) {
-    float* pr = part + (int64_t)blockIdx.y * cols;
-    for (int j = 0; j < 8; ++j)
-      if (c0 + j < cols) pr[c0 + j] = acc[j];
+    for (int k = threadIdx.x; k < BAB_COLS; k += 256) {
+      const int c = blockIdx.x * BAB_COLS + k;
+      if (c < cols) part[(int64_t)blockIdx.y * cols + c] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+    }
   }
 }
 
-// out[c] += sum_{r < R} part[r][c]. Block = 64 columns x 4 row lanes; grid.y row chunks, one
-// atomic per column per chunk (gridDim.y <= 8 adders per address).
-__global__ void col_reduce_add_kernel(const float* __restrict__ part, float* __restrict__ out, int R, int C) {
+// out_z[c] += sum_{r < R} part[z*R*C + r*C + c] for z < gridDim.z (LN folds dgamma and dbeta in one
+// launch). Block = 64 columns x 4 row lanes; gridDim.y row chunks (<= 32 adders per address).
+__global__ void col_reduce_add_kernel(const float* __restrict__ part, float* __restrict__ out0,
+                                      float* __restrict__ out1, int R, int C) {
   __shared__ float red[4][64];
+  const float* p = part + (int64_t)blockIdx.z * R * C;
+  float* out = blockIdx.z ? out1 : out0;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
   const int per = (R + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
   float s = 0.f;
   if (c < C)
-    for (int r = r0 + rl; r < r1; r += 4) s += part[(int64_t)r * C + c];
+    for (int r = r0 + rl; r < r1; r += 4) s += p[(int64_t)r * C + c];
   red[rl][threadIdx.x & 63] = s;
   __syncthreads();
   if (rl == 0 && c < C) {
@@ -298,17 +335,29 @@ __global__ void col_reduce_add_kernel(const float* __restrict__ part, float* __r
   }
 }
 
-void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st) {
+void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st) {
   if (R == 0 || C == 0) return;
-  const int gy = std::max(1, std::min(8, R / 16));
-  hipLaunchKernelGGL(col_reduce_add_kernel, dim3((C + 63) / 64, gy), dim3(256), 0, st, part, out, R, C);
+  const int gy = std::max(1, std::min(32, R / 8));
+  hipLaunchKernelGGL(col_reduce_add_kernel, dim3((C + 63) / 64, gy, out1 ? 2 : 1), dim3(256), 0, st, part, out0,
+                     out1, R, C);
+}
+void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st) {
+  col_reduce_add2(part, out, nullptr, R, C, st);
+}
+
+static void bab_geometry(int rows, int cols, int& gx, int& gy, int& rpb) {
+  gx = (cols + BAB_COLS - 1) / BAB_COLS;
+  // >= ~1024 blocks where the shape allows (4+ per CU), >= 32 rows per block (one 8-row batch
+  // per wave), slab rows = gy
+  gy = std::max(1, std::min((1024 + gx - 1) / gx, (rows + 31) / 32));
+  rpb = (((rows + gy - 1) / gy) + 31) / 32 * 32;
+  gy = (rows + rpb - 1) / rpb;
 }
 
 int bias_act_bwd_chunks(int rows, int cols) {
-  const int gx = (cols / 8 + 256) / 256;
-  int gy = std::max(1, std::min(rows / 16, 1024 / std::max(gx, 1)));
-  const int rpb = (rows + gy - 1) / gy;
-  return (rows + rpb - 1) / rpb;
+  int gx, gy, rpb;
+  bab_geometry(rows, cols, gx, gy, rpb);
+  return gy;
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -392,13 +441,15 @@ void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t 
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
                   int act, hipStream_t st) {
   if (rows == 0 || cols == 0) return;
-  const int threads = 256;
-  const int gx = (cols / 8 + threads) / threads;
-  const int gy = bias_act_bwd_chunks(rows, cols);
-  const int rpb = (rows + gy - 1) / gy;
+  int gx, gy, rpb;
+  bab_geometry(rows, cols, gx, gy, rpb);
   FFK_DT_DISPATCH(dt, {
-    hipLaunchKernelGGL(bias_act_bwd_kernel<T>, dim3(gx, gy), dim3(threads), 0, st, (const T*)dy, (const T*)z,
-                       (T*)dz, dbias ? ws : nullptr, rows, cols, act, rpb);
+    if (act != ACT_NONE)
+      hipLaunchKernelGGL((bias_act_bwd_kernel<T, true>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy, (const T*)z,
+                         (T*)dz, dbias ? ws : nullptr, rows, cols, act, rpb);
+    else if (dbias)
+      hipLaunchKernelGGL((bias_act_bwd_kernel<T, false>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy, (const T*)z,
+                         (T*)dz, ws, rows, cols, act, rpb);
   });
   if (dbias) col_reduce_add(ws, dbias, gy, cols, st);
 }

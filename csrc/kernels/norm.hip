@@ -170,17 +170,26 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  // per-wave partial column sums -> plain-stored slab rows (reduced by col_reduce_add)
+  // per-wave partial column sums -> folded over the block's 4 waves in LDS -> one plain-stored slab
+  // row per block (reduced by col_reduce_add2); dynamic LDS = 4 * cols floats, reused for beta
+  extern __shared__ float lds_red[];
+  const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = (c * 64 + lane) * V;
-    if (col < cols) {
+  for (int pass = 0; pass < 2; ++pass) {
+    float* slab = pass ? pbet : pgam;
+    if (!slab) continue;
 #pragma unroll
-      for (int j = 0; j < V; j += 4) {  // V fp32 partials = V/4 16-B stores
-        if (pgam) store16(pgam + (int64_t)wave * cols + col + j, &pg[c][j]);
-        if (pbet) store16(pbet + (int64_t)wave * cols + col + j, &pb[c][j]);
-      }
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * 64 + lane) * V;
+      if (col < cols)
+#pragma unroll
+        for (int j = 0; j < V; ++j) lds_red[w * cols + col + j] = pass ? pb[c][j] : pg[c][j];
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < cols; k += 256)
+      slab[(int64_t)blockIdx.x * cols + k] =
+          lds_red[k] + lds_red[cols + k] + lds_red[2 * cols + k] + lds_red[3 * cols + k];
+    __syncthreads();
   }
 }
 
@@ -246,7 +255,7 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 #undef LNF
 }
 
-int layernorm_bwd_waves(int rows) { return 4 * std::max(1, std::min((rows + 15) / 16, 1024)); }
+int layernorm_bwd_waves(int rows) { return std::max(1, std::min((rows + 15) / 16, 1024)); }  // slab rows = blocks
 
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
@@ -259,11 +268,11 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   const int nch = (cols + 64 * V - 1) / (64 * V);
   // ~4 rows per wave: enough waves in flight to cover HBM latency, slab partials stay small
   const int blocks = std::max(1, std::min((rows + 15) / 16, 1024));
-  const int nw = 4 * blocks;
+  const int nw = blocks;
   float* pg = dgamma ? ws : nullptr;
   float* pb = dbeta ? ws + (int64_t)nw * cols : nullptr;
   bool used_slab = false;
-#define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 0, st, (const T*)dy, (const T*)x, \
+#define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 4 * cols * sizeof(float), st, (const T*)dy, (const T*)x, \
                                      (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, rows, cols, accumulate); } while (0)
   if (dt == DT_BF16) {
     using T = bf16_t;
@@ -278,8 +287,9 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   }
 #undef LNB
   if (used_slab) {
-    if (dgamma) col_reduce_add(pg, dgamma, nw, cols, st);
-    if (dbeta) col_reduce_add(pb, dbeta, nw, cols, st);
+    if (dgamma && dbeta) col_reduce_add2(pg, dgamma, dbeta, nw, cols, st);  // pb = pg + nw * cols
+    else if (dgamma) col_reduce_add(pg, dgamma, nw, cols, st);
+    else if (dbeta) col_reduce_add(pb, dbeta, nw, cols, st);
   }
 }
 

@@ -34,6 +34,8 @@ void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias,
                   int act, hipStream_t st);
 int bias_act_bwd_chunks(int rows, int cols);
 void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st);
+// out0 += colsum(part[0:R]); out1 += colsum(part[R:2R]) (out1 may be null)
+void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st);
 
 // norm.hip
 void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
@@ -50,7 +52,7 @@ void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int 
                  hipStream_t st);
 // Fused softmax + sparse categorical cross-entropy: writes per-row loss (fp32) and dlogits = (p - onehot)*gscale.
 void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
-                          int cols, float gscale, hipStream_t st);
+                          int cols, float gscale, float* acc3 /*[3] or null*/, hipStream_t st);
 // Loss on already-normalised probabilities (reference semantics: loss follows a Softmax op)
 void xent_grad(int dt, const void* probs, const int* labels, const void* onehot, void* dprobs, float* loss, int rows,
                int cols, float gscale, int sparse, hipStream_t st);

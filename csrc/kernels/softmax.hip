@@ -65,27 +65,95 @@ __global__ void softmax_bwd_kernel(const T* __restrict__ y, const T* __restrict_
   }
 }
 
+// Visit one row with 16-B loads: a scalar head up to the first 16-B boundary (rows of an odd
+// width such as BERT's 30522-entry vocabulary start at every 4-B offset), a vector body, a scalar tail.
+template <typename T, typename F>
+__device__ __forceinline__ void row_visit(const T* __restrict__ xr, int cols, int lane, F&& f) {
+  constexpr int V = 16 / sizeof(T);
+  const int head = min(cols, (int)(((16 - ((uintptr_t)xr & 15)) & 15) / sizeof(T)));
+  if (lane < head) f(lane, Cvt<T>::to_f(xr[lane]));
+  const int nvec = (cols - head) / V;
+  const T* body = xr + head;
+  for (int i = lane; i < nvec; i += 64) {
+    float v[V];
+    load16(body + (int64_t)i * V, v);
+#pragma unroll
+    for (int j = 0; j < V; ++j) f(head + i * V + j, v[j]);
+  }
+  for (int c = head + nvec * V + lane; c < cols; c += 64) f(c, Cvt<T>::to_f(xr[c]));
+}
+
+// Fused softmax + sparse cross-entropy from the LOGITS (the [rows x classes] probabilities are
+// never written): pass 1 = online max / sum-exp / argmax with 16-B loads, pass 2 = the gradient
+// (p - onehot) * gscale.  Optional acc3 += {correct, sum CE, rows} folds the accuracy / CE metrics
+// (reference metrics_functions.cu) into the same read of the logits.
 template <typename T>
-__global__ void softmax_xent_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
+__global__ void __launch_bounds__(256) softmax_xent_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
                                     float* __restrict__ loss, T* __restrict__ dlogits, int rows, int cols,
-                                    float gscale) {
+                                    float gscale, float* __restrict__ acc3) {
+  constexpr int V = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  float correct = 0.f, ce = 0.f, cnt = 0.f;
   for (int row = wave; row < rows; row += nwaves) {
     const T* xr = logits + (int64_t)row * cols;
-    float m, s;
-    row_stats(xr, cols, 1.f, lane, m, s);
+    float m = -INFINITY, s = 0.f;
+    int bi = 0x7fffffff;
+    row_visit(xr, cols, lane, [&](int c, float v) {
+      if (v > m) { s = s * __expf(m - v) + 1.f; m = v; bi = c; }
+      else s += __expf(v - m);
+    });
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (m2 > m || (m2 == m && i2 < bi)) bi = i2;
+      online_merge(m, s, m2, s2);
+    }
     const int lab = labels[row];
     const float lse = m + __logf(s);
-    if (lane == 0 && loss) loss[row] = (lab >= 0 && lab < cols) ? lse - Cvt<T>::to_f(xr[lab]) : 0.f;
+    const bool valid = lab >= 0 && lab < cols;
+    const float l = valid ? lse - Cvt<T>::to_f(xr[valid ? lab : 0]) : 0.f;
+    if (lane == 0) {
+      if (loss) loss[row] = l;
+      correct += (bi == lab) ? 1.f : 0.f;
+      ce += l;
+      cnt += 1.f;
+    }
     if (dlogits) {
       T* dr = dlogits + (int64_t)row * cols;
-      for (int c = lane; c < cols; c += 64) {
-        const float p = __expf(Cvt<T>::to_f(xr[c]) - lse);
-        dr[c] = Cvt<T>::from_f((p - (c == lab ? 1.f : 0.f)) * gscale);
+      if ((((uintptr_t)dr ^ (uintptr_t)xr) & 15) == 0) {
+        const int head = min(cols, (int)(((16 - ((uintptr_t)xr & 15)) & 15) / sizeof(T)));
+        if (lane < head) {
+          const float p = __expf(Cvt<T>::to_f(xr[lane]) - lse);
+          dr[lane] = Cvt<T>::from_f((p - (lane == lab ? 1.f : 0.f)) * gscale);
+        }
+        const int nvec = (cols - head) / V;
+        for (int i = lane; i < nvec; i += 64) {
+          float v[V];
+          const int c0 = head + i * V;
+          load16(xr + c0, v);
+#pragma unroll
+          for (int j = 0; j < V; ++j) v[j] = (__expf(v[j] - lse) - (c0 + j == lab ? 1.f : 0.f)) * gscale;
+          store16(dr + c0, v);
+        }
+        for (int c = head + nvec * V + lane; c < cols; c += 64) {
+          const float p = __expf(Cvt<T>::to_f(xr[c]) - lse);
+          dr[c] = Cvt<T>::from_f((p - (c == lab ? 1.f : 0.f)) * gscale);
+        }
+      } else {
+        for (int c = lane; c < cols; c += 64) {
+          const float p = __expf(Cvt<T>::to_f(xr[c]) - lse);
+          dr[c] = Cvt<T>::from_f((p - (c == lab ? 1.f : 0.f)) * gscale);
+        }
       }
     }
+  }
+  if (acc3 && lane == 0 && cnt > 0.f) {
+    atomicAdd(acc3 + 0, correct);
+    atomicAdd(acc3 + 1, ce);
+    atomicAdd(acc3 + 2, cnt);
   }
 }
 
@@ -201,10 +269,10 @@ void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int 
                                      (const T*)dy, (T*)dx, rows, cols, scale, accumulate));
 }
 void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
-                          int cols, float gscale, hipStream_t st) {
+                          int cols, float gscale, float* acc3, hipStream_t st) {
   if (rows == 0) return;
   DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st,
-                                     (const T*)logits, labels, loss, (T*)dlogits, rows, cols, gscale));
+                                     (const T*)logits, labels, loss, (T*)dlogits, rows, cols, gscale, acc3));
 }
 void xent_grad(int dt, const void* probs, const int* labels, const void* onehot, void* dprobs, float* loss, int rows,
                int cols, float gscale, int sparse, hipStream_t st) {

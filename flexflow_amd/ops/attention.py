@@ -201,23 +201,34 @@ class MultiHeadAttention(OpImpl):
         if fused:
             dw = gw("qkv_weight")
             db = gw("qkv_bias")
+            acc = (ctx.extra.get("dx_accum") or {}).get(0)
             dx2 = K.linear_bwd(dqkv, s["x2"], s["wqkv"], None, K.ACT_NONE,
                                dw.view(3 * Hl * kd, -1) if dw is not None else None,
-                               db.view(-1) if db is not None else None, dw_beta=wb)
-            dx = dx2.view(B, Sq, -1)
+                               db.view(-1) if db is not None else None, dw_beta=wb,
+                               dx_out=acc.view(B * Sq, -1) if acc is not None else None)
+            dx = acc if acc is not None else dx2.view(B, Sq, -1)
             ctx.saved.clear()
             return [dx, None, None]  # all three inputs are the same tensor: gradient once
         grads = []
-        for name, g, d, S_ in (("q", dq, kd, Sq), ("k", dk, kd, Sk), ("v", dv, vd, Sk)):
+        accs = ctx.extra.get("dx_accum") or {}
+        for slot, (name, g, d, S_) in enumerate((("q", dq, kd, Sq), ("k", dk, kd, Sk), ("v", dv, vd, Sk))):
+            acc = accs.get(slot)
             dw = gw(f"{name}_weight")
             db = gw(f"{name}_bias")
             x2 = s[f"x_{name}"]
             dx2 = K.linear_bwd(g.view(B * S_, Hl * d), x2, s[f"w_{name}"], None, K.ACT_NONE,
                                dw.view(Hl * d, -1) if dw is not None else None,
-                               db.view(-1) if db is not None else None, dw_beta=wb)
-            grads.append(dx2.view(B, S_, -1))
+                               db.view(-1) if db is not None else None, dw_beta=wb,
+                               dx_out=acc.view(B * S_, -1) if acc is not None else None)
+            grads.append(acc if acc is not None else dx2.view(B, S_, -1))
         ctx.saved.clear()
         return grads
+
+    def accumulates_dx(self):
+        return True
+
+    def accum_may_alias_douts(self):
+        return True  # dy is consumed by the output projection before the QKV dgrad writes
 
     def flops(self, in_shapes, out_shapes, w_shapes):
         B, Sq, Eq = in_shapes[0]

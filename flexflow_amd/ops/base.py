@@ -143,6 +143,16 @@ class OpImpl:
         return float(elem * (sum(math.prod(s) for s in in_shapes) + sum(math.prod(s) for s in out_shapes)
                              + sum(math.prod(s) for s in w_shapes)))
 
+    def accumulates_dx(self) -> bool:
+        """True if backward honours ctx.extra['dx_accum'] = {input slot: tensor}: it then ADDS the
+        input gradient into that tensor (same shape/dtype) and returns it for that slot."""
+        return False
+
+    def accum_may_alias_douts(self) -> bool:
+        """True if every read of the output gradients is issued before the first write into a
+        dx_accum target, so that target may share storage with an output gradient."""
+        return False
+
     def uses_mfma(self) -> bool:
         return False
 

@@ -85,12 +85,17 @@ class Linear(OpImpl):
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         dw = ctx.wgrads[0] if ctx.wgrads else None
         db = ctx.wgrads[1] if (len(ctx.wgrads) > 1 and ctx.saved["has_b"]) else None
+        acc = (ctx.extra.get("dx_accum") or {}).get(0)
         dx = K.linear_bwd(dy2, x2, w, z, self.act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
-                          dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0)
+                          dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0,
+                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None)
         ctx.saved.clear()
         if dx is None:
             return [None]
-        return [dx.reshape(tuple(dy.shape[:-1]) + (x2.shape[1],))]
+        return [acc if acc is not None else dx.reshape(tuple(dy.shape[:-1]) + (x2.shape[1],))]
+
+    def accumulates_dx(self):
+        return True
 
     def flops(self, in_shapes, out_shapes, w_shapes):
         return 2.0 * math.prod(out_shapes[0]) * in_shapes[0][-1]

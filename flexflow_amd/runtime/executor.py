@@ -348,9 +348,12 @@ class Executor:
                 labels = lab.reshape(-1).to(torch.int32)
                 if not logits:
                     g, lrow = K.xent_grad(rows.contiguous(), labels, None, 1.0 / B, True)
-                else:  # fused softmax + cross-entropy straight from the logits
-                    g, lrow = K.softmax_xent(rows.contiguous(), labels, 1.0 / B)
-                self._metric_acc[0] += lrow.sum()
+                    self._metric_acc[0] += lrow.sum()
+                else:  # fused softmax + cross-entropy (+ accuracy/CE metrics) straight from the logits
+                    acc3 = torch.zeros(3, dtype=torch.float32, device=rows.device)
+                    g, lrow = K.softmax_xent(rows.contiguous(), labels, 1.0 / B, acc3)
+                    self._metric_acc[0] += acc3[1]
+                    self._xent_acc3 = acc3
                 self._lrow = lrow
             elif lt == LossType.LOSS_CATEGORICAL_CROSSENTROPY:
                 oh = lab.reshape(rows.shape).to(rows.dtype)
@@ -387,7 +390,13 @@ class Executor:
                 labels = lab.reshape(rows.shape).float().argmax(-1).to(torch.int32)
             else:
                 labels = None
-            if labels is not None and rows.shape[0] == labels.shape[0]:
+            acc3 = getattr(self, "_xent_acc3", None)
+            if acc3 is not None:  # already folded into the fused softmax-xent pass
+                self._xent_acc3 = None
+                self._metric_acc[1] += acc3[0]
+                self._metric_acc[2] += acc3[1]
+                self._metric_acc[3] += acc3[2]
+            elif labels is not None and rows.shape[0] == labels.shape[0]:
                 have_probs = self.softmax_fused and not self._softmax_emitted_logits()
                 acc3 = torch.zeros(3, dtype=torch.float32, device=v.device)
                 # argmax of logits == argmax of probabilities: accuracy needs no softmax pass
@@ -425,7 +434,10 @@ class Executor:
                     vals = [self.values.get(o.guid) for o in L.outputs]
                     douts = [d if d is not None else (torch.zeros_like(v) if v is not None else None)
                              for d, v in zip(douts, vals)]
-                    dxs = L.impl.backward(self.ctx[L.name], douts)
+                    ctx = self.ctx[L.name]
+                    ctx.extra["dx_accum"] = self._accum_targets(L, grads, douts)
+                    dxs = L.impl.backward(ctx, douts)
+                    ctx.extra["dx_accum"] = None
                 for w in L.weights:
                     self._wdone[w.guid] = self._wdone.get(w.guid, 0) + 1
                     if self._wdone[w.guid] == self.weight_users.get(w.guid, 1):
@@ -446,7 +458,30 @@ class Executor:
                 gp = self.bwd_tx[(L.name, j)].run(self.comm, gj, self._like(t))
                 if gp is not None:
                     prev = grads.get(t.guid)
-                    grads[t.guid] = gp if prev is None else prev + gp
+                    grads[t.guid] = gp if (prev is None or prev is gp) else prev + gp
+
+    def _accum_targets(self, L, grads, douts):
+        """Input slots whose existing gradient the op may accumulate into in place (a dgrad GEMM
+        with beta = 1 instead of a separate add): the tensor already has a gradient from another
+        consumer, the backward transfer is the identity, and no other live gradient (or this op's
+        own output gradient) aliases that buffer."""
+        if not L.impl.accumulates_dx():
+            return None
+        out = {}
+        for j, t in enumerate(L.inputs):
+            prev = grads.get(t.guid)
+            if prev is None or not self.in_grad.get((L.name, j)) or self.bwd_tx[(L.name, j)].kind != "identity":
+                continue
+            if any(u.guid == t.guid for u in L.inputs[:j]):
+                continue  # offered to the first slot only; the op returns None for the repeats
+            sp = prev.untyped_storage().data_ptr()
+            if any(g is not None and g.untyped_storage().data_ptr() == sp for k, g in grads.items() if k != t.guid) \
+                    or (not L.impl.accum_may_alias_douts()
+                        and any(d is not None and d.untyped_storage().data_ptr() == sp for d in douts)) \
+                    or not prev.is_contiguous():
+                continue
+            out[j] = prev
+        return out or None
 
     def zero_gradients(self):
         for ar in self.arenas.values():

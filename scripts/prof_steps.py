@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-step kernel breakdown from a rocprofv3 --kernel-trace CSV.
+
+Steps are delimited by the optimizer kernel (one fused adam/sgd launch per weight arena per step);
+the first `--skip` steps (autotuning, graph capture warm-up) are dropped so the numbers reflect
+the steady state only.  Prints ms/step per kernel (grouped by demangled-name prefix), the busy
+time and the wall span per step (span - busy = launch gaps / host stalls).
+
+usage: prof_steps.py run_kernel_trace.csv [--skip 2] [--top 40] [--delim adam_kernel]
+"""
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("--skip", type=int, default=2)
+ap.add_argument("--top", type=int, default=40)
+ap.add_argument("--delim", default="adam_kernel|sgd_kernel")
+a = ap.parse_args()
+
+rows = list(csv.DictReader(open(a.trace)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+delim = re.compile(a.delim)
+ends = [i for i, r in enumerate(rows) if delim.search(r["Kernel_Name"])]
+# several arenas -> several optimizer launches back to back; keep the last of each run
+marks = [e for k, e in enumerate(ends) if k + 1 == len(ends) or ends[k + 1] != e + 1]
+if len(marks) <= a.skip + 1:
+    raise SystemExit(f"only {len(marks)} steps found")
+lo, hi = marks[a.skip] + 1, marks[-1] + 1
+steps = len(marks) - 1 - a.skip
+win = rows[lo:hi]
+per = defaultdict(lambda: [0.0, 0])
+
+
+def short(n):
+    n = re.sub(r"\(.*$", "", n)
+    n = re.sub(r"^void ", "", n)
+    if n.startswith("Cijk_") or n.startswith("Custom_Cijk"):
+        m = re.search(r"MT\d+x\d+x\d+", n)
+        return "hipblaslt " + n.split("_")[1 if n.startswith("Cijk") else 2] + "_" + \
+            n.split("_")[2 if n.startswith("Cijk") else 3] + " " + (m.group(0) if m else "")
+    return n[:110]
+
+
+busy = 0.0
+for r in win:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    k = short(r["Kernel_Name"])
+    per[k][0] += d
+    per[k][1] += 1
+    busy += d
+span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e6
+print(f"{steps} steps: busy {busy / steps:.3f} ms/step, span {span / steps:.3f} ms/step, "
+      f"{len(win) / steps:.0f} kernels/step")
+for k, (t, c) in sorted(per.items(), key=lambda kv: -kv[1][0])[:a.top]:
+    print(f"{t / steps:8.3f} ms/step {c / steps:6.1f}/step {100 * t / busy:5.1f}%  {k}")

@@ -163,10 +163,9 @@ def test_flash_attention_strided_qkv(ffC):
     assert _rel(o.permute(0, 2, 1, 3), ref) < 2e-2
 
 
-@pytest.mark.parametrize("cols", [1024, 768, 100])
-def test_layernorm(ffC, cols):
+@pytest.mark.parametrize("cols,rows", [(1024, 300), (768, 300), (100, 300), (1024, 8200)])
+def test_layernorm(ffC, cols, rows):
     torch.manual_seed(5)
-    rows = 300
     x = torch.randn(rows, cols, device=DEV).bfloat16()
     r = torch.randn(rows, cols, device=DEV).bfloat16()
     g = torch.randn(cols, device=DEV).bfloat16()
@@ -213,6 +212,48 @@ def test_softmax_and_xent(ffC):
     ref.backward()
     assert abs(loss.mean().item() - ref.item()) < 1e-4
     assert _rel(dl, xr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("cols", [30522, 1001, 64])
+def test_softmax_xent_bf16_metrics(ffC, cols):
+    """Fused softmax-xent on bf16 logits whose rows start at every 4-B offset (odd vocab), with the
+    accuracy / CE metrics folded into the same pass."""
+    torch.manual_seed(16)
+    rows = 203
+    x = (torch.randn(rows, cols, device=DEV) * 3).bfloat16()
+    labels = torch.randint(0, cols, (rows,), device=DEV, dtype=torch.int32)
+    labels[::7] = x[::7].float().argmax(-1).int()
+    loss = torch.empty(rows, device=DEV)
+    dl = torch.empty_like(x)
+    acc3 = torch.zeros(3, device=DEV)
+    ffC.softmax_xent(x, labels, loss, dl, rows, cols, 1.0 / rows, acc3)
+    xr = x.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(xr, labels.long(), reduction="none")
+    ref.sum().backward()
+    assert _rel(loss, ref) < 1e-3
+    assert _rel(dl.float() * rows, xr.grad) < 1e-2
+    assert acc3[0].item() == (x.float().argmax(-1) == labels.long()).sum().item()
+    assert abs(acc3[1].item() - ref.sum().item()) < 1e-3 * ref.sum().item()
+    assert acc3[2].item() == rows
+
+
+@pytest.mark.parametrize("rows,cols,act", [(8192, 1024, 10), (8192, 4096, 14), (300, 30522, 10), (77, 1000, 12),
+                                           (4096, 520, 11)])
+def test_bias_act_bwd(ffC, rows, cols, act):
+    torch.manual_seed(17)
+    dy = torch.randn(rows, cols, device=DEV).bfloat16()
+    z = torch.randn(rows, cols, device=DEV).bfloat16()
+    db = torch.ones(cols, device=DEV)
+    if act == 10:
+        ffC.bias_act_bwd(dy, None, None, db, rows, cols, act)
+        dz_ref = dy.float()
+    else:
+        dz = torch.empty_like(dy)
+        ffC.bias_act_bwd(dy, z, dz, db, rows, cols, act)
+        from flexflow_amd.kernels import act_grad_ref
+        dz_ref = dy.float() * act_grad_ref(z.float(), act)
+        assert _rel(dz, dz_ref) < 1e-2
+    assert _rel(db, 1.0 + dz_ref.sum(0)) < 1e-3
 
 
 def test_adam_sgd_embedding_dropout(ffC):
