@@ -6,7 +6,9 @@ parallelization strategy, one process per MI355X (torchrun), bf16 compute, synth
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 
-Per-GPU batch is fixed (weak scaling): global_batch = batch_per_gpu * N. Every timed step is a
+Per-GPU batch is fixed (weak scaling): global_batch = batch_per_gpu * N (default 32 sequences
+of 512 tokens per GPU: MI355X has 288 GB of HBM, and at 16 the step is too short to amortise the
+optimizer pass and the small-GEMM tails). Every timed step is a
 full training iteration (forward, backward, gradient all-reduce, optimizer update). Rank 0 prints
 ONE JSON line; the step time is the MAX over ranks of the time between two barrier+synchronize
 fences around exactly K steps.
@@ -35,8 +37,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="bert-large", choices=["bert-large", "bert-base", "bert-tiny"])
-    ap.add_argument("--batch-per-gpu", type=int, default=16)
+    ap.add_argument("--model", default="bert-large",
+                    help="bert-large | bert-base | bert-tiny | any flexflow_amd.models.MODELS entry "
+                         "(alexnet, resnet50, inception_v3, dlrm, ...)")
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="default 32 for BERT (HBM-sized: 288 GB/GPU), 64 for the other models")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--search", default="unity", help="unity | mcmc | dp")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -47,28 +52,43 @@ def parse():
 
 
 def build(args, search):
-    from flexflow_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+    """Returns (ff, global_batch, info); info = {seq, flops_per_sample, params, extra config fields}."""
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    from flexflow_amd.models import build as build_model
     from flexflow_amd.models.bert import BertConfig, build_bert
     world = int(os.environ.get("WORLD_SIZE", "1"))
     flags = ["--dtype", args.dtype, "--search", search]
     if args.no_hip_graphs:
         flags.append("--no-hip-graphs")
     cfg = FFConfig(flags)
-    gb = args.batch_per_gpu * world
+    bert = args.model.startswith("bert")
+    bpg = args.batch_per_gpu or (32 if bert else 64)
+    gb = bpg * world
     cfg.batch_size = gb
-    bc = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "bert-tiny": BertConfig.tiny}[args.model](args.seq)
-    bc.seq = args.seq
-    bc.max_pos = max(bc.max_pos, args.seq)
     ff = FFModel(cfg)
-    ids, pos, out = build_bert(ff, gb, bc)
-    opt = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)
-    ff.optimizer = opt
-    ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
     rng = np.random.default_rng(1234)
-    ids.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq), dtype=np.int32))
-    pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (gb, 1)))
-    ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq, 1), dtype=np.int32))
-    return ff, bc, gb
+    if bert:
+        bc = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "bert-tiny": BertConfig.tiny}[args.model](args.seq)
+        bc.seq = args.seq
+        bc.max_pos = max(bc.max_pos, args.seq)
+        ids, pos, out = build_bert(ff, gb, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        ids.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (gb, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq, 1), dtype=np.int32))
+        info = {"seq": bc.seq, "flops_per_sample": bc.train_flops_per_seq(), "params": bc.params(),
+                "extra": {"hidden": bc.hidden, "layers": bc.layers, "heads": bc.heads, "vocab": bc.vocab}}
+        return ff, gb, info
+    inputs, out, loss, mets, make_batch = build_model(args.model, ff, gb)
+    ff.optimizer = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)
+    ff.compile(loss_type=loss, metrics=mets)
+    arrs, lab = make_batch(rng)
+    for t, a in zip(inputs, arrs):
+        t.set_tensor(ff, a)
+    ff.label_tensor.set_tensor(ff, lab)
+    params = sum(int(np.prod(w.dims)) for L in ff.layers for w in L.weights)
+    return ff, gb, {"seq": None, "flops_per_sample": None, "params": params, "extra": {}}
 
 
 def describe(ff, world):
@@ -120,11 +140,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    ff, bc, gb = build(args, args.search)
+    ff, gb, info = build(args, args.search)
     el = timed(ff, args.steps, args.warmup, world)
     ms = el / args.steps * 1e3
     sps = gb * args.steps / el
-    flops = bc.train_flops_per_seq() * gb * args.steps / el
     res = {
         "metric": BASELINE_METRIC,
         "value": round(sps, 3),
@@ -137,13 +156,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (random token ids / labels, random-init weights)",
-        "config": {"model": args.model, "global_batch": gb, "seq_len": bc.seq,
-                   "parallelism": describe(ff, world), "search": (ff.search_report or {}).get("algo"),
-                   "optimizer": args.optimizer, "params": bc.params(), "hidden": bc.hidden, "layers": bc.layers,
-                   "heads": bc.heads, "vocab": bc.vocab},
-        "model_tflops_per_gpu": round(flops / world / 1e12, 2),
+        "data": "synthetic (random inputs / labels, random-init weights)",
+        "config": dict({"model": args.model, "global_batch": gb, "seq_len": info["seq"],
+                        "parallelism": describe(ff, world), "search": (ff.search_report or {}).get("algo"),
+                        "optimizer": args.optimizer, "params": info["params"]}, **info["extra"]),
     }
+    if info["flops_per_sample"]:
+        res["model_tflops_per_gpu"] = round(info["flops_per_sample"] * sps / world / 1e12, 2)
     if args.compare_dp and world > 1:
         del ff
         ff2, _, _ = build(args, "dp")
