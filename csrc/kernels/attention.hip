@@ -134,21 +134,27 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
       }
     }
-    // scale, mask, online softmax (lane-local + xor-32 partner)
-    float mx = -INFINITY;
+    // mask (only on tiles that cross the sequence end or the causal diagonal: a wave-uniform
+    // test), online softmax on the raw scores (lane-local + xor-32 partner), scale folded into
+    // one FMA per element: p = exp2(s * sl2 - m * sl2)
     const int kbase = t * KV;
+    const bool need_mask = (kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0);
+    if (need_mask) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float v = sacc[kt][r] * sl2;
-        if (key >= a.Sk || (a.causal && key > qrow)) v = -INFINITY;
-        sacc[kt][r] = v;
-        mx = fmaxf(mx, v);
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= a.Sk || (a.causal && key > qrow)) sacc[kt][r] = -INFINITY;
+        }
       }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kt][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
     const float mnew = fmaxf(m, mx);
     const float msafe = mnew == -INFINITY ? 0.f : mnew;
     const float alpha = exp2f(m - msafe);
@@ -157,7 +163,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(sacc[kt][r] - msafe);
+        const float p = exp2f(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
         sacc[kt][r] = p;
         rs += p;
       }
@@ -222,23 +228,35 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 // delta[bh][q] = sum_d dO[q][d] * O[q][d]
 template <int D>
 __global__ void attn_bwd_pre_kernel(AttnArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // delta[row] = sum_d O[row][d] * dO[row][d]: D/8 lanes per row, one 16-B load of each per lane
+  constexpr int LPR = D / 8;
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gt / LPR;
+  const int part = (int)(gt % LPR);
   const int64_t total = (int64_t)a.B * a.H * a.Sq;
-  if (gw >= total) return;
-  const int bh = gw / a.Sq, q = gw % a.Sq, b = bh / a.H, hh = bh % a.H;
-  const bf16_t* O = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh + (int64_t)q * a.o_ss;
-  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh + (int64_t)q * a.do_ss;
   float s = 0.f;
-  for (int d = lane; d < D; d += 64) s += bf2f(O[d]) * bf2f(dO[d]);
-  s = wave_sum(s);
-  if (lane == 0) a.delta[gw] = s;
+  if (row < total) {
+    const int bh = (int)(row / a.Sq), q = (int)(row % a.Sq), b = bh / a.H, hh = bh % a.H;
+    const bf16_t* O = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh + (int64_t)q * a.o_ss + part * 8;
+    const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh + (int64_t)q * a.do_ss + part * 8;
+    float o[8], d[8];
+    load16(O, o);
+    load16(dO, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += o[j] * d[j];
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (row < total && part == 0) a.delta[row] = s;
 }
 
-template <int D>
-__global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
-  constexpr int QT = 64;     // queries per loop step
-  constexpr int KB = 128;    // keys per workgroup (4 waves x 32)
+// NW waves x 32 keys per workgroup. NW = 8 (256 keys) halves the fp32 dQ partial slabs that
+// attn_dq_finish_kernel has to sum (the dominant HBM traffic of the backward at S = 512).
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int QT = 64;       // queries per loop step
+  constexpr int KB = 32 * NW;  // keys per workgroup
   constexpr int QB = QT * D * 2;
   // LDS: Q tile, dO tile, K block image, dS^T image [KB][QT], lse/delta
   __shared__ __attribute__((aligned(16))) char smem[2 * QB + KB * D * 2 + KB * QT * 2 + 2 * QT * 4];
@@ -263,7 +281,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
 
   // K block -> LDS (needed for dQ), K^T / V^T fragments -> registers (B operands, key on lane)
   {
-    TileStage<D, KB, 256> st;
+    TileStage<D, KB, NT> st;
     st.load(K, a.k_ss, kb0, a.Sk, tid);
     st.store(k_l, tid);
   }
@@ -292,7 +310,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
     const int qbase = t * QT;
     __syncthreads();  // previous iteration done with q_l/do_l/ds_l
     {
-      TileStage<D, QT, 256> sq, sd;
+      TileStage<D, QT, NT> sq, sd;
       sq.load(Q, a.q_ss, qbase, a.Sq, tid);
       sd.load(dO, a.do_ss, qbase, a.Sq, tid);
       sq.store(q_l, tid);
@@ -365,7 +383,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
     }
     __syncthreads();
     // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's 128 keys; wave -> (qt, dt) tiles
-    for (int tile = wave; tile < 2 * (D / 32); tile += 4) {
+    for (int tile = wave; tile < 2 * (D / 32); tile += NW) {
       const int qt = tile / (D / 32), dt = tile % (D / 32);
       f32x16 acc = f32x16{};
 #pragma unroll
@@ -404,7 +422,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_kernel(AttnArgs a) {
   }
   // causal: query tiles before qt_begin contribute nothing; zero their partial rows
   if (a.causal) {
-    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += 256) dq_part[i] = 0.f;
+    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
   }
   // write dK, dV: lane holds key (lane&31), d = 32dt + (r&3) + 8(r>>2) + 4h
   if (key < a.Sk) {
@@ -451,8 +469,10 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
   }
 }
 
+static int bwd_waves(int) { return 4; }  // 8 (256 keys per WG) measured 1.5x slower at S=512: 4 idle waves in the dQ stage
+
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
-  const int nkb = (Sk + 127) / 128;
+  const int nkb = (Sk + 32 * bwd_waves(Sk) - 1) / (32 * bwd_waves(Sk));
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
@@ -463,21 +483,24 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
 }
 
 void attn_bwd(AttnArgs a, hipStream_t st) {
-  const int nkb = (a.Sk + 127) / 128;
+  const int nw = bwd_waves(a.Sk);
+  const int nkb = (a.Sk + 32 * nw - 1) / (32 * nw);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  dim3 gpre((unsigned)((rows + 3) / 4));
+  dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
   dim3 grid(nkb, a.B * a.H);
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
   dim3 gfin(ew_grid(per / 4, 256));
+#define FFK_ATTN_BWD(DD)                                                                                 \
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, gpre, dim3(256), 0, st, a);                               \
+  if (nw == 8) hipLaunchKernelGGL((attn_bwd_kernel<DD, 8>), grid, dim3(512), 0, st, a);                 \
+  else hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                         \
+  hipLaunchKernelGGL(attn_dq_finish_kernel<DD>, gfin, dim3(256), 0, st, a, nkb);
   if (a.D == 64) {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
+    FFK_ATTN_BWD(64)
   } else if (a.D == 128) {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, gpre, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
+    FFK_ATTN_BWD(128)
   }
+#undef FFK_ATTN_BWD
 }
 
 }  // namespace ffk

@@ -33,7 +33,7 @@ T* ptr(const optional<Tensor>& t) {
 void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> Z, int64_t M, int64_t N,
           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t batch,
           bool a_k, bool b_k, double alpha, double beta, int64_t act, int64_t splitk, optional<Tensor> ws,
-          bool big) {
+          int64_t impl) {
   check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A/B must be bf16");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm: C must be bf16/fp32");
@@ -61,7 +61,7 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
   p.out_f32 = C.scalar_type() == at::kFloat;
   p.a_bytes = A.numel() * 2;
   p.b_bytes = B.numel() * 2;
-  p.allow_big = big;
+  p.impl = (int)impl;
   p.splitk = 1;
   if (splitk > 1 && ws.has_value() && ws->defined()) {
     TORCH_CHECK(ws->numel() * ws->element_size() >= ffk::gemm_workspace_bytes(M, N, K, batch, splitk),
@@ -72,14 +72,23 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
   ffk::gemm_bf16(p, cur_stream());
 }
 
-int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch) {
-  return ffk::gemm_pick_splitk(M, N, K, batch);
+int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t impl) {
+  return ffk::gemm_pick_splitk(M, N, K, batch, (int)impl);
 }
 
 void unary_fwd(Tensor x, Tensor y, int64_t op, double s) {
   check_dev(x, "x");
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous());
   ffk::unary_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), x.numel(), op, s, cur_stream());
+}
+void bias_act_fwd(Tensor z, optional<Tensor> bias, optional<Tensor> zout, Tensor y, int64_t rows, int64_t cols,
+                  int64_t act) {
+  check_dev(z, "z");
+  TORCH_CHECK(z.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && cols % 8 == 0);
+  TORCH_CHECK(z.numel() >= rows * cols && y.numel() >= rows * cols && z.is_contiguous() && y.is_contiguous());
+  TORCH_CHECK(!bias || bias->numel() >= cols);
+  ffk::bias_act_fwd(z.data_ptr(), ptr(bias), bias && bias->scalar_type() == at::kBFloat16, ptr(zout), y.data_ptr(),
+                    rows, cols, act, cur_stream());
 }
 void unary_bwd(Tensor x, Tensor y, Tensor dy, Tensor dx, int64_t op, double s, bool acc) {
   TORCH_CHECK(x.numel() == dx.numel() && dy.numel() == dx.numel() && y.numel() == dx.numel());
@@ -247,9 +256,9 @@ void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
   a.dk = (uint16_t*)dk.data_ptr(); a.dk_sb = dks[0]; a.dk_sh = dks[1]; a.dk_ss = dks[2];
   a.dv = (uint16_t*)dv.data_ptr(); a.dv_sb = dvs[0]; a.dv_sh = dvs[1]; a.dv_ss = dvs[2];
   a.lse = lse.data_ptr<float>();
-  const int nkb = (Sk + 127) / 128;
+  const int64_t ws_floats = ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D);
   a.dq_acc = ws.data_ptr<float>();
-  a.delta = a.dq_acc + (int64_t)nkb * B * H * Sq * D;
+  a.delta = a.dq_acc + ws_floats - (int64_t)B * H * Sq;  // layout: [nkb partial dQ slabs][delta]
   a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.D = D; a.scale = scale; a.causal = causal;
   ffk::attn_bwd(a, cur_stream());
 }
@@ -261,8 +270,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("Z"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
-        py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("big") = true);
-  m.def("gemm_pick_splitk", &gemm_pick_splitk);
+        py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2);
+  m.def("gemm_pick_splitk", &gemm_pick_splitk, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch"),
+        py::arg("impl") = 2);
   m.def("unary_fwd", &unary_fwd);
   m.def("unary_bwd", &unary_bwd);
   m.def("binary_fwd", &binary_fwd);
@@ -271,6 +281,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("bias_act_fwd", &bias_act_fwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("softmax_fwd", &softmax_fwd);

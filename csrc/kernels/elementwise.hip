@@ -360,6 +360,37 @@ int bias_act_bwd_chunks(int rows, int cols) {
   return gy;
 }
 
+// Epilogue pass for library GEMMs: zb = z + bias[col] (stored back if zout), y = act(zb).
+// bf16, cols % 8 == 0: one 16-B vector per thread-step. In place (y == z) is allowed.
+__global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __restrict__ bias, int bias_bf16,
+                                    bf16_t* zout, bf16_t* y, int64_t rows, int cols, int act) {
+  const int64_t nv = rows * (int64_t)cols / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t e = v * 8;
+    const int c = (int)(e % cols);
+    float x[8];
+    load16(z + e, x);
+    if (bias) {
+      if (bias_bf16) {
+        float b[8];
+        load16((const bf16_t*)bias + c, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] += b[j];
+      } else {
+        const float4 b0 = *reinterpret_cast<const float4*>((const float*)bias + c);
+        const float4 b1 = *reinterpret_cast<const float4*>((const float*)bias + c + 4);
+        x[0] += b0.x; x[1] += b0.y; x[2] += b0.z; x[3] += b0.w;
+        x[4] += b1.x; x[5] += b1.y; x[6] += b1.z; x[7] += b1.w;
+      }
+      if (zout) store16(zout + e, x);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = act_fwd(act, x[j]);
+    store16(y + e, x);
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 #define FFK_DT_DISPATCH(dt, ...)                        \
   do {                                                  \
@@ -438,6 +469,13 @@ void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t 
                        (T*)dx, n, rate, accumulate);
   });
 }
+void bias_act_fwd(const void* z, const void* bias, int bias_bf16, void* zout, void* y, int64_t rows, int cols,
+                  int act, hipStream_t st) {
+  if (rows == 0 || cols == 0) return;
+  hipLaunchKernelGGL(bias_act_fwd_kernel, dim3(ew_grid(rows * cols / 8, 256)), dim3(256), 0, st, (const bf16_t*)z,
+                     bias, bias_bf16, (bf16_t*)zout, (bf16_t*)y, rows, cols, act);
+}
+
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
                   int act, hipStream_t st) {
   if (rows == 0 || cols == 0) return;

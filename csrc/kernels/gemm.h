@@ -24,12 +24,14 @@ struct GemmArgs {
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
-  bool allow_big = true;
+  int impl = 2;  // 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
 };
 
 void gemm_bf16(GemmArgs p, hipStream_t stream);
 int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk);
-int gemm_pick_splitk(int M, int N, int K, int batch);
+int gemm_pick_splitk(int M, int N, int K, int batch, int impl = 2);
 bool gemm_big_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+bool gemm256_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+int gemm256_bn(int M, int N, int batch, int splitk);
 
 }  // namespace ffk

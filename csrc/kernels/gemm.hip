@@ -347,11 +347,16 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
   return (int64_t)M * N * batch * splitk * 4;
 }
 
-int gemm_pick_splitk(int M, int N, int K, int batch) {
-  // tile count of the kernel that will run (256x128 DMA kernel when K % 64 == 0)
-  const bool big = (K % 64 == 0);
-  const int tiles = big ? ((M + 255) / 256) * ((N + 127) / 128) * batch
-                        : ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
+int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
+  // tile count of the kernel that will run
+  int64_t tiles;
+  if (impl == 2 && K % 32 == 0) {
+    tiles = (int64_t)((M + 255) / 256) * ((N + gemm256_bn(M, N, batch, 1) - 1) / gemm256_bn(M, N, batch, 1)) * batch;
+  } else if (impl >= 1 && K % 64 == 0) {
+    tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  } else {
+    tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
+  }
   if (tiles >= 256 || K < 1024) return 1;
   // minimise (waves of 256 CUs) / split, with a small charge per split for the fp32 slab reduce
   int best = 1;
@@ -361,6 +366,13 @@ int gemm_pick_splitk(int M, int N, int K, int batch) {
     if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
   }
   return best;
+}
+
+static bool try_large(const GemmArgs& p, bool a_al, bool b_al, hipStream_t stream) {
+  if (!(a_al && b_al && p.a_bytes > 0)) return false;
+  if (p.impl == 2 && gemm256_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
+  if (p.impl >= 1 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
+  return false;
 }
 
 void gemm_bf16(GemmArgs p, hipStream_t stream) {
@@ -383,8 +395,7 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   if (p.splitk > 1 && p.ws != nullptr) {
     p.kchunk = ((p.K + p.splitk - 1) / p.splitk + BK - 1) / BK * BK;
     dim3 grid(tm * tn, p.batch * p.splitk);
-    if (!(p.allow_big && a_al && b_al && p.a_bytes > 0 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)))
-      dispatch_layout<2>(p, grid, stream, a_al, b_al);
+    if (!try_large(p, a_al, b_al, stream)) dispatch_layout<2>(p, grid, stream, a_al, b_al);
     const int64_t total = (int64_t)p.M * p.N * p.batch;
     if (p.out_f32) hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
     else hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
@@ -392,7 +403,7 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   }
   p.splitk = 1;
   p.kchunk = p.K;
-  if (p.allow_big && a_al && b_al && p.a_bytes > 0 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)) return;
+  if (try_large(p, a_al, b_al, stream)) return;
   dim3 grid(tm * tn, p.batch);
   if (p.out_f32) dispatch_layout<1>(p, grid, stream, a_al, b_al);
   else dispatch_layout<0>(p, grid, stream, a_al, b_al);

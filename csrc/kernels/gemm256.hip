@@ -1,0 +1,366 @@
+// 256 x {256x32, 128x64} bf16 MFMA GEMM, 8 waves in two ping-pong groups, 4/3-deep LDS-DMA ring.
+//
+// Why this structure (measured on the 256x128x64 kernel of gemm_big.hip with rocprofv3 --pmc,
+// profiles/gemm_pmc_r1.txt): its waves spent ~32 % of their cycles parked at the per-K-tile
+// barrier / vmcnt wait and only ~24 % issuing, while hipBLASLt's kernel parks ~16 %. Two waves
+// share each SIMD and the single barrier per K-tile lines them up, so both read LDS at the same
+// time and both issue MFMAs at the same time. Here:
+//   * tile 256(M) x BN(N) x 32(K); waves = 2 (M) x 4 (N), 128 x BN/4 outputs per wave
+//     (8 x BN/64 mfma_f32_16x16x32_bf16 fragments; operands swapped so a lane owns 4 consecutive
+//     output columns -> 8-byte stores);
+//   * each K-tile is two phases {LDS reads; barrier; 16 MFMAs; barrier}. Waves 4-7 run one
+//     barrier behind waves 0-3 (one extra barrier at the start, balanced at the end), and waves w
+//     and w+4 sit on the same SIMD (waves are dealt to SIMDs round-robin), so on every SIMD one
+//     wave issues MFMAs while the other reads its next fragments — the ping-pong of
+//     cdna_hip_programming.md "The 256^2 8-phase template"; s_setprio(1) around the MFMA bursts;
+//   * LDS reads complete (lgkmcnt(0)) before each barrier, so a barrier proves every earlier read
+//     of a ring slot is done: the DMA that refills slot (t+3)%4 (issued in tile t's second phase)
+//     can never overwrite data a lagging wave still has to read;
+//   * operands arrive by buffer_load ... lds (16 B / lane, 1 KiB per wave instruction, hardware
+//     zero-fill past the end of the buffer); 4 slots of 32 KiB = 128 KiB in flight, tile t+1 is
+//     waited for (counted vmcnt, never 0 in steady state) one phase before its first read;
+//   * K-contiguous tiles are stored as 64-B rows with 16-B chunk ^ (((row >> 2) & 1) << 1): an
+//     exhaustive search over chunk XORs of row bits for the four ds_read_b128 lane groups of the
+//     16x16x32 operand pattern (16 rows x 4 chunks) gives this as conflict-free; MN-contiguous
+//     tiles use 128-wide halves of 256-B rows with the T10 image (b) XOR, read by
+//     ds_read_b64_tr_b16 (same image as gemm_big.hip);
+//   * XCD-aware bijective block remap + GROUP_M = 8 tile order (per-XCD L2 reuse).
+// Requires K % BK == 0 (split-K chunks are multiples of 64), 16-B aligned operand rows,
+// operands < 2 GiB. Epilogue contract identical to gemm.hip (bias, activation, pre-activation
+// store Z, alpha/beta, bf16 or fp32 C, fp32 split-K slabs).
+#include "common.h"
+#include "gemm.h"
+
+namespace ffk {
+namespace g256 {
+
+constexpr int BM = 256, NT = 512;
+
+// K-tile geometry per output-tile width: BN = 256 -> BK = 32 with a 4-slot ring (4 x 32 KiB);
+// BN = 128 -> BK = 64 with a 3-slot ring (3 x 48 KiB), so that each phase still issues 16 MFMAs
+// per wave (8 would be too short to cover the other group's LDS reads).
+template <int BN> struct Geo;
+template <> struct Geo<256> { static constexpr int BK = 32, NBUF = 4; };
+template <> struct Geo<128> { static constexpr int BK = 64, NBUF = 3; };
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// 16-B chunk swizzle of a K-contiguous row of BK bf16 (64-B rows: 4 chunks, 128-B rows: 8 chunks)
+template <int BK>
+__device__ __forceinline__ int swz_k(int row) {
+  if constexpr (BK == 32) return ((row >> 2) & 1) << 1;
+  else return row & 7;
+}
+__device__ __forceinline__ int swz_mn(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// One 1-KiB DMA piece of an operand tile. K-contiguous: 1024 / (2 BK) rows of 2 BK bytes.
+// MN-contiguous: 4 k-rows of one 128-wide half (256 B each).
+template <bool KCONT, int BK>
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, char* lds_tile, int64_t ld, int mn0, int k0,
+                                          int piece, int lane) {
+  constexpr int CPR = BK / 8;  // 16-B chunks per K-contiguous row
+  int64_t elem;
+  if (KCONT) {
+    const int row = piece * (64 / CPR) + lane / CPR;
+    const int c = (lane % CPR) ^ swz_k<BK>(row);
+    elem = (int64_t)(mn0 + row) * ld + k0 + c * 8;
+  } else {
+    const int half = piece / (BK / 4);
+    const int krow = (piece % (BK / 4)) * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_mn(krow);
+    elem = (int64_t)(k0 + krow) * ld + mn0 + half * 128 + c * 8;
+  }
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(lds_tile + piece * 1024), 16, (int)(elem * 2), 0, 0, 0);
+}
+
+// 16 (rows along M or N) x 32 (k, sub-step kk of the K-tile) fragment for mfma_f32_16x16x32_bf16.
+template <bool KCONT, int BK>
+__device__ __forceinline__ bf16x8 frag(const char* tile, int r0, int kk, int lane) {
+  if (KCONT) {
+    const int row = r0 + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(tile + row * (BK * 2) + ((c ^ swz_k<BK>(row)) << 4));
+  } else {
+    const char* hl = tile + (r0 >> 7) * (BK * 256);
+    const int rr = r0 & 127;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int chunk = (rr >> 3) + (p >> 1);
+    bf16x8 out;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int krow = 32 * kk + 8 * g + 4 * hf + q;
+      const int off = krow * 256 + ((chunk ^ swz_mn(krow)) << 4) + 8 * (p & 1);
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(hl + off));
+      bf16x4 b = __builtin_bit_cast(bf16x4, v);
+      out[4 * hf + 0] = b[0];
+      out[4 * hf + 1] = b[1];
+      out[4 * hf + 2] = b[2];
+      out[4 * hf + 3] = b[3];
+    }
+    return out;
+  }
+}
+
+__device__ __forceinline__ void tile_coords(int bid, int tm, int tn, int& tile_m, int& tile_n) {
+  const int nwg = tm * tn;
+  bid = xcd_remap(bid, nwg);
+  constexpr int GM = 8;
+  const int per_group = GM * tn;
+  const int group = bid / per_group;
+  const int first_m = group * GM;
+  const int gsize = min(tm - first_m, GM);
+  const int in_g = bid % per_group;
+  tile_m = first_m + in_g % gsize;
+  tile_n = in_g / gsize;
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N == 0 || N == 4 || N == 6 || N == 8 || N == 12, "add the vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+// Wait until at most `tiles_after` tiles' worth of this wave's DMAs are outstanding.
+template <int PW, int NBUF>
+__device__ __forceinline__ void wait_tiles(int tiles_after) {
+  if constexpr (NBUF >= 4) {
+    if (tiles_after >= 2) { wait_vm<2 * PW>(); return; }
+  }
+  if (tiles_after >= 1) wait_vm<PW>();
+  else wait_vm<0>();
+}
+
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <bool A_K, bool B_K, int BN, int OUT_MODE>
+__global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
+  constexpr int BK = Geo<BN>::BK, NBUF = Geo<BN>::NBUF, KK = BK / 32;
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_PIECES = A_BYTES / 1024, PIECES = STAGE / 1024;
+  constexpr int PW = PIECES / 8;  // DMA instructions per wave per K-tile
+  constexpr int WN = BN / 4;      // output columns per wave
+  constexpr int NF = WN / 16;     // N fragments per wave
+  static_assert(PIECES % 8 == 0, "pieces must split evenly over 8 waves");
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
+  int tile_m, tile_n;
+  tile_coords(blockIdx.x, tm, tn, tile_m, tile_n);
+  const int z = blockIdx.y;
+  const int b = z / p.splitk, ks = z % p.splitk;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = ks * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = max(0, (kend - kbeg) / BK);
+
+  const bf16_t* Ab = p.A + (int64_t)b * p.sA;
+  const bf16_t* Bb = p.B + (int64_t)b * p.sB;
+  const int64_t a_rem = a_bytes - (int64_t)b * p.sA * 2;
+  const int64_t b_rem = b_bytes - (int64_t)b * p.sB * 2;
+  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)min(a_rem, (int64_t)0x7fffffff), 0x00020000);
+  __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)min(b_rem, (int64_t)0x7fffffff), 0x00020000);
+
+  f32x4 acc[8][NF];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int t) {
+    char* st = smem + (t % NBUF) * STAGE;
+    const int k0 = kbeg + t * BK;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int piece = wave * PW + i;
+      if (piece < A_PIECES) dma_piece<A_K, BK>(ra, st, p.lda, m0, k0, piece, lane);
+      else dma_piece<B_K, BK>(rb, st + A_BYTES, p.ldb, n0, k0, piece - A_PIECES, lane);
+    }
+  };
+
+  // prologue: tiles 0..2 in flight, tile 0 landed everywhere before the first read
+  const int pre = min(nk, NBUF - 1);
+  for (int t = 0; t < pre; ++t) issue(t);
+  wait_tiles<PW, NBUF>(pre - 1);
+  barrier();
+  if (wr == 1) barrier();  // ping-pong: the second wave group runs one barrier behind
+
+  bf16x8 af[KK][4], bfr[KK][NF];
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t % NBUF) * STAGE;
+    // ---- phase 0: rows 0..63 of this wave's 128
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) bfr[kk][j] = frag<B_K, BK>(cur + A_BYTES, wc * WN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag<A_K, BK>(cur, wr * 128 + i * 16, kk, lane);
+    }
+    lgkm0();
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---- phase 1: rows 64..127; refill slot (t+NBUF-1)%NBUF, make sure tile t+1 has landed
+    if (t + NBUF - 1 < nk) issue(t + NBUF - 1);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag<A_K, BK>(cur, wr * 128 + 64 + i * 16, kk, lane);
+    wait_tiles<PW, NBUF>(min(nk, t + NBUF) - (t + 2));
+    lgkm0();
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  }
+  if (wr == 0) barrier();  // balance the barrier count of the two groups
+
+  const int mrow = m0 + wr * 128 + (lane & 15);
+  const int ncol = n0 + wc * WN + (lane >> 4) * 4;
+  if (OUT_MODE == 2) {
+    float* W = p.ws + (int64_t)z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + i * 16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int n = ncol + j * 16;
+        float* dst = W + (int64_t)m * p.N + n;
+        if (n + 3 < p.N && (p.N & 3) == 0) {
+          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha,
+                                                        acc[i][j][2] * p.alpha, acc[i][j][3] * p.alpha);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) if (n + r < p.N) dst[r] = acc[i][j][r] * p.alpha;
+        }
+      }
+    }
+    return;
+  }
+  typedef typename std::conditional<OUT_MODE == 0, bf16_t, float>::type OutT;
+  OutT* C = reinterpret_cast<OutT*>(p.C) + (int64_t)b * p.sC;
+  bf16_t* Zp = p.Z ? reinterpret_cast<bf16_t*>(p.Z) + (int64_t)b * p.sC : nullptr;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + i * 16;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= p.N) continue;
+      float v[4];
+      const bool full = p.vec_ok && (n + 3 < p.N);
+      OutT* dst = C + (int64_t)m * p.ldc + n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = acc[i][j][r] * p.alpha;
+        if (p.beta != 0.f && n + r < p.N) x += p.beta * Cvt<OutT>::to_f(dst[r]);
+        if (p.bias && n + r < p.N)
+          x += p.bias_bf16 ? bf2f(((const bf16_t*)p.bias)[n + r]) : ((const float*)p.bias)[n + r];
+        v[r] = x;
+      }
+      if (Zp) {
+        bf16_t* zd = Zp + (int64_t)m * p.ldc + n;
+        if (full) {
+          ushort4 o; o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
+          *reinterpret_cast<ushort4*>(zd) = o;
+        } else {
+          for (int r = 0; r < 4; ++r) if (n + r < p.N) zd[r] = f2bf(v[r]);
+        }
+      }
+      if (p.act != ACT_NONE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fwd(p.act, v[r]);
+      }
+      if (full) {
+        if (OUT_MODE == 0) {
+          ushort4 o; o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
+          *reinterpret_cast<ushort4*>(dst) = o;
+        } else {
+          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) if (n + r < p.N) dst[r] = Cvt<OutT>::from_f(v[r]);
+      }
+    }
+  }
+}
+
+template <int BN, int MODE>
+static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm256_kernel<true, true, BN, MODE>), grid, dim3(NT), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm256_kernel<true, false, BN, MODE>), grid, dim3(NT), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm256_kernel<false, true, BN, MODE>), grid, dim3(NT), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm256_kernel<false, false, BN, MODE>), grid, dim3(NT), 0, s, p, ab, bb);
+}
+
+template <int BN>
+static void launch_mode(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb, int mode) {
+  if (mode == 2) launch<BN, 2>(p, grid, s, ab, bb);
+  else if (mode == 1) launch<BN, 1>(p, grid, s, ab, bb);
+  else launch<BN, 0>(p, grid, s, ab, bb);
+}
+
+}  // namespace g256
+
+// Tile width for the 256-row kernel: time ~ (waves of 256 CUs) x (per-tile time), a 256x128 tile
+// costing ~0.55 of a 256x256 one (half the MFMAs, a little more LDS traffic per flop).
+int gemm256_bn(int M, int N, int batch, int splitk) {
+  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch * splitk;
+  const int64_t t128 = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch * splitk;
+  const double c256 = (double)((t256 + 255) / 256);
+  const double c128 = 0.55 * (double)((t128 + 255) / 256);
+  return c128 < c256 ? 128 : 256;
+}
+
+bool gemm256_bf16(const GemmArgs& p0, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+  using namespace g256;
+  GemmArgs p = p0;
+  const int bn = gemm256_bn(p.M, p.N, p.batch, p.splitk > 1 && p.ws ? p.splitk : 1);
+  if (p.K % (bn == 256 ? 32 : 64) != 0 || a_bytes > 0x7fffffffLL || b_bytes > 0x7fffffffLL || a_bytes <= 0 || b_bytes <= 0) return false;
+  if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15) || p.lda % 8 || p.ldb % 8 || p.sA % 8 || p.sB % 8) return false;
+  if (!p.a_kcontig && p.M % 8) return false;
+  if (!p.b_kcontig && p.N % 8) return false;
+  const bool split = p.splitk > 1 && p.ws != nullptr;
+  if (!split) p.splitk = 1;
+  p.kchunk = split ? ((p.K + p.splitk - 1) / p.splitk + 63) / 64 * 64 : p.K;
+  const int tm = (p.M + BM - 1) / BM, tn = (p.N + bn - 1) / bn;
+  dim3 grid(tm * tn, p.batch * p.splitk);
+  const int mode = split ? 2 : (p.out_f32 ? 1 : 0);
+  if (bn == 256) launch_mode<256>(p, grid, stream, a_bytes, b_bytes, mode);
+  else launch_mode<128>(p, grid, stream, a_bytes, b_bytes, mode);
+  return true;
+}
+
+}  // namespace ffk

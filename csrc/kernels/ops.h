@@ -30,6 +30,9 @@ void dropout_fwd(int dt, const void* x, void* y, uint8_t* mask, int64_t n, float
 void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float rate, int accumulate,
                  hipStream_t st);
 // dbias += colsum(dz); ws: fp32 slab of bias_act_bwd_chunks(rows, cols) * cols floats
+// y = act(z + bias) (bf16, cols % 8 == 0); zout (may be z) receives z + bias when bias is given
+void bias_act_fwd(const void* z, const void* bias, int bias_bf16, void* zout, void* y, int64_t rows, int cols,
+                  int act, hipStream_t st);
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
                   int act, hipStream_t st);
 int bias_act_bwd_chunks(int rows, int cols);

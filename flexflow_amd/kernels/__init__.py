@@ -71,6 +71,9 @@ def act_grad_ref(z, act):
 import os as _os
 
 _TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
+# our kernels: 256-row ping-pong (csrc/kernels/gemm256.hip), 256x128 LDS-DMA (gemm_big.hip), 128x128
+IMPLS = {"k256": 2, "big": 1, "128": 0}
+IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []
 
@@ -131,6 +134,15 @@ def _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batc
         Cv.copy_(r)
 
 
+def _lib_gemm_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act):
+    """Plain library GEMM into the pre-activation buffer, then one fused pass of ours
+    (z += bias; C = act(z)): for shapes where the vendor GEMM plus one elementwise pass beats our
+    fused epilogue (and torch's bias GEMM, which is slower than its plain one)."""
+    zbuf = Z if Z is not None else C
+    _lib_gemm(A, B, zbuf, M, N, K, a_k, b_k, lda, ldb, N, 1.0, 0.0, None, 1, 0, 0, 0)
+    ext().bias_act_fwd(zbuf, bias, zbuf if bias is not None else None, C, M, N, act)
+
+
 def _time(fn, reps=8):
     fn()
     fn()
@@ -148,19 +160,19 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
     """C = act(alpha*op(A).op(B) + beta*C + bias); raw strided views (see csrc/kernels/gemm.hip).
 
     On the device, each call site (shape, layouts, epilogue) is autotuned once, outside graph
-    capture, among our 256x128 LDS-DMA MFMA kernel, our 128x128 MFMA kernel and — for plain GEMMs
-    without a fused activation / pre-activation store — the vendor library GEMM."""
+    capture, among our MFMA kernels (IMPLS) and — for plain GEMMs without a fused activation /
+    pre-activation store — the vendor library GEMM. splitk=None lets each kernel pick its split."""
     if native(C) and A.dtype == torch.bfloat16:
         X = ext()
-        if splitk is None:
-            splitk = X.gemm_pick_splitk(M, N, K, batch) if batch == 1 else 1
 
-        def ours(big, out=C):
+        def ours(impl, out=C, sk=None):
+            s = sk if sk is not None else (splitk if splitk is not None else
+                                           (X.gemm_pick_splitk(M, N, K, batch, impl) if batch == 1 else 1))
             ws = None
-            if splitk > 1:
-                ws = torch.empty(M * N * batch * splitk, device=C.device, dtype=torch.float32)
+            if s > 1:
+                ws = torch.empty(M * N * batch * s, device=C.device, dtype=torch.float32)
             X.gemm(A, B, out, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act,
-                   splitk, ws, big)
+                   s, ws, impl)
 
         key = (M, N, K, a_k, b_k, lda, ldb, ldc, batch, C.dtype, bias is not None, Z is not None, act,
                beta != 0.0, splitk)
@@ -168,13 +180,19 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
         if choice is None:
             plain = act == ACT_NONE and Z is None and sC in (0, M * N) and ldc == N
             if not _TUNE or torch.cuda.is_current_stream_capturing():
-                choice = "big"
+                choice = IMPL_DEFAULT
             else:
                 scratch = torch.zeros_like(C)
-                cands = {"big": lambda: ours(True, scratch), "128": lambda: ours(False, scratch)}
+                cands = {k: (lambda i=i: ours(i, scratch)) for k, i in IMPLS.items()}
                 if plain:
                     cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
                                                      bias, batch, sA, sB, sC)
+                if (act != ACT_NONE or bias is not None) and alpha == 1.0 and beta == 0.0 and batch == 1 and \
+                        ldc == N and N % 8 == 0 and C.dtype == torch.bfloat16 and \
+                        (Z is None or Z.dtype == torch.bfloat16):
+                    zs = torch.empty_like(C) if Z is not None else None
+                    cands["lib_act"] = lambda: _lib_gemm_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda, ldb, bias,
+                                                             act)
                 times = {k: _time(f) for k, f in cands.items()}
                 choice = min(times, key=times.get)
                 TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
@@ -182,8 +200,10 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             _tuned[key] = choice
         if choice == "lib":
             _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC)
+        elif choice == "lib_act":
+            _lib_gemm_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act)
         else:
-            ours(choice == "big")
+            ours(IMPLS[choice])
         return C
     # reference / fp32 path (library GEMM on device, plain torch on CPU)
     Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)

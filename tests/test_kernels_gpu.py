@@ -16,26 +16,48 @@ def _rel(a, b):
 
 
 def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0, act=10, batch=1, sA=0, sB=0,
-          sC=0, splitk=1, ws=None):
+          sC=0, splitk=1, ws=None, impl=2):
     lda = A.shape[-1]
     ldb = B.shape[-1]
     ldc = C.shape[-1]
-    C_.gemm(A, B, C, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act, splitk, ws)
+    C_.gemm(A, B, C, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act, splitk, ws,
+            impl)
 
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
                                    (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
-def test_gemm_layouts(ffC, a_k, b_k, M, N, K):
+@pytest.mark.parametrize("impl", [2, 1, 0])
+def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
     Bn = torch.randn(N, K, device=DEV).bfloat16()
     A = Am if a_k else Am.t().contiguous()
     B = Bn if b_k else Bn.t().contiguous()
     C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    _gemm(ffC, A, B, C, M, N, K, a_k, b_k)
+    _gemm(ffC, A, B, C, M, N, K, a_k, b_k, impl=impl)
     ref = Am.float() @ Bn.float().t()
     assert _rel(C, ref) < 1e-2
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 4096, 1), (8192, 3072, 1024, 2), (1024, 4096, 8192, 4),
+                                          (1000, 600, 1056, 1), (2048, 2048, 2048, 3)])
+def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk):
+    """256-row ping-pong kernel: BERT-Large shapes (both tile widths), split-K slabs, edge tiles."""
+    torch.manual_seed(11)
+    Am = torch.randn(M, K, device=DEV).bfloat16()
+    Bn = torch.randn(N, K, device=DEV).bfloat16()
+    A = Am if a_k else Am.t().contiguous()
+    B = Bn if b_k else Bn.t().contiguous()
+    ref = Am.float() @ Bn.float().t()
+    ws = torch.empty(M * N * splitk, device=DEV) if splitk > 1 else None
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _gemm(ffC, A, B, C, M, N, K, a_k, b_k, splitk=splitk, ws=ws, impl=2)
+    assert _rel(C, ref) < 1e-2
+    C32 = torch.ones(M, N, device=DEV)
+    _gemm(ffC, A, B, C32, M, N, K, a_k, b_k, beta=1.0, splitk=splitk, ws=ws, impl=2)
+    assert _rel(C32, ref + 1.0) < 1e-3
 
 
 def test_gemm_epilogue_bias_gelu_f32_beta(ffC):
@@ -293,3 +315,27 @@ def test_adam_sgd_embedding_dropout(ffC):
     keep = mask.float().mean().item()
     assert abs(keep - 0.75) < 0.01
     assert torch.allclose(y[mask.bool()], torch.full_like(y[mask.bool()], 1 / 0.75))
+
+
+@pytest.mark.parametrize("act,with_bias,with_z", [(14, True, True), (11, False, True), (10, True, False)])
+def test_lib_gemm_bias_act_epilogue(ffC, act, with_bias, with_z):
+    """Library GEMM + our fused bias/activation pass (the tuner's 'lib_act' candidate) and the
+    autotuned wrapper agree with the fp32 reference."""
+    from flexflow_amd import kernels as Kn
+    torch.manual_seed(12)
+    M, N, K = 512, 384, 256
+    A = torch.randn(M, K, device=DEV).bfloat16()
+    B = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV) if with_bias else None
+    z = A.float() @ B.float().t() + (bias if with_bias else 0.0)
+    ref = Kn.act_ref(z, act)
+    for fn in ("lib_act", "tuned"):
+        C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        Z = torch.empty_like(C) if with_z else None
+        if fn == "lib_act":
+            Kn._lib_gemm_act(A, B, C, Z, M, N, K, True, True, K, K, bias, act)
+        else:
+            Kn.gemm(A, B, C, M, N, K, True, True, K, K, N, bias=bias, Z=Z, act=act)
+        assert _rel(C, ref) < 1e-2
+        if with_z:
+            assert _rel(Z, z) < 1e-2
