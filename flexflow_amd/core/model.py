@@ -426,18 +426,25 @@ class FFModel:
         if seq_length is not None:
             self.iter_config_seq_length = seq_length
         self.executor.forward()
+        self._metrics_pending = True
 
     def zero_gradients(self):
         self.executor.zero_gradients()
 
     def backward(self, seq_length=None):
-        self.executor.backward()
+        self.executor.backward()  # loss gradient + metrics of the last forward
+        self._metrics_pending = False
 
     def update(self):
         self.executor.update(self.optimizer)
 
     def compute_metrics(self):
-        return None  # metrics accumulate on device during backward; folded lazily
+        """Metrics of the last forward (reference FFModel::compute_metrics). During training they
+        are produced by backward's fused loss kernel; after a forward-only pass (evaluation) the
+        loss/metric kernels run here."""
+        if getattr(self, "_metrics_pending", False):
+            self.executor.compute_loss_grad()
+            self._metrics_pending = False
 
     def reset_metrics(self):
         self.executor.reset_metrics()

@@ -1,0 +1,46 @@
+"""Keras metrics (reference keras/metrics.py) -> MetricsType."""
+from __future__ import annotations
+
+from ..type import MetricsType
+
+
+class Metric:
+    type = None
+
+
+class Accuracy(Metric):
+    type = MetricsType.METRICS_ACCURACY
+
+
+class CategoricalCrossentropy(Metric):
+    type = MetricsType.METRICS_CATEGORICAL_CROSSENTROPY
+
+
+class SparseCategoricalCrossentropy(Metric):
+    type = MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY
+
+
+class MeanSquaredError(Metric):
+    type = MetricsType.METRICS_MEAN_SQUARED_ERROR
+
+
+class RootMeanSquaredError(Metric):
+    type = MetricsType.METRICS_ROOT_MEAN_SQUARED_ERROR
+
+
+class MeanAbsoluteError(Metric):
+    type = MetricsType.METRICS_MEAN_ABSOLUTE_ERROR
+
+
+_BY_NAME = {"accuracy": Accuracy, "categorical_crossentropy": CategoricalCrossentropy,
+            "sparse_categorical_crossentropy": SparseCategoricalCrossentropy, "mean_squared_error": MeanSquaredError,
+            "mse": MeanSquaredError, "root_mean_squared_error": RootMeanSquaredError,
+            "mean_absolute_error": MeanAbsoluteError, "mae": MeanAbsoluteError}
+
+
+def get(spec):
+    if isinstance(spec, Metric):
+        return spec
+    if spec not in _BY_NAME:
+        raise ValueError(f"unsupported metric {spec!r}")
+    return _BY_NAME[spec]()

@@ -487,8 +487,27 @@ class Executor:
         for ar in self.arenas.values():
             ar.grad.zero_()
 
+    def _apply_regularizers(self):
+        """Keras-style weight regularizers (layer attr 'regularizer' with l1/l2): grad += 2*l2*w +
+        l1*sign(w) on the fp32 master copy, after the gradient all-reduce (the reference keeps the
+        regularizer on the layer but applies none)."""
+        for L in self.layers:
+            reg = L.attrs.get("regularizer")
+            if reg is None or not L.weights:
+                continue
+            l1, l2 = reg.grad_terms() if hasattr(reg, "grad_terms") else (0.0, float(reg))
+            w = L.weights[0]
+            if w.guid not in self.weight_loc:
+                continue
+            m, g, _ = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])
+            if l2:
+                g.add_(m, alpha=2.0 * l2)
+            if l1:
+                g.add_(torch.sign(m), alpha=l1)
+
     def update(self, optimizer):
         self.bucketer.flush()
+        self._apply_regularizers()
         optimizer.next()
         for ar in self.arenas.values():
             if ar.size:
