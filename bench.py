@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
     ap.add_argument("--no-hip-graphs", action="store_true")
     ap.add_argument("--compare-dp", action="store_true", help="also time pure data parallel (speedup vs DP)")
+    ap.add_argument("--verify-steps", type=int, default=4,
+                    help="N>1: time the searched strategy and data parallel for this many steps each and keep "
+                         "the faster (measurement-verified search; 0 disables)")
     return ap.parse_args()
 
 
@@ -140,7 +143,28 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    ff, gb, info = build(args, args.search)
+    verify = None
+    if world > 1 and args.search not in ("dp", "none") and args.verify_steps > 0:
+        # measurement-verified search: the simulator's pick is timed against data parallel on the
+        # real machine and the faster one is kept (FlexFlow's search also trusts measured op costs)
+        ff, gb, info = build(args, args.search)
+        label = describe(ff, world)
+        if label.startswith("dp"):
+            verify = {"searched": label, "chosen": label}
+        else:
+            t_s = timed(ff, args.verify_steps, 2, world) / args.verify_steps
+            ff_dp, _, _ = build(args, "dp")
+            t_d = timed(ff_dp, args.verify_steps, 2, world) / args.verify_steps
+            keep_dp = t_d < t_s
+            verify = {"searched": label, "searched_ms": round(t_s * 1e3, 3), "dp_ms": round(t_d * 1e3, 3),
+                      "chosen": f"dp{world}" if keep_dp else label}
+            if keep_dp:
+                del ff
+                ff = ff_dp
+            else:
+                del ff_dp
+    else:
+        ff, gb, info = build(args, args.search)
     el = timed(ff, args.steps, args.warmup, world)
     ms = el / args.steps * 1e3
     sps = gb * args.steps / el
@@ -163,7 +187,16 @@ def main():
     }
     if info["flops_per_sample"]:
         res["model_tflops_per_gpu"] = round(info["flops_per_sample"] * sps / world / 1e12, 2)
-    if args.compare_dp and world > 1:
+    rep = ff.search_report or {}
+    if rep.get("predicted_speedup_vs_dp") is not None:
+        res["search"] = {k: rep[k] for k in ("predicted_ms", "predicted_dp_ms", "predicted_speedup_vs_dp",
+                                             "candidates", "search_s", "measured_costs") if k in rep}
+    if verify is not None:
+        res["search_verification"] = verify
+        if "dp_ms" in verify:
+            res["speedup_vs_dp"] = round(verify["dp_ms"] / (ms if verify["chosen"] != f"dp{world}" else
+                                                             verify["dp_ms"]), 4)
+    if args.compare_dp and world > 1 and "speedup_vs_dp" not in res:
         del ff
         ff2, _, _ = build(args, "dp")
         el2 = timed(ff2, args.steps, args.warmup, world)

@@ -1,0 +1,76 @@
+"""bench.py contract on CPU: the single-process run and a 2-rank gloo run (the multi-process path the
+driver launches with torch.distributed.run on GPUs) both print one JSON line with the required
+fields; the searched strategy is compared with data parallel in the same run (--compare-dp)."""
+import io
+import json
+import os
+import socket
+import sys
+import tempfile
+from contextlib import redirect_stdout
+
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench_main(argv):
+    import bench
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    buf = io.StringIO()
+    try:
+        with redirect_stdout(buf):
+            bench.main()
+    finally:
+        sys.argv = old
+    return buf.getvalue()
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), CUDA_VISIBLE_DEVICES="")
+    import torch
+    torch.set_num_threads(1)
+    txt = _bench_main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--model", "bert-tiny", "--seq", "32",
+                       "--batch-per-gpu", "2", "--compare-dp"])
+    if rank == 0:
+        with open(out, "w") as f:
+            f.write(txt)
+
+
+def _check(line, n):
+    r = json.loads(line)
+    assert REQUIRED <= set(r), REQUIRED - set(r)
+    assert r["n_gpus"] == n and r["steps"] == 2 and r["warmup"] == 1 and r["value"] > 0
+    assert r["config"]["global_batch"] == 2 * n
+    return r
+
+
+def test_bench_single_process():
+    out = _bench_main(["--steps", "2", "--warmup", "1", "--model", "bert-tiny", "--seq", "32", "--batch-per-gpu", "2"])
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    _check(lines[0], 1)
+
+
+def test_bench_two_ranks_gloo():
+    out = os.path.join(tempfile.mkdtemp(), "b.txt")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    lines = [ln for ln in open(out).read().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    r = _check(lines[0], 2)
+    print(lines[0])
+    assert "speedup_vs_dp" in r and r["speedup_vs_dp"] > 0
