@@ -250,6 +250,25 @@ __global__ void attn_bwd_pre_kernel(AttnArgs a) {
   if (row < total && part == 0) a.delta[row] = s;
 }
 
+// dS^T image [key][64 queries] (128-B rows): byte offset of (key row, query q), q % 4 == 0. The
+// 8-B unit index is XORed with f(row) = row[2:0] | (row[1]^row[3])<<3 — found by exhaustive search
+// over linear XOR maps to be conflict-free both for the 8-B writes (16 consecutive key rows per
+// lane group, banks mod 32) and for the ds_read_b64_tr_b16 reads of the dQ stage (banks mod 64);
+// the unswizzled image cost ~57 % extra LDS cycles (SQ_LDS_BANK_CONFLICT, profiles/attn_pmc_r1.txt).
+// Workgroup barrier that orders LDS only: __syncthreads() also waits vmcnt(0), which here would
+// stall every q-tile on the dQ partial stores (and on the next tile's prefetch) for a full
+// memory round trip.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int dst_off(int row, int q) {
+  const int f = (row & 7) | ((((row >> 1) ^ (row >> 3)) & 1) << 3);
+  return row * 128 + (((q >> 2) ^ f) << 3) + (q & 3) * 2;
+}
+
 // NW waves x 32 keys per workgroup. NW = 8 (256 keys) halves the fp32 dQ partial slabs that
 // attn_dq_finish_kernel has to sum (the dominant HBM traffic of the backward at S = 512).
 template <int D, int NW>
@@ -258,14 +277,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   constexpr int QT = 64;       // queries per loop step
   constexpr int KB = 32 * NW;  // keys per workgroup
   constexpr int QB = QT * D * 2;
-  // LDS: Q tile, dO tile, K block image, dS^T image [KB][QT], lse/delta
-  __shared__ __attribute__((aligned(16))) char smem[2 * QB + KB * D * 2 + KB * QT * 2 + 2 * QT * 4];
-  char* q_l = smem;
-  char* do_l = smem + QB;
-  char* k_l = smem + 2 * QB;
+  // LDS: 2 x {Q tile, dO tile, lse, delta} (double-buffered: tile t+1 is fetched into registers
+  // while tile t is computed), K block image, dS^T image [KB][QT]
+  constexpr int TILE = 2 * QB + 2 * QT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + KB * QT * 2];
+  char* k_l = smem + 2 * TILE;
   char* ds_l = k_l + KB * D * 2;
-  float* lse_l = reinterpret_cast<float*>(ds_l + KB * QT * 2);
-  float* dl_l = lse_l + QT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
@@ -306,22 +323,42 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
   float* dq_part = a.dq_acc + (int64_t)blockIdx.x * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
 
+  TileStage<D, QT, NT> sq, sd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  auto fetch = [&](int t) {  // global -> registers
+    const int qbase = t * QT;
+    sq.load(Q, a.q_ss, qbase, a.Sq, tid);
+    sd.load(dO, a.do_ss, qbase, a.Sq, tid);
+    if (tid < QT) {
+      const int q = qbase + tid;
+      lse_r = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
+      dl_r = q < a.Sq ? DL[q] : 0.f;
+    }
+  };
+  auto stash = [&](int t) {  // registers -> LDS buffer t & 1
+    char* tb = smem + (t & 1) * TILE;
+    sq.store(tb, tid);
+    sd.store(tb + QB, tid);
+    if (tid < QT) {
+      reinterpret_cast<float*>(tb + 2 * QB)[tid] = lse_r;
+      reinterpret_cast<float*>(tb + 2 * QB)[QT + tid] = dl_r;
+    }
+  };
+  if (qt_begin < nqt) {
+    fetch(qt_begin);
+    stash(qt_begin);
+  }
+  __syncthreads();
+
   for (int t = qt_begin; t < nqt; ++t) {
     const int qbase = t * QT;
-    __syncthreads();  // previous iteration done with q_l/do_l/ds_l
-    {
-      TileStage<D, QT, NT> sq, sd;
-      sq.load(Q, a.q_ss, qbase, a.Sq, tid);
-      sd.load(dO, a.do_ss, qbase, a.Sq, tid);
-      sq.store(q_l, tid);
-      sd.store(do_l, tid);
-      if (tid < QT) {
-        const int q = qbase + tid;
-        lse_l[tid] = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
-        dl_l[tid] = q < a.Sq ? DL[q] : 0.f;
-      }
-    }
-    __syncthreads();
+    char* tb = smem + (t & 1) * TILE;
+    const char* q_l = tb;
+    const char* do_l = tb + QB;
+    const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
+    const float* dl_l = lse_l + QT;
+    const bool more = t + 1 < nqt;
+    if (more) fetch(t + 1);  // in flight during this tile's MFMAs
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       // S[q][key] and dP[q][key] for 32 queries x this wave's 32 keys
@@ -378,10 +415,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
         ushort4 o;
         o.x = f2bf(pacc[4 * g + 0]); o.y = f2bf(pacc[4 * g + 1]);
         o.z = f2bf(pacc[4 * g + 2]); o.w = f2bf(pacc[4 * g + 3]);
-        *reinterpret_cast<ushort4*>(ds_l + krow * (QT * 2) + ql * 2) = o;
+        *reinterpret_cast<ushort4*>(ds_l + dst_off(krow, ql)) = o;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's 128 keys; wave -> (qt, dt) tiles
     for (int tile = wave; tile < 2 * (D / 32); tile += NW) {
       const int qt = tile / (D / 32), dt = tile % (D / 32);
@@ -394,8 +431,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
           // tr read of dS^T [key][q]: 16-lane group G covers q cols 32qt + 16(G&1) + i, key rows
           const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
           const int kr = 16 * ks + 8 * h + qi;
-          const bf16x4 lo = tr_read(ds_l, kr * (QT * 2) + cq * 2);
-          const bf16x4 hi = tr_read(ds_l, (kr + 4) * (QT * 2) + cq * 2);
+          const bf16x4 lo = tr_read(ds_l, dst_off(kr, cq));
+          const bf16x4 hi = tr_read(ds_l, dst_off(kr + 4, cq));
           af[0] = lo[0]; af[1] = lo[1]; af[2] = lo[2]; af[3] = lo[3];
           af[4] = hi[0]; af[5] = hi[1]; af[6] = hi[2]; af[7] = hi[3];
         }
@@ -419,6 +456,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
         if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
       }
     }
+    if (more) stash(t + 1);  // other buffer: its last readers finished before this tile's first sync
+    lds_barrier();           // tile t+1 visible; dS^T reads of tile t done before it is rewritten
   }
   // causal: query tiles before qt_begin contribute nothing; zero their partial rows
   if (a.causal) {
@@ -483,7 +522,7 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
 }
 
 void attn_bwd(AttnArgs a, hipStream_t st) {
-  const int nw = bwd_waves(a.Sk);
+  const int nw = bwd_waves(a.Sk);  // only the 4-wave variant is instantiated
   const int nkb = (a.Sk + 32 * nw - 1) / (32 * nw);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
@@ -492,8 +531,7 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
   dim3 gfin(ew_grid(per / 4, 256));
 #define FFK_ATTN_BWD(DD)                                                                                 \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, gpre, dim3(256), 0, st, a);                               \
-  if (nw == 8) hipLaunchKernelGGL((attn_bwd_kernel<DD, 8>), grid, dim3(512), 0, st, a);                 \
-  else hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                         \
+  hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                              \
   hipLaunchKernelGGL(attn_dq_finish_kernel<DD>, gfin, dim3(256), 0, st, a, nkb);
   if (a.D == 64) {
     FFK_ATTN_BWD(64)

@@ -21,6 +21,7 @@ struct GemmArgs {
   bool out_f32 = false;
   bool bias_bf16 = false;
   bool vec_ok = false;
+  bool vec8_ok = false;  // 16-B row chunks of C/Z (and of the split-K slab) can be stored whole
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)

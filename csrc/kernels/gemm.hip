@@ -385,6 +385,9 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
   const int osz = p.out_f32 ? 4 : 2;
   p.vec_ok = ((p.ldc % 4) == 0) && ((p.sC % 4) == 0) && (((uintptr_t)p.C) % (4 * osz) == 0) &&
              (p.Z == nullptr || ((uintptr_t)p.Z % 8) == 0);
+  p.vec8_ok = (p.N % 8 == 0) && ((p.ldc % 8) == 0) && ((p.sC % 8) == 0) && (((uintptr_t)p.C) % 16 == 0) &&
+              (p.Z == nullptr || ((uintptr_t)p.Z % 16) == 0) &&
+              (p.bias == nullptr || ((uintptr_t)p.bias % 16) == 0);
   if (p.M * (int64_t)p.N * p.K < 64 * 64 * 64 && !(a_al && b_al)) {
     dim3 grid((p.N + 15) / 16, (p.M + 15) / 16, p.batch);
     if (p.out_f32) hipLaunchKernelGGL(gemm_fallback_kernel<float>, grid, dim3(16, 16), 0, stream, p, p.a_kcontig, p.b_kcontig);

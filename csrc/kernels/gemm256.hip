@@ -244,6 +244,85 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
   }
   if (wr == 0) barrier();  // balance the barrier count of the two groups
 
+  if (p.vec8_ok) {
+    // Coalesced epilogue through LDS (the operand ring is free now: every wave has passed the
+    // loop's last barrier). A wave writes 32 of its 128 output rows as fp32 into its own padded
+    // [32][WN+4] LDS image (16-B writes, the +4-float pad makes the 8-lane write groups hit
+    // distinct banks), then reads them back 8 consecutive columns per lane and applies
+    // bias / beta*C / pre-activation store / activation with 16-B (bf16) or 32-B (fp32) accesses:
+    // each row leaves as one contiguous 2*WN-byte segment instead of 16 scattered 8-byte pieces.
+    // Only the wave's own rows are touched, and LDS executes a wave's instructions in order,
+    // so no barrier is needed between the write and the read-back.
+    constexpr int LDW = WN + 4;
+    float* st = reinterpret_cast<float*>(smem) + wave * (32 * LDW);
+    typedef typename std::conditional<OUT_MODE == 0, bf16_t, float>::type OutT2;
+    OutT2* C = OUT_MODE == 2 ? nullptr : reinterpret_cast<OutT2*>(p.C) + (int64_t)b * p.sC;
+    bf16_t* Zp = p.Z ? reinterpret_cast<bf16_t*>(p.Z) + (int64_t)b * p.sC : nullptr;
+    float* W = OUT_MODE == 2 ? p.ws + (int64_t)z * p.M * p.N : nullptr;
+#pragma unroll
+    for (int qtr = 0; qtr < 4; ++qtr) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          const f32x4 v = acc[2 * qtr + i][j];
+          *reinterpret_cast<float4*>(st + (i * 16 + (lane & 15)) * LDW + j * 16 + (lane >> 4) * 4) =
+              make_float4(v[0] * p.alpha, v[1] * p.alpha, v[2] * p.alpha, v[3] * p.alpha);
+        }
+      constexpr int CPR = WN / 8;  // 8-column chunks per row
+#pragma unroll
+      for (int it = 0; it < 32 * CPR / 64; ++it) {
+        const int idx = it * 64 + lane;
+        const int r = idx / CPR, c8 = (idx % CPR) * 8;
+        const int m = m0 + wr * 128 + qtr * 32 + r;
+        const int n = n0 + wc * WN + c8;
+        const float4 lo = *reinterpret_cast<const float4*>(st + r * LDW + c8);
+        const float4 hi = *reinterpret_cast<const float4*>(st + r * LDW + c8 + 4);
+        if (m >= p.M || n >= p.N) continue;
+        float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        if (OUT_MODE == 2) {
+          float4* d = reinterpret_cast<float4*>(W + (int64_t)m * p.N + n);
+          d[0] = lo;
+          d[1] = hi;
+          continue;
+        }
+        OutT2* dst = C + (int64_t)m * p.ldc + n;
+        if (p.beta != 0.f) {
+          float c[8];
+          if (OUT_MODE == 0) load16(reinterpret_cast<const bf16_t*>(dst), c);
+          else {
+            const float4 c0 = reinterpret_cast<const float4*>(dst)[0], c1 = reinterpret_cast<const float4*>(dst)[1];
+            c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w; c[4] = c1.x; c[5] = c1.y; c[6] = c1.z; c[7] = c1.w;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] += p.beta * c[e];
+        }
+        if (p.bias) {
+          float bb[8];
+          if (p.bias_bf16) load16(reinterpret_cast<const bf16_t*>(p.bias) + n, bb);
+          else {
+            const float4 b0 = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.bias) + n)[0];
+            const float4 b1 = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.bias) + n)[1];
+            bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] += bb[e];
+        }
+        if (Zp) store16(Zp + (int64_t)m * p.ldc + n, x);
+        if (p.act != ACT_NONE) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = act_fwd(p.act, x[e]);
+        }
+        if (OUT_MODE == 0) store16(reinterpret_cast<bf16_t*>(dst), x);
+        else {
+          reinterpret_cast<float4*>(dst)[0] = make_float4(x[0], x[1], x[2], x[3]);
+          reinterpret_cast<float4*>(dst)[1] = make_float4(x[4], x[5], x[6], x[7]);
+        }
+      }
+    }
+    return;
+  }
+
   const int mrow = m0 + wr * 128 + (lane & 15);
   const int ncol = n0 + wc * WN + (lane >> 4) * 4;
   if (OUT_MODE == 2) {
