@@ -110,12 +110,25 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // Activation codes (match flexflow_amd.type.ActiMode numeric values).
 enum Act : int { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13, ACT_GELU = 14 };
 
+// erf with |error| < 1.5e-7 (Abramowitz & Stegun 7.1.26): one v_rcp, one v_exp and five FMAs
+// instead of libm erff's branchy polynomial — the GELU epilogues evaluate it per output element.
+__device__ __forceinline__ float fast_erf(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(1.f + 0.3275911f * ax);
+  float y = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  y = __builtin_fmaf(y, t, 1.421413741f);
+  y = __builtin_fmaf(y, t, -0.284496736f);
+  y = __builtin_fmaf(y, t, 0.254829592f);
+  y = 1.f - y * t * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ACT_RELU: return fmaxf(x, 0.f);
     case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
     case ACT_TANH: return tanhf(x);
-    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_GELU: return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f));
     default: return x;
   }
 }
@@ -126,7 +139,7 @@ __device__ __forceinline__ float act_grad(int act, float x) {
     case ACT_SIGMOID: { float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
     case ACT_TANH: { float t = tanhf(x); return 1.f - t * t; }
     case ACT_GELU: {
-      float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      float cdf = 0.5f * (1.f + fast_erf(x * 0.70710678118654752f));
       float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
       return cdf + x * pdf;
     }

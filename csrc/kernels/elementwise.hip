@@ -13,7 +13,7 @@ __device__ __forceinline__ float unary_f(int op, float x, float s) {
     case U_SIGMOID: return 1.f / (1.f + __expf(-x));
     case U_TANH: return tanhf(x);
     case U_ELU: return x > 0.f ? x : (__expf(x) - 1.f);
-    case U_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case U_GELU: return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f));
     case U_EXP: return __expf(x);
     case U_SIN: return __sinf(x);
     case U_COS: return __cosf(x);
@@ -40,7 +40,7 @@ __device__ __forceinline__ float unary_df(int op, float x, float y, float s) {
     case U_TANH: return 1.f - y * y;
     case U_ELU: return x > 0.f ? 1.f : y + 1.f;
     case U_GELU: {
-      float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      float cdf = 0.5f * (1.f + fast_erf(x * 0.70710678118654752f));
       return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
     }
     case U_EXP: return y;

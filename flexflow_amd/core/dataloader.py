@@ -35,12 +35,16 @@ class SingleDataLoader:
         self.batch_size = bs
         self.idx = 0
         self._ring = None
-        try:
-            from flexflow_amd import _core  # noqa: F401
-            if hasattr(_core, "BatchRing") and self.full.dtype in (np.float32, np.int32, np.int64):
-                self._ring = _core.BatchRing(self.full, bs, 3)
-        except Exception:
-            self._ring = None
+        self._slot = None
+        if self.full.shape[0] >= bs:
+            try:
+                from flexflow_amd import _core
+                # 3 host staging slots filled by the native background thread (gather of the next
+                # batch overlaps the current step); a slot is handed back once its batch was fed
+                self._bufs = [np.empty((bs,) + self.full.shape[1:], dtype=self.full.dtype) for _ in range(3)]
+                self._ring = _core.BatchRing(self.full, bs, self._bufs)
+            except (ImportError, RuntimeError, TypeError):
+                self._ring = None
 
     @property
     def num_samples(self):
@@ -63,8 +67,9 @@ class SingleDataLoader:
             if self._ring is not None:
                 self._ring.reset(0)
         if self._ring is not None:
-            batch = self._ring.next()
+            slot = self._ring.next()
+            m.executor.feed(self.tensor, self._bufs[slot])  # pageable source: the copy is complete on return
+            self._ring.release(slot)
         else:
-            batch = self.full[self.idx:self.idx + bs]
-        m.executor.feed(self.tensor, batch)
+            m.executor.feed(self.tensor, self.full[self.idx:self.idx + bs])
         self.idx += bs
