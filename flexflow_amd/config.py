@@ -69,6 +69,9 @@ class FFConfig:
         self.grad_bucket_mb = 64.0
         self.seed = 1234
         self.trace_dir = ""
+        self.check_nan_every = 0      # --check-nan N: loss finite-check every N steps (0 = off)
+        self.watchdog_s = 0.0         # --watchdog S: dump all stacks if a step exceeds S seconds
+        self.dist_timeout_s = 1800.0  # --dist-timeout S: torch.distributed collective timeout
         self.iter_config_seq_length = -1
         self._traces: dict = {}
 
@@ -193,6 +196,12 @@ class FFConfig:
                 self.seed = int(nxt())
             elif a == "--trace-dir":
                 self.trace_dir = nxt()
+            elif a == "--check-nan":
+                self.check_nan_every = int(nxt())
+            elif a == "--watchdog":
+                self.watchdog_s = float(nxt())
+            elif a == "--dist-timeout":
+                self.dist_timeout_s = float(nxt())
             i += 1
         if self.only_data_parallel:
             self.search_algo = "dp"

@@ -66,6 +66,8 @@ def _ensure_dist(config: FFConfig):
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", config.local_rank % torch.cuda.device_count())
+        import datetime
+        kw["timeout"] = datetime.timedelta(seconds=float(getattr(config, "dist_timeout_s", 1800.0)))
         dist.init_process_group(backend=backend, **kw)
     elif torch.cuda.is_available():
         torch.cuda.set_device(config.local_rank % torch.cuda.device_count())
@@ -402,6 +404,30 @@ class FFModel:
             from ..pcg.strategy import save_strategy
             save_strategy(cfg.export_strategy_file, self.strategy, cfg.num_devices,
                           extra={"search": self.search_report})
+        # aux subsystems: per-op profiling / traces, non-finite detection, hang watchdog, dot export
+        self.profiler = None
+        self.guard = None
+        self.watchdog = None
+        if cfg.profiling or cfg.trace_dir:
+            from ..runtime.profiler import OpProfiler
+            self.profiler = OpProfiler(self.executor, cfg.rank)
+            self.executor.hooks.append(self.profiler)
+        if cfg.check_nan_every or os.environ.get("FF_DEBUG_NAN") == "1":
+            from ..runtime.health import NonFiniteGuard
+            self.guard = NonFiniteGuard(self.executor, cfg.check_nan_every or 1,
+                                        per_op=os.environ.get("FF_DEBUG_NAN") == "1")
+            if self.guard.per_op:
+                self.executor.hooks.append(self.guard)
+        if cfg.watchdog_s > 0:
+            from ..runtime.health import Watchdog
+            self.watchdog = Watchdog(cfg.watchdog_s)
+        if cfg.rank == 0 and (cfg.export_strategy_computation_graph_file or cfg.export_strategy_task_graph_file):
+            from ..utils.dot import export_computation_graph, export_task_graph
+            if cfg.export_strategy_computation_graph_file:
+                export_computation_graph(self, cfg.export_strategy_computation_graph_file,
+                                         include_costs=cfg.include_costs_dot_graph)
+            if cfg.export_strategy_task_graph_file:
+                export_task_graph(self, cfg.export_strategy_task_graph_file)
 
     def _find_tensor(self, guid):
         for L in self.layers:
@@ -461,7 +487,36 @@ class FFModel:
         """One full iteration (forward, zero_gradients, backward, update) — the unit captured by
         hipGraphs in runtime/graph.py."""
         from ..runtime.graph import run_train_step
+        if self.watchdog is not None:
+            self.watchdog.arm()
         run_train_step(self)
+        if self.watchdog is not None:
+            self.watchdog.disarm()
+        if self.profiler is not None:
+            self.profiler.next_step()
+        if self.guard is not None:
+            self.guard.after_step(self.executor._metric_acc[0])
+
+    # ---- checkpoint / profiling
+    def save_checkpoint(self, path):
+        from ..runtime.checkpoint import save_checkpoint
+        return save_checkpoint(self, path)
+
+    def load_checkpoint(self, path, strict=True):
+        from ..runtime.checkpoint import load_checkpoint
+        return load_checkpoint(self, path, strict)
+
+    def profile_report(self, top=40):
+        """Per-op device time table (--profiling); also writes the Chrome trace to --trace-dir."""
+        if self.profiler is None:
+            return ""
+        if self.config.trace_dir:
+            self.profiler.chrome_trace(os.path.join(self.config.trace_dir, f"trace_rank{self.config.rank}.json"))
+        return self.profiler.report(top)
+
+    def export_dot(self, path, include_costs=False):
+        from ..utils.dot import export_computation_graph
+        return export_computation_graph(self, path, include_costs=include_costs)
 
     def recompile_on_condition(self, r):
         """reference FFModel::recompile_on_condition (model.cc:2422-2426)."""

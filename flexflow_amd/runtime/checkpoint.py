@@ -1,0 +1,88 @@
+"""Checkpoint / resume (the reference has only per-tensor host get/set, parallel_tensor.cc:650-748;
+long runs need whole-job checkpoints).
+
+Layout of a checkpoint directory:
+    meta.json                 step, world size, strategy (per-op OpConfig JSON), optimizer hyper-
+                              parameters and bias-correction state, arena layout
+    rank{r}.safetensors       that rank's fp32 master weights and optimizer state, one tensor per
+                              weight arena ("arena{i}.master", "arena{i}.m", "arena{i}.v", ...)
+Every rank writes its own shard (no gather through rank 0: 288 GB HBM per GPU means shards can be
+large), loading checks that the strategy and arena layout match the running job. Files are
+safetensors — no pickle anywhere, so checkpoints from an untrusted source cannot execute code.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+from safetensors.torch import load_file, save_file
+
+
+def _arenas(ex):
+    return [(i, ar) for i, ar in enumerate(ex.arenas.values()) if ar.size]
+
+
+def save_checkpoint(model, path: str):
+    ex = model.executor
+    opt = model.optimizer
+    cfg = model.config
+    os.makedirs(path, exist_ok=True)
+    tensors = {}
+    layout = []
+    for i, ar in _arenas(ex):
+        tensors[f"arena{i}.master"] = ar.master.detach().contiguous().cpu()
+        st = getattr(opt, "state", {}).get(id(ar))
+        if st is not None:
+            for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
+                tensors[f"arena{i}.opt{j}"] = t.detach().contiguous().cpu()
+        layout.append({"arena": i, "size": int(ar.size), "entries": [[getattr(e[0], "name", str(e[0])), int(e[1]), int(e[2])] for e in ar.entries]})
+    save_file(tensors, os.path.join(path, f"rank{cfg.rank}.safetensors"))
+    if cfg.rank == 0:
+        meta = {
+            "step": int(ex.step_idx),
+            "world_size": int(cfg.world_size),
+            # positional (layer order), so a rebuilt model whose auto-generated names differ still matches
+            "strategy": [[L.name, L.op_type.name, model.strategy[L.name].to_json()] for L in model.layers],
+            "optimizer": {k: v for k, v in vars(opt).items() if isinstance(v, (int, float, bool, str))},
+            "arenas": layout,
+        }
+        with open(os.path.join(path, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    return path
+
+
+def load_checkpoint(model, path: str, strict: bool = True):
+    ex = model.executor
+    opt = model.optimizer
+    cfg = model.config
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    if strict and meta["world_size"] != cfg.world_size:
+        raise ValueError(f"checkpoint was written by {meta['world_size']} ranks, job has {cfg.world_size}")
+    if strict:
+        cur = [[L.op_type.name, model.strategy[L.name].to_json()] for L in model.layers]
+        if cur != [[op, c] for _, op, c in meta["strategy"]]:
+            raise ValueError("checkpoint strategy differs from the compiled strategy (import it with "
+                             "--import-strategy to resume)")
+    tensors = load_file(os.path.join(path, f"rank{cfg.rank}.safetensors"))
+    for i, ar in _arenas(ex):
+        m = tensors[f"arena{i}.master"]
+        if m.numel() != ar.master.numel():
+            raise ValueError(f"arena {i} size mismatch")
+        ar.master.copy_(m.to(ar.master.device))
+        if ar.lowp is not None:
+            ar.lowp.copy_(ar.master.to(ar.lowp.dtype))
+        st = getattr(opt, "state", {}).get(id(ar))
+        if st is not None:
+            for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
+                key = f"arena{i}.opt{j}"
+                if key in tensors:
+                    t.copy_(tensors[key].to(t.device))
+    for k, v in meta.get("optimizer", {}).items():
+        if hasattr(opt, k) and not callable(getattr(opt, k)):
+            setattr(opt, k, v)
+    ex.step_idx = int(meta["step"])
+    return meta["step"]

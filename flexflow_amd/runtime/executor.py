@@ -73,6 +73,7 @@ class Executor:
         self.model = model
         cfg = model.config
         self.config = cfg
+        self.hooks = []  # per-op context managers: OpProfiler, NonFiniteGuard (runtime/profiler.py, health.py)
         self.rank, self.world = cfg.rank, cfg.world_size
         self.device = _device_for(cfg)
         self.training = training
@@ -324,9 +325,15 @@ class Executor:
                 ctx.training = tr
                 ctx.step = self.step_idx
                 ws = [self.weight_tensor(w) for w in L.weights]
-                outs = L.impl.forward(ctx, xs, ws)
-                for o, v in zip(L.outputs, outs):
-                    vals[o.guid] = v
+                if self.hooks:
+                    with self._hooked(L, "fwd"):
+                        outs = L.impl.forward(ctx, xs, ws)
+                        for o, v in zip(L.outputs, outs):
+                            vals[o.guid] = v
+                else:
+                    outs = L.impl.forward(ctx, xs, ws)
+                    for o, v in zip(L.outputs, outs):
+                        vals[o.guid] = v
             else:
                 for o in L.outputs:
                     vals[o.guid] = None
@@ -436,7 +443,11 @@ class Executor:
                              for d, v in zip(douts, vals)]
                     ctx = self.ctx[L.name]
                     ctx.extra["dx_accum"] = self._accum_targets(L, grads, douts)
-                    dxs = L.impl.backward(ctx, douts)
+                    if self.hooks:
+                        with self._hooked(L, "bwd"):
+                            dxs = L.impl.backward(ctx, douts)
+                    else:
+                        dxs = L.impl.backward(ctx, douts)
                     ctx.extra["dx_accum"] = None
                 for w in L.weights:
                     self._wdone[w.guid] = self._wdone.get(w.guid, 0) + 1
@@ -459,6 +470,14 @@ class Executor:
                 if gp is not None:
                     prev = grads.get(t.guid)
                     grads[t.guid] = gp if (prev is None or prev is gp) else prev + gp
+
+    def _hooked(self, L, phase):
+        """Nest every attached hook's op(L, phase) context (profiler, non-finite guard)."""
+        from contextlib import ExitStack
+        st = ExitStack()
+        for h in self.hooks:
+            st.enter_context(h.op(L, phase))
+        return st
 
     def _accum_targets(self, L, grads, douts):
         """Input slots whose existing gradient the op may accumulate into in place (a dgrad GEMM

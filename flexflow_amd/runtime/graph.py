@@ -28,7 +28,7 @@ class StepGraph:
         ex = m.executor
         if not (m.config.hip_graphs and torch.cuda.is_available() and ex.device.type == "cuda"):
             return False
-        if self.failed:
+        if self.failed or ex.hooks:  # per-op hooks time / inspect individual ops: run eagerly
             return False
         if ex.comm.distributed and os.environ.get("FF_GRAPH_COLLECTIVES", "0") != "1":
             return False

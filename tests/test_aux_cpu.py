@@ -1,0 +1,91 @@
+"""Aux subsystems: per-op profiling + Chrome trace, non-finite detection, watchdog, determinism
+(race) check, checkpoint/resume, dot export of the computation / task graph and of rules."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, SGDOptimizer
+from flexflow_amd.models import build
+from flexflow_amd.runtime.health import NonFiniteError, determinism_check
+
+
+def _model(flags=(), name="mnist_mlp", opt="adam", batch=8):
+    cfg = FFConfig(["--no-hip-graphs"] + list(flags))
+    cfg.batch_size = batch
+    ff = FFModel(cfg)
+    inputs, out, loss, mets, make_batch = build(name, ff, batch, small=True)
+    ff.optimizer = AdamOptimizer(ff, 1e-3) if opt == "adam" else SGDOptimizer(ff, 0.05)
+    ff.compile(loss_type=loss, metrics=mets)
+    arrs, lab = make_batch(np.random.default_rng(0))
+    for t, a in zip(inputs, arrs):
+        t.set_tensor(ff, a)
+    ff.label_tensor.set_tensor(ff, lab)
+    return ff, inputs
+
+
+def test_profiler_and_trace(tmp_path):
+    ff, _ = _model(["--profiling", "--trace-dir", str(tmp_path)])
+    for _ in range(2):
+        ff.train_step()
+    rep = ff.profile_report()
+    assert "forward" in rep and "OP_LINEAR" in rep
+    tr = json.load(open(tmp_path / "trace_rank0.json"))
+    names = {e["name"] for e in tr["traceEvents"]}
+    assert any(n.endswith(" fwd") for n in names) and any(n.endswith(" bwd") for n in names)
+
+
+def test_nonfinite_guard_names_the_op(monkeypatch):
+    monkeypatch.setenv("FF_DEBUG_NAN", "1")
+    ff, inputs = _model(["--check-nan", "1"])
+    x = np.zeros(tuple(inputs[0].dims), np.float32)
+    x[0, 0] = np.nan
+    inputs[0].set_tensor(ff, x)
+    with pytest.raises(NonFiniteError, match="output of"):
+        ff.train_step()
+
+
+def test_watchdog_arms_and_disarms():
+    ff, _ = _model(["--watchdog", "30"])
+    ff.train_step()
+    assert ff.watchdog is not None
+
+
+def test_determinism_check():
+    ff, _ = _model()
+    ff.train_step()
+    assert determinism_check(ff, steps=2)
+
+
+def test_checkpoint_resume_matches_uninterrupted(tmp_path):
+    ff, _ = _model(opt="adam")
+    for _ in range(2):
+        ff.train_step()
+    ff.save_checkpoint(str(tmp_path / "ck"))
+    for _ in range(2):
+        ff.train_step()
+    w_ref = [np.asarray(w.get_weights(ff)).copy() for L in ff.layers for w in L.weights]
+    ff2, _ = _model(opt="adam")
+    step = ff2.load_checkpoint(str(tmp_path / "ck"))
+    assert step == 2
+    for _ in range(2):
+        ff2.train_step()
+    w2 = [np.asarray(w.get_weights(ff2)).copy() for L in ff2.layers for w in L.weights]
+    for a, b in zip(w_ref, w2):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    meta = json.load(open(tmp_path / "ck" / "meta.json"))
+    assert meta["step"] == 2 and "strategy" in meta
+
+
+def test_dot_exports(tmp_path):
+    cg, tg = tmp_path / "cg.dot", tmp_path / "tg.dot"
+    ff, _ = _model(["--compgraph", str(cg), "--taskgraph", str(tg), "--include-costs-dot-graph"])
+    t = cg.read_text()
+    assert t.startswith('digraph') and "LINEAR" in t and "->" in t
+    assert "fwd" in tg.read_text()
+    from flexflow_amd import _core
+    from flexflow_amd.pcg.substitutions import BUILTIN
+    from flexflow_amd.utils.dot import rule_to_dot
+    r = _core.load_rules(BUILTIN)[0]
+    assert "digraph" in open(rule_to_dot(r, str(tmp_path / "r.dot"))).read()
