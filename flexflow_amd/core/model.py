@@ -306,6 +306,26 @@ class FFModel:
             agg.append(self.softmax(self.dense(e, expert_hidden_size, ActiMode.AC_MODE_RELU)))
         return self.aggregate(agg, num_exp, lambda_bal)
 
+    # ---- explicit parallel ops (ops/parallel_ops.py): identity compute, pinned output layout
+    def repartition(self, input, dim, degree, name=None):
+        return self._add(OperatorType.OP_REPARTITION, [input], name, dim=int(dim), degree=int(degree)).outputs[0]
+
+    def combine(self, input, dim=0, degree=None, name=None):
+        return self._add(OperatorType.OP_COMBINE, [input], name, dim=int(dim), degree=degree).outputs[0]
+
+    def replicate(self, input, degree, name=None):
+        return self._add(OperatorType.OP_REPLICATE, [input], name, degree=int(degree)).outputs[0]
+
+    def reduction(self, input, dim=0, degree=1, name=None):
+        return self._add(OperatorType.OP_REDUCTION, [input], name, dim=int(dim), degree=int(degree)).outputs[0]
+
+    def allreduce(self, input, name=None):
+        return self._add(OperatorType.OP_ALLREDUCE, [input], name).outputs[0]
+
+    def fused_parallel(self, input, ops, name=None):
+        """ops: [(kind, dim, degree)] with kind in repartition/combine/replicate/allreduce."""
+        return self._add(OperatorType.OP_FUSED_PARALLEL, [input], name, ops=[tuple(o) for o in ops]).outputs[0]
+
     def _share(self, L, shared_op):
         if shared_op is None:
             return
@@ -389,6 +409,8 @@ class FFModel:
         training = self.comp_mode == CompMode.TRAINING
         self.executor = Executor(self, self.strategy, loss_type, self.metrics, training=training)
         self.executor.init_weights(cfg.seed)
+        if os.environ.get("FF_NO_INPLACE") != "1":
+            self.executor._plan_inplace()
         if self.optimizer is not None and training:
             self.executor.init_optimizer(self.optimizer)
         for guid, v in self._pending_values.items():

@@ -468,13 +468,18 @@ def unary_ref(name, x, s):
     return r.to(x.dtype)
 
 
-def unary_fwd(name, x, s=0.0):
+def unary_fwd(name, x, s=0.0, out=None):
+    """y = f(x); out=x computes in place (elementwise, same index: safe)."""
     if native(x) and x.dtype in (torch.bfloat16, torch.float32):
         xc = x.contiguous()
-        y = torch.empty_like(xc)
+        y = out if out is not None else torch.empty_like(xc)
         ext().unary_fwd(xc, y, U[name], float(s))
         return y
-    return unary_ref(name, x, s)
+    r = unary_ref(name, x, s)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 def unary_bwd(name, x, y, dy, s=0.0):

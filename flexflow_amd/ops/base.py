@@ -143,6 +143,15 @@ class OpImpl:
         return float(elem * (sum(math.prod(s) for s in in_shapes) + sum(math.prod(s) for s in out_shapes)
                              + sum(math.prod(s) for s in w_shapes)))
 
+    def can_inplace(self) -> bool:
+        """True if forward may write its (single) output into its first input's buffer."""
+        return False
+
+    def saves_output(self) -> bool:
+        """True if backward reads this op's own output tensor (then a consumer must not overwrite
+        it in place). Conservative default."""
+        return True
+
     def accumulates_dx(self) -> bool:
         """True if backward honours ctx.extra['dx_accum'] = {input slot: tensor}: it then ADDS the
         input gradient into that tensor (same shape/dtype) and returns it for that slot."""

@@ -25,6 +25,12 @@ UNARY = {
 }
 
 
+# functions whose gradient can be computed from the output alone, so the output may overwrite the
+# input (reference in-place optimisation, model.cc:2885-2919 / Op::can_inplace_output)
+INPLACE_OK = {"relu", "sigmoid", "tanh", "exp", "scalar_multiply", "scalar_add", "scalar_sub",
+              "scalar_true_divide"}
+
+
 @register(*UNARY.keys())
 class ElementUnary(OpImpl):
     def __init__(self, layer):
@@ -40,11 +46,23 @@ class ElementUnary(OpImpl):
         x = xs[0]
         if self.fn == "identity":
             return [x]
+        if ctx.extra.get("inplace") and x.is_contiguous():
+            y = K.unary_fwd(self.fn, x, self.scalar, out=x)
+            if ctx.training:
+                ctx.saved["x"] = y  # the input was overwritten; the gradient needs y only
+                ctx.saved["y"] = y
+            return [y]
         y = K.unary_fwd(self.fn, x, self.scalar)
         if ctx.training:
             ctx.saved["x"] = x
             ctx.saved["y"] = y
         return [y]
+
+    def can_inplace(self):
+        return self.fn in INPLACE_OK
+
+    def saves_output(self):
+        return True
 
     def backward(self, ctx, douts):
         dy = douts[0]
@@ -60,6 +78,9 @@ BINARY = {OperatorType.OP_EW_ADD: "add", OperatorType.OP_EW_SUB: "sub", Operator
 
 @register(*BINARY.keys())
 class ElementBinary(OpImpl):
+    def saves_output(self):
+        return False  # backward reads inputs / its own saved buffers only
+
     def __init__(self, layer):
         super().__init__(layer)
         self.fn = BINARY[layer.op_type]

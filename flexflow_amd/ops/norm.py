@@ -24,6 +24,9 @@ from .base import OpImpl, WeightSpec, register
 class LayerNorm(OpImpl):
     op_type = OperatorType.OP_LAYERNORM
 
+    def saves_output(self):
+        return False  # backward reads inputs / its own saved buffers only
+
     @classmethod
     def infer(cls, attrs, in_dims, in_dtypes):
         d = in_dims[0]

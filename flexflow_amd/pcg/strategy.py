@@ -129,6 +129,9 @@ def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute
     divides the device count, placed on aligned contiguous device blocks (reference
     register_all_machine_views: 1-D views `i | N`, graph.cc:2329-2360)."""
     impl = layer.impl
+    pin = getattr(impl, "pinned_config", None)
+    if pin is not None:  # explicit parallel ops (ops/parallel_ops.py) fix their output layout
+        return [pin(num_devices)]
     sizes = impl.axis_sizes()
     kinds = impl.axis_kinds()
     axes = [a for a, k in enumerate(kinds) if k in allow_kinds and impl.supports_axis(a)]
@@ -163,6 +166,9 @@ def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute
 def data_parallel_config(layer, num_devices: int) -> OpConfig:
     """Reference --only-data-parallel: partition the sample dim over all devices when legal,
     otherwise run the op on device 0 (degree 1)."""
+    pin = getattr(layer.impl, "pinned_config", None)
+    if pin is not None:
+        return pin(num_devices)
     sizes = layer.impl.axis_sizes()
     n = len(sizes)
     for d in sorted(divisors(num_devices), reverse=True):

@@ -471,6 +471,36 @@ class Executor:
                     prev = grads.get(t.guid)
                     grads[t.guid] = gp if (prev is None or prev is gp) else prev + gp
 
+    def _plan_inplace(self):
+        """Reference in-place optimisation (model.cc:2885-2919): an element-wise op whose gradient
+        needs only its output overwrites its input when that input has no other reader — one
+        consumer, not a model input or output, the producer's backward does not read it, and the
+        edge is the identity transfer on this rank."""
+        consumers = {}
+        for L in self.layers:
+            for t in L.inputs:
+                consumers[t.guid] = consumers.get(t.guid, 0) + 1
+        prod = {}
+        for L in self.layers:
+            for o in L.outputs:
+                prod[o.guid] = L
+        out_guid = self.output_tensor.guid if self.output_tensor is not None else None
+        n = 0
+        for L in self.layers:
+            if not L.impl.can_inplace() or len(L.inputs) != 1 or not self.local.get(L.name):
+                continue
+            t = L.inputs[0]
+            P = prod.get(t.guid)
+            if P is None or P.op_type == OperatorType.OP_INPUT or consumers.get(t.guid, 0) != 1:
+                continue
+            if t.guid == out_guid or P.impl.saves_output() or len(P.outputs) != 1:
+                continue
+            if self.fwd_tx[(L.name, 0)].kind != "identity" or t.data_type != L.outputs[0].data_type:
+                continue
+            self.ctx[L.name].extra["inplace"] = True
+            n += 1
+        return n
+
     def _hooked(self, L, phase):
         """Nest every attached hook's op(L, phase) context (profiler, non-finite guard)."""
         from contextlib import ExitStack

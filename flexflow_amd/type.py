@@ -163,6 +163,7 @@ class OperatorType(IntEnum):
     OP_REDUCTION = 86
     OP_PIPELINE = 87
     OP_FUSED_PARALLEL = 88
+    OP_ALLREDUCE = 89  # extension: explicit all-reduce parallel op (not in the reference snapshot's enum)
     OP_INVALID = 89
 
 

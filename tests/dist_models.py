@@ -24,6 +24,18 @@ def build(name, ff):
         feeds[x] = rng.standard_normal((B, 16)).astype(np.float32)
         lab = rng.integers(0, 10, (B, 1)).astype(np.int32)
         loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+    elif name == "parops":
+        # explicit parallel ops: hidden activation repartitioned along features, combined back
+        x = ff.create_tensor([B, 16], DataType.DT_FLOAT, name="x")
+        t = ff.dense(x, 32, ActiMode.AC_MODE_RELU, name="d1")
+        t = ff.repartition(t, 1, 2, name="rp")
+        t = ff.relu(t, name="r2")
+        t = ff.combine(t, 1, name="cb")
+        t = ff.dense(t, 10, name="d3")
+        ff.softmax(t, name="sm")
+        feeds[x] = rng.standard_normal((B, 16)).astype(np.float32)
+        lab = rng.integers(0, 10, (B, 1)).astype(np.int32)
+        loss = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
     elif name in ("attn", "attn_tp"):
         x = ff.create_tensor([B, 6, 16], DataType.DT_FLOAT, name="x")
         a = ff.multihead_attention(x, x, x, 16, 4, name="mha")
@@ -115,3 +127,4 @@ def run(name, world, strategy_file=None, steps=2, lr=0.05):
             out[f"{l.name}.{i}"] = w.get_weights(ff)
     out["__output__"] = ff._get_tensor_value(ff.output_tensor())
     return out
+

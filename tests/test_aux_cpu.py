@@ -89,3 +89,28 @@ def test_dot_exports(tmp_path):
     from flexflow_amd.utils.dot import rule_to_dot
     r = _core.load_rules(BUILTIN)[0]
     assert "digraph" in open(rule_to_dot(r, str(tmp_path / "r.dot"))).read()
+
+
+def test_inplace_plan_same_results(monkeypatch):
+    """In-place element-wise ops (add -> relu in ResNet blocks) change memory, not math."""
+    def run():
+        ff, _ = _model(name="resnet50", batch=1, opt="sgd")
+        ff.train_step()
+        ff.train_step()
+        return ff, [np.asarray(w.get_weights(ff)).copy() for L in ff.layers for w in L.weights]
+    ff1, w1 = run()
+    n = sum(1 for L in ff1.layers if ff1.executor.ctx.get(L.name) is not None
+            and ff1.executor.ctx[L.name].extra.get("inplace"))
+    assert n >= 10
+    monkeypatch.setenv("FF_NO_INPLACE", "1")
+    _, w2 = run()
+    for a, b in zip(w1, w2):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_launcher_argv():
+    from flexflow_amd.run import build_argv
+    a = build_argv(["-ll:gpu", "4", "train.py", "--epochs", "2"])
+    assert a[:2] == ["--nproc-per-node", "4"] and "127.0.0.1" in a and a[-3:] == ["train.py", "--epochs", "2"]
+    b = build_argv(["--nproc=2", "--master-addr", "10.0.0.1", "x.py"])
+    assert "127.0.0.1" not in b and b[-1] == "x.py"

@@ -72,7 +72,7 @@ def _run_single(name):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("name", ["mlp", "mlp_tp", "mlp_place", "mlp_hybrid", "attn", "attn_tp", "cnn",
+@pytest.mark.parametrize("name", ["mlp", "mlp_tp", "mlp_place", "mlp_hybrid", "parops", "attn", "attn_tp", "cnn",
                                   "cnn_attr", "emb", "emb_vocab"])
 def test_parallel_matches_single(name):
     base = name.split("_")[0]
