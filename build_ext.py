@@ -118,10 +118,29 @@ def build_core(jobs: int = 8, verbose: bool = False) -> str | None:
     return out
 
 
+def build_capi(verbose: bool = False) -> str | None:
+    """libflexflow_c.so: the C API (csrc/capi) over an embedded CPython runtime."""
+    src = os.path.join(ROOT, "csrc", "capi", "flexflow_c.cc")
+    if not os.path.exists(src):
+        return None
+    out = os.path.join(PKG, "libflexflow_c.so")
+    hdr = os.path.join(ROOT, "csrc", "capi", "flexflow_c.h")
+    if _newer(src, out, [hdr]):
+        paths = sysconfig.get_paths()
+        libdir = sysconfig.get_config_var("LIBDIR")
+        ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+        _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-I", paths["include"], src,
+              "-L", libdir, f"-lpython{ver}", f"-Wl,-rpath,{libdir}", "-o", out])
+        if verbose:
+            print(f"[build_ext] C API -> {out}")
+    return out
+
+
 def build_all(verbose: bool = True) -> None:
     jobs = min(8, os.cpu_count() or 4)
     build_core(jobs, verbose)
     build_kernels(jobs, verbose)
+    build_capi(verbose)
 
 
 if __name__ == "__main__":
