@@ -26,5 +26,7 @@ struct AttnArgs {
 void attn_fwd(AttnArgs a, hipStream_t st);
 void attn_bwd(AttnArgs a, hipStream_t st);
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D);
+int attn_bwd_variant();
+void attn_set_bwd_variant(int v);
 
 }  // namespace ffk

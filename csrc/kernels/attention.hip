@@ -484,6 +484,240 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   }
 }
 
+// Backward, one wave per SIMD: each wave owns KG groups of 32 keys (KG = 2 at D = 64 -> 256 keys
+// per workgroup, so at S = 512 only two fp32 dQ partial slabs are written and re-read instead of
+// four — the slab round trip was the dominant HBM traffic of attn_bwd_kernel). The Q/dO fragment
+// reads (ds_read_b128) and the transposed dO/Q reads of the dV/dK products are shared by the KG
+// key groups, so each LDS byte feeds KG x the MFMAs. 1-D grid through the XCD remap so that the key
+// blocks of one (batch, head) run on one XCD and share its L2 copy of Q / dO / lse / delta.
+template <int D, int KG>
+__global__ void __launch_bounds__(256, 1) attn_bwd_kg_kernel(AttnArgs a, int nkb) {
+  constexpr int NW = 4, NT = 256, QT = 64;
+  constexpr int KB = 32 * KG * NW;  // keys per workgroup
+  constexpr int QB = QT * D * 2;
+  constexpr int TILE = 2 * QB + 2 * QT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + KB * QT * 2];
+  char* k_l = smem + 2 * TILE;
+  char* ds_l = k_l + KB * D * 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int lid = xcd_remap(blockIdx.x, nkb * a.B * a.H);
+  const int bh = lid / nkb, kblk = lid % nkb;
+  const int b = bh / a.H, hh = bh % a.H;
+  const int kb0 = kblk * KB;
+  const int kw0 = kb0 + wave * KG * 32;  // first key of this wave
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh;
+  const float* LSE = a.lse + (int64_t)bh * a.Sq;
+  const float* DL = a.delta + (int64_t)bh * a.Sq;
+  const float sl2 = a.scale * LOG2E;
+
+  {
+    TileStage<D, KB, NT> st;
+    st.load(K, a.k_ss, kb0, a.Sk, tid);
+    st.store(k_l, tid);
+  }
+  bf16x8 kf[KG][D / 16], vf[KG][D / 16];
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const int key = kw0 + g * 32 + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (key < a.Sk) {
+        kf[g][s] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * a.k_ss + 16 * s + 8 * h);
+        vf[g][s] = *reinterpret_cast<const bf16x8*>(V + (int64_t)key * a.v_ss + 16 * s + 8 * h);
+      } else {
+        kf[g][s] = bf16x8{};
+        vf[g][s] = bf16x8{};
+      }
+    }
+  }
+  f32x16 dk[KG][D / 32], dv[KG][D / 32];
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) { dk[g][i] = f32x16{}; dv[g][i] = f32x16{}; }
+
+  const int qt_begin = a.causal ? kb0 / QT : 0;
+  const int nqt = (a.Sq + QT - 1) / QT;
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  float* dq_part = a.dq_acc + (int64_t)kblk * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
+
+  TileStage<D, QT, NT> sq, sd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  auto fetch = [&](int t) {
+    const int qbase = t * QT;
+    sq.load(Q, a.q_ss, qbase, a.Sq, tid);
+    sd.load(dO, a.do_ss, qbase, a.Sq, tid);
+    if (tid < QT) {
+      const int q = qbase + tid;
+      lse_r = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
+      dl_r = q < a.Sq ? DL[q] : 0.f;
+    }
+  };
+  auto stash = [&](int t) {
+    char* tb = smem + (t & 1) * TILE;
+    sq.store(tb, tid);
+    sd.store(tb + QB, tid);
+    if (tid < QT) {
+      reinterpret_cast<float*>(tb + 2 * QB)[tid] = lse_r;
+      reinterpret_cast<float*>(tb + 2 * QB)[QT + tid] = dl_r;
+    }
+  };
+  if (qt_begin < nqt) {
+    fetch(qt_begin);
+    stash(qt_begin);
+  }
+  __syncthreads();
+
+  for (int t = qt_begin; t < nqt; ++t) {
+    const int qbase = t * QT;
+    char* tb = smem + (t & 1) * TILE;
+    const char* q_l = tb;
+    const char* do_l = tb + QB;
+    const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
+    const float* dl_l = lse_l + QT;
+    const bool more = t + 1 < nqt;
+    if (more) fetch(t + 1);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 sacc[KG], pacc[KG];
+#pragma unroll
+      for (int g = 0; g < KG; ++g) { sacc[g] = f32x16{}; pacc[g] = f32x16{}; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const int row = 32 * qt + (lane & 31);
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          sacc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[g][s], sacc[g], 0, 0, 0);
+          pacc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[g][s], pacc[g], 0, 0, 0);
+        }
+      }
+      bf16x8 pb[KG][2], sb[KG][2];
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const int key = kw0 + g * 32 + (lane & 31);
+        // wave-uniform: does this 32x32 block cross the sequence end or the causal diagonal?
+        const bool need_mask = (kw0 + g * 32 + 31 >= a.Sk) || (a.causal && kw0 + g * 32 + 31 > qbase + 32 * qt);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float p = exp2f(__builtin_fmaf(sacc[g][r], sl2, -lse_l[ql]));
+          if (need_mask && (key >= a.Sk || (a.causal && key > qbase + ql))) p = 0.f;
+          sacc[g][r] = p;
+          pacc[g][r] = p * (pacc[g][r] - dl_l[ql]);
+        }
+        pb[g][0] = pack8(sacc[g], 0); pb[g][1] = pack8(sacc[g], 8);
+        sb[g][0] = pack8(pacc[g], 0); sb[g][1] = pack8(pacc[g], 8);
+      }
+      // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
+          bf16x8 ao, aq;
+          {
+            const bf16x4 lo = tr_read(do_l, aoff<D>(r0, col));
+            const bf16x4 hi = tr_read(do_l, aoff<D>(r0 + 8, col));
+            ao[0] = lo[0]; ao[1] = lo[1]; ao[2] = lo[2]; ao[3] = lo[3];
+            ao[4] = hi[0]; ao[5] = hi[1]; ao[6] = hi[2]; ao[7] = hi[3];
+          }
+          {
+            const bf16x4 lo = tr_read(q_l, aoff<D>(r0, col));
+            const bf16x4 hi = tr_read(q_l, aoff<D>(r0 + 8, col));
+            aq[0] = lo[0]; aq[1] = lo[1]; aq[2] = lo[2]; aq[3] = lo[3];
+            aq[4] = hi[0]; aq[5] = hi[1]; aq[6] = hi[2]; aq[7] = hi[3];
+          }
+#pragma unroll
+          for (int g = 0; g < KG; ++g) {
+            dv[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, pb[g][s2], dv[g][dt], 0, 0, 0);
+            dk[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, sb[g][s2], dk[g][dt], 0, 0, 0);
+          }
+        }
+      }
+      // dS^T image rows = local key index
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const int krow = (wave * KG + g) * 32 + (lane & 31);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int ql = 32 * qt + 8 * q4 + 4 * h;
+          ushort4 o;
+          o.x = f2bf(pacc[g][4 * q4 + 0]); o.y = f2bf(pacc[g][4 * q4 + 1]);
+          o.z = f2bf(pacc[g][4 * q4 + 2]); o.w = f2bf(pacc[g][4 * q4 + 3]);
+          *reinterpret_cast<ushort4*>(ds_l + dst_off(krow, ql)) = o;
+        }
+      }
+    }
+    lds_barrier();
+    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's KB keys; wave -> (qt, dt) tiles
+#pragma unroll
+    for (int tile = wave; tile < 2 * (D / 32); tile += NW) {
+      const int qt = tile / (D / 32), dt = tile % (D / 32);
+      f32x16 acc = f32x16{};
+#pragma unroll 4
+      for (int ks = 0; ks < KB / 16; ++ks) {
+        bf16x8 af, bk;
+        {
+          const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
+          const int kr = 16 * ks + 8 * h + qi;
+          const bf16x4 lo = tr_read(ds_l, dst_off(kr, cq));
+          const bf16x4 hi = tr_read(ds_l, dst_off(kr + 4, cq));
+          af[0] = lo[0]; af[1] = lo[1]; af[2] = lo[2]; af[3] = lo[3];
+          af[4] = hi[0]; af[5] = hi[1]; af[6] = hi[2]; af[7] = hi[3];
+        }
+        {
+          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
+          const int kr = 16 * ks + 8 * h + qi;
+          const bf16x4 lo = tr_read(k_l, aoff<D>(kr, cd));
+          const bf16x4 hi = tr_read(k_l, aoff<D>(kr + 4, cd));
+          bk[0] = lo[0]; bk[1] = lo[1]; bk[2] = lo[2]; bk[3] = lo[3];
+          bk[4] = hi[0]; bk[5] = hi[1]; bk[6] = hi[2]; bk[7] = hi[3];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int d = 32 * dt + (lane & 31);
+        if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
+      }
+    }
+    if (more) stash(t + 1);
+    lds_barrier();
+  }
+  if (a.causal) {
+    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
+  }
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const int key = kw0 + g * 32 + (lane & 31);
+    if (key >= a.Sk) continue;
+    bf16_t* dK = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh + (int64_t)key * a.dk_ss;
+    bf16_t* dV = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh + (int64_t)key * a.dv_ss;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int d = dt * 32 + 8 * q4 + 4 * h;
+        ushort4 o;
+        o.x = f2bf(dk[g][dt][4 * q4 + 0] * a.scale); o.y = f2bf(dk[g][dt][4 * q4 + 1] * a.scale);
+        o.z = f2bf(dk[g][dt][4 * q4 + 2] * a.scale); o.w = f2bf(dk[g][dt][4 * q4 + 3] * a.scale);
+        *reinterpret_cast<ushort4*>(dK + d) = o;
+        o.x = f2bf(dv[g][dt][4 * q4 + 0]); o.y = f2bf(dv[g][dt][4 * q4 + 1]);
+        o.z = f2bf(dv[g][dt][4 * q4 + 2]); o.w = f2bf(dv[g][dt][4 * q4 + 3]);
+        *reinterpret_cast<ushort4*>(dV + d) = o;
+      }
+    }
+  }
+}
+
 // dq[q][d] = scale * sum_kb dq_part[kb][bh][q][d]
 template <int D>
 __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
@@ -508,10 +742,26 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
   }
 }
 
-static int bwd_waves(int) { return 4; }  // 8 (256 keys per WG) measured 1.5x slower at S=512: 4 idle waves in the dQ stage
+// Backward variant: 0 = attn_bwd_kernel (4 waves x 32 keys, 2 workgroups per CU), 1 = the
+// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64). Settable for A/B
+// runs in one process (attn_set_bwd_variant); default from FF_ATTN_BWD (0 unless set: at
+// B32 H16 S512 D64 variant 0 measured 0.306 ms vs 0.314 ms for variant 1 — the halved dQ slab
+// traffic did not pay for the lost second workgroup per CU; scripts/attn_probe.py).
+static int g_bwd_variant = -1;
+int attn_bwd_variant() {
+  if (g_bwd_variant < 0) {
+    const char* e = getenv("FF_ATTN_BWD");
+    g_bwd_variant = e ? atoi(e) : 0;
+  }
+  return g_bwd_variant;
+}
+void attn_set_bwd_variant(int v) { g_bwd_variant = v; }
+
+// keys per backward workgroup
+static int bwd_keys(int D) { return (attn_bwd_variant() == 1 && D == 64) ? 256 : 128; }
 
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
-  const int nkb = (Sk + 32 * bwd_waves(Sk) - 1) / (32 * bwd_waves(Sk));
+  const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
@@ -522,16 +772,18 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
 }
 
 void attn_bwd(AttnArgs a, hipStream_t st) {
-  const int nw = bwd_waves(a.Sk);  // only the 4-wave variant is instantiated
-  const int nkb = (a.Sk + 32 * nw - 1) / (32 * nw);
+  const int kg = attn_bwd_variant() == 1;
+  const int nkb = (a.Sk + bwd_keys(a.D) - 1) / bwd_keys(a.D);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
   dim3 grid(nkb, a.B * a.H);
+  dim3 grid1((unsigned)(nkb * a.B * a.H));
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
   dim3 gfin(ew_grid(per / 4, 256));
 #define FFK_ATTN_BWD(DD)                                                                                 \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, gpre, dim3(256), 0, st, a);                               \
-  hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                              \
+  if (kg) hipLaunchKernelGGL((attn_bwd_kg_kernel<DD, DD == 64 ? 2 : 1>), grid1, dim3(256), 0, st, a, nkb); \
+  else hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                         \
   hipLaunchKernelGGL(attn_dq_finish_kernel<DD>, gfin, dim3(256), 0, st, a, nkb);
   if (a.D == 64) {
     FFK_ATTN_BWD(64)

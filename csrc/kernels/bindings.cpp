@@ -302,4 +302,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_ws", &attn_bwd_ws);
+  m.def("attn_set_bwd_variant", [](int v) { ffk::attn_set_bwd_variant(v); });
+  m.def("attn_bwd_variant", []() { return ffk::attn_bwd_variant(); });
 }

@@ -60,7 +60,9 @@ class PerfMetrics:
 
 def _ensure_dist(config: FFConfig):
     if config.world_size > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # FF_DIST_BACKEND=gloo lets several ranks share one GPU (multi-rank rehearsal on a 1-GPU box;
+        # RCCL refuses two ranks on one device)
+        backend = os.environ.get("FF_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if torch.cuda.is_available():
             torch.cuda.set_device(config.local_rank % torch.cuda.device_count())
         kw = {}

@@ -568,15 +568,19 @@ class Executor:
             optimizer.init_state(ar)
 
     # ------------------------------------------------------------------ value access
-    def gather_full(self, t, local: Optional[torch.Tensor], layout: Layout) -> torch.Tensor:
-        """Full logical value on every rank (for get_tensor / get_weights)."""
+    def gather_full(self, t, local: Optional[torch.Tensor], layout: Layout,
+                    dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """Full logical value on every rank (for get_tensor / get_weights). `dtype` is the element
+        type the holders send (weights: their fp32 master copy); ranks that hold no part of the
+        tensor receive into a buffer of that type, so every rank posts the same message sizes."""
         if not self.comm.distributed:
             assert layout.num_parts == 1 or layout.device_set() == (self.rank,), layout
             return local
         dst = Layout(layout.shape, (1,) * layout.ndim, self.world, tuple(range(self.world)))
         tx = Transfer(layout, dst, layout.partial, self.rank)
         self.comm.ensure_groups(tx.rank_sets())
-        return tx.run(self.comm, local, self._like(t))
+        like = self._like(t) if dtype is None else torch.empty(0, dtype=dtype, device=self.device)
+        return tx.run(self.comm, local, like)
 
     def get_value(self, t):
         if self.model.label_tensor is not None and t.guid == self.model.label_tensor.guid:
@@ -592,13 +596,13 @@ class Executor:
         loc = self.weight_tensor(w) if w.guid in self.weight_loc else None
         if loc is not None and w.guid in self.weight_loc:
             loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[0]
-        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False))
+        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False), dtype=torch.float32)
 
     def get_weight_grad(self, w):
         loc = None
         if w.guid in self.weight_loc:
             loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]
-        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False))
+        return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False), dtype=torch.float32)
 
     def set_weight(self, w, value: np.ndarray):
         if w.guid not in self.weight_loc:

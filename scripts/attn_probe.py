@@ -21,15 +21,38 @@ base, dbase = qkv.view(-1), dqkv.view(-1)
 q, k, v = base, base[H * D:], base[2 * H * D:]
 dq, dk, dv = dbase, dbase[H * D:], dbase[2 * H * D:]
 scale = D ** -0.5
-for i in range(reps + 2):
-    if i == 2:
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-    lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
-    Kn.flash_attn_bwd(q, sq, k, sq, v, sq, o, so, do, so, lse, dq, sq, dk, sq, dv, sq, B, H, S, S, D, scale, False)
-e.record()
-e.synchronize()
-ms = s.elapsed_time(e) / reps
-fl = 4.0 * B * H * S * S * D * 3.5
-print(f"attn fwd+bwd B={B} H={H} S={S} D={D}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TFLOPS (fwd+bwd)")
+X = Kn.ext()
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
+fwd_ms = timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False))
+fl_f = 4.0 * B * H * S * S * D
+print(f"attn fwd B={B} H={H} S={S} D={D}: {fwd_ms:.3f} ms {fl_f / fwd_ms / 1e9:.1f} TFLOPS")
+# backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
+res = {0: [], 1: []}
+outs = {}
+for rnd in range(3):
+    for var in (0, 1):
+        X.attn_set_bwd_variant(var)
+        res[var].append(timed(lambda: Kn.flash_attn_bwd(q, sq, k, sq, v, sq, o, so, do, so, lse, dq, sq, dk, sq,
+                                                        dv, sq, B, H, S, S, D, scale, False)))
+        outs[var] = dqkv.clone()
+fl_b = 2.5 * fl_f
+for var in (0, 1):
+    ms = min(res[var])
+    print(f"attn bwd variant {var}: {ms:.3f} ms {fl_b / ms / 1e9:.1f} TFLOPS  (rounds {[round(t, 3) for t in res[var]]})")
+d = (outs[0].float() - outs[1].float()).abs().max().item()
+print(f"max |variant0 - variant1| over dq/dk/dv: {d:.4g}")
+X.attn_set_bwd_variant(0)

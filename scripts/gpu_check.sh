@@ -15,7 +15,12 @@ run() {  # name timeout cmd...
 : > $OUT/steps.log
 for step in "$@"; do
   case $step in
-    tests) run tests 600 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    ktests) run ktests 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -q --timeout 120 --timeout-method thread ;;
+    attn) run attn 300 python -u -m pytest tests/test_kernels_gpu.py -q -k flash --timeout 120 --timeout-method thread ;;
+    probe) run probe 200 python scripts/attn_probe.py 32 16 512 64 20 ;;
+    mtests) run mtests 900 python -u -m pytest tests/test_models_gpu.py -q --timeout 400 --timeout-method thread ;;
+    dtests) run dtests 600 python -u -m pytest tests/test_distributed_gpu.py -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) FF_TUNE_LOG=$OUT/tune.json run bench 600 python bench.py --steps 10 --warmup 3 ;;
     microbench) run microbench 400 python scripts/bench_kernels.py ;;

@@ -107,6 +107,8 @@ def run(name, world, strategy_file=None, steps=2, lr=0.05):
         flags += ["--import-strategy", strategy_file]
     elif world > 1:
         flags += ["--only-data-parallel"]
+    if os.environ.get("FF_TEST_DTYPE"):
+        flags += ["--dtype", os.environ["FF_TEST_DTYPE"]]
     cfg = FFConfig(flags)
     cfg.batch_size = B
     ff = FFModel(cfg)

@@ -81,3 +81,13 @@ def test_parallel_matches_single(name):
     for k, v in ref.items():
         assert k in par, k
         np.testing.assert_allclose(par[k], v, rtol=2e-4, atol=2e-5, err_msg=f"{name}: {k}")
+
+
+def test_bf16_placement_get_weights(monkeypatch):
+    """bf16 model whose ops all sit on rank 0 (a placement the search picks for tiny models): rank 1
+    holds no shard, yet get_weights() must post the same (fp32 master) message sizes on both ranks."""
+    monkeypatch.setenv("FF_TEST_DTYPE", "bf16")
+    ref = _run_single("mlp")
+    par = _run_parallel("mlp_place")
+    for k, v in ref.items():
+        np.testing.assert_allclose(par[k], v, rtol=2e-2, atol=2e-3, err_msg=k)
