@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "dataloader.h"
+#include "graph_utils.h"
 #include "pcg.h"
 
 namespace py = pybind11;
@@ -172,4 +173,86 @@ PYBIND11_MODULE(_core, m) {
       .def("release", &PyBatchRing::release)
       .def("reset", &PyBatchRing::reset)
       .def("depth", &PyBatchRing::depth);
+
+  // ---------------------------------------------------------------- graph / machine utilities
+  py::class_<Digraph>(m, "Digraph")
+      .def(py::init<int>(), py::arg("n") = 0)
+      .def(py::init([](int n, const std::vector<std::pair<int, int>>& edges) {
+             Digraph g(n);
+             for (auto& e : edges) g.add_edge(e.first, e.second);
+             return g;
+           }),
+           py::arg("n"), py::arg("edges"))
+      .def("num_nodes", &Digraph::num_nodes)
+      .def("add_node", &Digraph::add_node)
+      .def("add_edge", &Digraph::add_edge)
+      .def("remove_edge", &Digraph::remove_edge)
+      .def("has_edge", &Digraph::has_edge)
+      .def("successors", &Digraph::successors)
+      .def("predecessors", &Digraph::predecessors)
+      .def("edges", &Digraph::edges)
+      .def("roots", &Digraph::roots)
+      .def("leaves", &Digraph::leaves)
+      .def("topo_order", &Digraph::topo_order)
+      .def("dominators", &Digraph::dominators)
+      .def("post_dominators", &Digraph::post_dominators)
+      .def("imm_dominators", &Digraph::imm_dominators)
+      .def("imm_post_dominators", &Digraph::imm_post_dominators)
+      .def("bottlenecks", &Digraph::bottlenecks)
+      .def("descendants", &Digraph::descendants, py::arg("v"), py::arg("undirected") = false)
+      .def("weakly_connected_components", &Digraph::weakly_connected_components)
+      .def("transitive_reduction", &Digraph::transitive_reduction);
+
+  py::class_<DisjointSet>(m, "DisjointSet")
+      .def(py::init<int>())
+      .def("find", &DisjointSet::find)
+      .def("unite", &DisjointSet::unite)
+      .def("same", &DisjointSet::same)
+      .def("size", &DisjointSet::size);
+  m.def("select_random", &select_random, py::arg("weights"), py::arg("u"));
+  m.def("hash_combine", [](uint64_t seed, uint64_t v) {
+    hash_combine(seed, v);
+    return seed;
+  });
+
+  py::class_<MachineView>(m, "MachineView")
+      .def(py::init([](int start, std::vector<int> dim, std::vector<int> stride) {
+             if (dim.size() != stride.size()) throw std::invalid_argument("MachineView: dim/stride rank mismatch");
+             MachineView v;
+             v.start_device_id = start;
+             v.dim = std::move(dim);
+             v.stride = std::move(stride);
+             return v;
+           }),
+           py::arg("start_device_id") = 0, py::arg("dim") = std::vector<int>{1}, py::arg("stride") = std::vector<int>{1})
+      .def_readwrite("device_type", &MachineView::device_type)
+      .def_readwrite("start_device_id", &MachineView::start_device_id)
+      .def_readwrite("dim", &MachineView::dim)
+      .def_readwrite("stride", &MachineView::stride)
+      .def_property_readonly("ndims", &MachineView::ndims)
+      .def("num_parts", &MachineView::num_parts)
+      .def("device_id", &MachineView::device_id)
+      .def("device_ids", &MachineView::device_ids)
+      .def("hash", &MachineView::hash)
+      .def("__eq__", &MachineView::operator==)
+      .def("__hash__", [](const MachineView& v) { return (int64_t)(v.hash() >> 1); })
+      .def("__repr__", &MachineView::str);
+
+  py::class_<MachineResource>(m, "MachineResource")
+      .def(py::init([](int nodes, int gpus, int avail, int start) {
+             MachineResource r;
+             r.num_nodes = nodes;
+             r.all_gpus_per_node = gpus;
+             r.available_gpus_per_node = avail < 0 ? gpus : avail;
+             r.start_gpu_id = start;
+             return r;
+           }),
+           py::arg("num_nodes") = 1, py::arg("gpus_per_node") = 8, py::arg("available_gpus_per_node") = -1,
+           py::arg("start_gpu_id") = 0)
+      .def_readwrite("num_nodes", &MachineResource::num_nodes)
+      .def_readwrite("all_gpus_per_node", &MachineResource::all_gpus_per_node)
+      .def_readwrite("available_gpus_per_node", &MachineResource::available_gpus_per_node)
+      .def_readwrite("start_gpu_id", &MachineResource::start_gpu_id)
+      .def("is_valid_machine_view", &MachineResource::is_valid_machine_view)
+      .def("enumerate_views", &MachineResource::enumerate_views, py::arg("max_parts") = 0);
 }

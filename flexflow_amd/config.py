@@ -63,7 +63,10 @@ class FFConfig:
         self.synthetic_input = False
         # MI355X-native additions
         self.compute_dtype = DataType.DT_FLOAT  # models built in fp32 unless --dtype bf16
-        self.hip_graphs = True
+        # hipGraph capture of the train step: "auto" captures only when the eager step is short
+        # enough for launch overhead to matter (runtime/graph.py), True always, False never
+        self.hip_graphs = "auto"
+        self.graph_min_step_ms = 15.0
         self.search_algo = "unity"  # unity | mcmc | dp (data-parallel only) | none
         self.mcmc_iterations = 2000
         self.grad_bucket_mb = 64.0
@@ -186,6 +189,8 @@ class FFConfig:
                                       "float": DataType.DT_FLOAT}[v]
             elif a == "--no-hip-graphs":
                 self.hip_graphs = False
+            elif a == "--hip-graphs":
+                self.hip_graphs = True
             elif a == "--search":
                 self.search_algo = nxt()
             elif a == "--mcmc-iterations":

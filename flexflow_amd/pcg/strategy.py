@@ -123,11 +123,34 @@ def divisors(n: int) -> List[int]:
     return [d for d in range(1, n + 1) if n % d == 0]
 
 
+def machine_device_sets(num_devices: int, gpus_per_node: Optional[int] = None) -> Dict[int, List[Tuple[int, ...]]]:
+    """parts -> device tuples of every machine view of the machine (native MachineResource:
+    aligned contiguous blocks `i | N` as the reference's register_all_machine_views,
+    graph.cc:2329-2360, plus whole-node 2-D grids and one-GPU-per-node strided views on multi-node
+    machines). Falls back to contiguous aligned blocks when the native core is not built."""
+    gpn = max(1, min(gpus_per_node or num_devices, num_devices))
+    nodes = max(1, num_devices // gpn)
+    out: Dict[int, List[Tuple[int, ...]]] = {}
+    try:
+        from flexflow_amd import _core
+        res = _core.MachineResource(num_nodes=nodes, gpus_per_node=gpn)
+        for v in res.enumerate_views():
+            ids = tuple(v.device_ids())
+            out.setdefault(len(ids), [])
+            if ids not in out[len(ids)]:
+                out[len(ids)].append(ids)
+    except ImportError:
+        for p in divisors(num_devices):
+            out[p] = [tuple(range(st, st + p)) for st in range(0, num_devices, p)]
+    return out
+
+
 def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute", "parameter"),
-                      max_configs: int = 64, contiguous_starts: bool = True) -> List[OpConfig]:
+                      max_configs: int = 64, contiguous_starts: bool = True,
+                      device_sets: Optional[Dict[int, List[Tuple[int, ...]]]] = None) -> List[OpConfig]:
     """Candidate parallelizations of one op: degree combos over its allowed axes whose product
-    divides the device count, placed on aligned contiguous device blocks (reference
-    register_all_machine_views: 1-D views `i | N`, graph.cc:2329-2360)."""
+    divides the device count, each placed on every machine view with that many parts
+    (machine_device_sets; contiguous_starts=False keeps only the view starting at device 0)."""
     impl = layer.impl
     pin = getattr(impl, "pinned_config", None)
     if pin is not None:  # explicit parallel ops (ops/parallel_ops.py) fix their output layout
@@ -137,15 +160,17 @@ def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute
     axes = [a for a, k in enumerate(kinds) if k in allow_kinds and impl.supports_axis(a)]
     out: List[OpConfig] = []
     degs = [1] * len(sizes)
+    if device_sets is None:
+        device_sets = machine_device_sets(num_devices)
 
     def rec(i, prod):
         if i == len(axes):
             P = prod
-            starts = range(0, num_devices, P) if contiguous_starts else [0]
-            for st in starts:
-                if st + P > num_devices:
-                    continue
-                cfg = OpConfig(tuple(degs), tuple(range(st, st + P)))
+            sets = device_sets.get(P, [tuple(range(P))])
+            if not contiguous_starts:
+                sets = [s for s in sets if s[0] == 0][:1] or sets[:1]
+            for devs in sets:
+                cfg = OpConfig(tuple(degs), tuple(devs))
                 if valid_config(layer, cfg):
                     out.append(cfg)
             return

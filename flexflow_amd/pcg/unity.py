@@ -86,8 +86,11 @@ def build_problem(model, n_devices: int, measure: bool):
     all_cands = []
     nodes = []
     out_t = model.output_tensor()
+    from .strategy import machine_device_sets
+    dsets = machine_device_sets(n_devices, prob.machine.gpus_per_node)
     for i, L in enumerate(layers):
-        cands = enumerate_configs(L, n_devices, kinds, max_configs=int(os.environ.get("FF_MAX_CANDS", "32")))
+        cands = enumerate_configs(L, n_devices, kinds, max_configs=int(os.environ.get("FF_MAX_CANDS", "32")),
+                                  device_sets=dsets)
         dp = data_parallel_config(L, n_devices)
         if dp not in cands:
             cands.append(dp)

@@ -8,6 +8,12 @@ optimizer update (one fused kernel per arena, with host-side bias-corrected scal
 bucket all-reduces that belong to it run after the replay. Multi-rank steps with in-step
 collectives are captured too when FF_GRAPH_COLLECTIVES=1 (RCCL supports stream capture);
 otherwise they run eagerly with backward-overlapped bucketed all-reduce.
+
+Policy (config.hip_graphs = "auto", the default): the eager warm-up steps are timed; a step whose
+GPU work is long (>= config.graph_min_step_ms, e.g. BERT-Large: 55 ms) keeps running eagerly —
+measured on MI355X, replaying its ~800-node graph took 58.7 ms/step against 55.1 ms eager (the
+graph's per-node dispatch costs more than the host's launch stream, which runs far ahead of the
+GPU) — while short steps (DLRM, small CNNs), where host launch latency dominates, are captured.
 """
 from __future__ import annotations
 
@@ -22,11 +28,15 @@ class StepGraph:
         self.graph = None
         self.warm = 0
         self.failed = False
+        self.eager_ms = []  # timed eager warm-up steps ("auto" policy)
+        self.decision = None
 
     def enabled(self) -> bool:
         m = self.model
         ex = m.executor
         if not (m.config.hip_graphs and torch.cuda.is_available() and ex.device.type == "cuda"):
+            return False
+        if self.decision is False:
             return False
         if self.failed or ex.hooks:  # per-op hooks time / inspect individual ops: run eagerly
             return False
@@ -45,10 +55,21 @@ class StepGraph:
             return
         if self.warm < 2:
             self.warm += 1
+            auto = m.config.hip_graphs == "auto"
+            if auto and self.warm == 2:  # the first step pays autotuning; time the second
+                torch.cuda.synchronize()
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
             ex.zero_gradients()
             ex.forward()
             ex.backward()
             ex.update(m.optimizer)
+            if auto and self.warm == 2:
+                en.record()
+                en.synchronize()
+                ms = st.elapsed_time(en)
+                self.eager_ms.append(ms)
+                self.decision = ms < float(m.config.graph_min_step_ms)
             return
         if self.graph is None:
             torch.cuda.synchronize()
