@@ -5,11 +5,16 @@ kernel per GPU shard each iteration. Here each rank keeps the dataset in host me
 `next_batch`, stages ONLY its own shard of the batch (per the input tensor's layout) into a
 persistent device buffer with an asynchronous pinned-memory H2D copy. When the native data-loader
 ring (flexflow_amd._core.BatchRing) is available the next batch is pre-gathered into pinned memory
-by a background C++ thread while the current step runs.
+by a background C++ thread while the current step runs, and on a GPU its host->device copy is
+issued on the device context's h2d stream right after the current batch is fed
+(runtime/device.H2DPrefetcher: pinned host slots, two device staging buffers, the compute stream
+waits on the copy's event only when the batch is consumed), so input staging never sits on the
+step's critical path.
 """
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from ..type import DataType
 
@@ -36,12 +41,22 @@ class SingleDataLoader:
         self.idx = 0
         self._ring = None
         self._slot = None
+        self._pf = None          # H2D prefetcher (GPU only)
+        self._inflight = None    # host slot whose copy is in flight
         if self.full.shape[0] >= bs:
             try:
                 from flexflow_amd import _core
                 # 3 host staging slots filled by the native background thread (gather of the next
-                # batch overlaps the current step); a slot is handed back once its batch was fed
-                self._bufs = [np.empty((bs,) + self.full.shape[1:], dtype=self.full.dtype) for _ in range(3)]
+                # batch overlaps the current step); a slot is handed back once its batch was fed.
+                # On a GPU the slots are pinned so their H2D copies are truly asynchronous.
+                shape = (bs,) + self.full.shape[1:]
+                if torch.cuda.is_available():
+                    self._pinned = [torch.empty(shape, dtype=torch.from_numpy(self.full[:1]).dtype, pin_memory=True)
+                                    for _ in range(3)]
+                    self._bufs = [t.numpy() for t in self._pinned]
+                else:
+                    self._pinned = None
+                    self._bufs = [np.empty(shape, dtype=self.full.dtype) for _ in range(3)]
                 self._ring = _core.BatchRing(self.full, bs, self._bufs)
             except (ImportError, RuntimeError, TypeError):
                 self._ring = None
@@ -56,16 +71,49 @@ class SingleDataLoader:
 
     def reset(self):
         self.idx = 0
+        self._drop_prefetch()
         if self._ring is not None:
             self._ring.reset(0)
+
+    def _drop_prefetch(self):
+        if self._pf is not None and self._pf.pending is not None:
+            self._pf.take()
+            self._release_inflight()
+
+    def _release_inflight(self):
+        if self._inflight is not None:
+            ev = self._pf.events[self._pf.i] if self._pf is not None else None
+            if ev is not None:
+                ev.synchronize()
+            self._ring.release(self._inflight)
+            self._inflight = None
+
+    def _prefetch(self, m):
+        if self._pf is None:
+            from ..runtime.device import DeviceContext, H2DPrefetcher
+            self._pf = H2DPrefetcher(DeviceContext.get(m.executor.device))
+        slot = self._ring.next()
+        self._pf.stage(self._pinned[slot])
+        self._inflight = slot
 
     def next_batch(self, ffmodel=None):
         m = ffmodel or self.model
         bs = self.batch_size
         if self.idx + bs > self._num_samples:
             self.idx = 0
+            self._drop_prefetch()
             if self._ring is not None:
                 self._ring.reset(0)
+        if self._ring is not None and self._pinned is not None and m.executor.device.type == "cuda":
+            if self._pf is None or self._pf.pending is None:
+                self._prefetch(m)
+            dev = self._pf.take()
+            m.executor.feed(self.tensor, dev)  # device-to-device, ordered after the H2D event
+            self._release_inflight()
+            self.idx += bs
+            if self.idx + bs <= self._num_samples:  # stage the next batch under the coming step
+                self._prefetch(m)
+            return
         if self._ring is not None:
             slot = self._ring.next()
             m.executor.feed(self.tensor, self._bufs[slot])  # pageable source: the copy is complete on return

@@ -333,7 +333,9 @@ def flash_attn_fwd(q, qs, k, ks, v, vs, o, os_, B, H, Sq, Sk, D, scale, causal):
 def flash_attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, B, H, Sq, Sk, D, scale,
                    causal):
     X = ext()
-    ws = torch.empty(X.attn_bwd_ws(B, H, Sq, Sk, D), device=q.device, dtype=torch.float32)
+    from ..runtime.device import DeviceContext
+    # dQ partial slabs + delta: one arena buffer shared (stream-ordered) by every attention layer
+    ws = DeviceContext.get(q.device).workspace("attn_bwd", X.attn_bwd_ws(B, H, Sq, Sk, D))
     X.attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, ws, B, H, Sq, Sk, D, scale,
                causal)
 
