@@ -87,6 +87,40 @@ def _views(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC):
 
 _ADDMM_F32_OUT = [True]  # torch.addmm(out_dtype=fp32, out=C) usable in place
 
+# Library-GEMM solution table. The vendor GEMMs (plain, no fused epilogue) go through PyTorch's
+# TunableOp, which picks per (layout, M, N, K) among every hipBLASLt and rocBLAS solution instead of
+# the library heuristic; the picks for our models' shapes were measured on an MI355X and ship in
+# tuning/tunableop_gfx950.csv (its Validator lines pin the torch / HIP / hipBLASLt / rocBLAS versions,
+# a mismatching table is ignored). FF_TUNABLEOP=use (default) reads the table with tuning off
+# (unlisted shapes keep the library default), =tune also tunes unlisted shapes and writes the
+# merged table to FF_TUNABLEOP_FILE at exit, =off leaves TunableOp alone.
+TUNABLE_CSV = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..", "tuning", "tunableop_gfx950.csv")
+_tunable_state = [None]
+
+
+def tunable_setup():
+    if _tunable_state[0] is not None:
+        return _tunable_state[0]
+    mode = _os.environ.get("FF_TUNABLEOP", "use")
+    state = "off"
+    if mode != "off" and torch.cuda.is_available():
+        import torch.cuda.tunable as tun
+        if mode == "tune":
+            tun.enable(True)
+            tun.tuning_enable(True)
+            if _os.path.exists(TUNABLE_CSV):
+                tun.read_file(TUNABLE_CSV)
+            tun.set_filename(_os.environ.get("FF_TUNABLEOP_FILE", "tunableop_results.csv"), False)
+            state = "tune"
+        elif _os.path.exists(TUNABLE_CSV):
+            tun.enable(True)
+            tun.tuning_enable(False)
+            state = "use" if tun.read_file(TUNABLE_CSV) else "rejected"
+            if state == "rejected":
+                tun.enable(False)
+    _tunable_state[0] = state
+    return state
+
 
 def _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC):
     """Plain GEMM on the vendor library (hipBLASLt via torch): bf16 in, bf16 or fp32 out, optional
@@ -164,6 +198,8 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
     pre-activation store — the vendor library GEMM. splitk=None lets each kernel pick its split."""
     if native(C) and A.dtype == torch.bfloat16:
         X = ext()
+        if _tunable_state[0] is None:
+            tunable_setup()
 
         def ours(impl, out=C, sk=None):
             s = sk if sk is not None else (splitk if splitk is not None else

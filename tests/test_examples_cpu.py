@@ -1,0 +1,45 @@
+"""The examples/ tree runs end to end on CPU at reduced sizes (reference test strategy: the
+examples/python/* scripts are exercised by tests/python_interface_test.sh, and the
+osdi22ae scripts by the artifact runs). Each script runs in its own process, as a user would."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, "examples", "python")
+
+CASES = [
+    ("native/mnist_mlp.py", ["-b", "64", "-e", "2", "--samples", "2048", "-a"]),
+    ("native/mnist_cnn.py", ["-b", "32", "--samples", "256"]),
+    ("native/cifar10_cnn_concat.py", ["-b", "32", "--samples", "128"]),
+    ("native/multi_head_attention.py", ["-b", "2", "--seq-length", "16", "--hidden-size", "32", "--num-heads", "4",
+                                        "--iterations", "2", "--explicit"]),
+    ("native/bert_proxy_native.py", ["-b", "2", "--seq-length", "16", "--hidden-size", "32", "--num-heads", "4",
+                                     "--num_layers", "2", "--iterations", "2", "--train"]),
+    ("native/print_layers.py", []),
+    ("native/alexnet.py", ["-b", "4", "--iterations", "1", "--small"]),
+    ("native/dlrm.py", ["-b", "16", "--iterations", "2", "--small"]),
+    ("native/transformer.py", ["-b", "2", "--iterations", "1", "--small"]),
+    ("native/mixture_of_experts.py", ["-b", "16", "--iterations", "2", "--small"]),
+    ("keras/seq_mnist_mlp.py", ["--samples", "1024", "-a"]),
+    ("keras/func_mnist_mlp_concat.py", ["--samples", "512"]),
+    ("keras/seq_reuters_mlp.py", ["--samples", "1024"]),
+    ("pytorch/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-a"]),
+]
+
+
+@pytest.mark.parametrize("script,args", CASES, ids=[c[0] for c in CASES])
+def test_example_runs(script, args, tmp_path):
+    env = dict(os.environ, FF_TUNABLEOP="off")
+    r = subprocess.run([sys.executable, os.path.join(EX, script)] + args, cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_osdi_scripts_parse():
+    d = os.path.join(ROOT, "examples", "scripts", "osdi22ae")
+    for f in sorted(os.listdir(d)):
+        r = subprocess.run(["bash", "-n", os.path.join(d, f)], capture_output=True, text=True)
+        assert r.returncode == 0, (f, r.stderr)
