@@ -92,8 +92,8 @@ _ADDMM_F32_OUT = [True]  # torch.addmm(out_dtype=fp32, out=C) usable in place
 # the library heuristic; the picks for our models' shapes were measured on an MI355X and ship in
 # tuning/tunableop_gfx950.csv (its Validator lines pin the torch / HIP / hipBLASLt / rocBLAS versions,
 # a mismatching table is ignored). FF_TUNABLEOP=use (default) reads the table with tuning off
-# (unlisted shapes keep the library default), =tune also tunes unlisted shapes and writes the
-# merged table to FF_TUNABLEOP_FILE at exit, =off leaves TunableOp alone.
+# (unlisted shapes keep the library default), =tune tunes every shape met and writes the table
+# to FF_TUNABLEOP_FILE at exit, =off leaves TunableOp alone.
 TUNABLE_CSV = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..", "tuning", "tunableop_gfx950.csv")
 _tunable_state = [None]
 
@@ -106,10 +106,10 @@ def tunable_setup():
     if mode != "off" and torch.cuda.is_available():
         import torch.cuda.tunable as tun
         if mode == "tune":
+            # tunes every shape it meets from scratch: the file written at exit holds only what
+            # this process tuned, so a table read in first would be dropped from it
             tun.enable(True)
             tun.tuning_enable(True)
-            if _os.path.exists(TUNABLE_CSV):
-                tun.read_file(TUNABLE_CSV)
             tun.set_filename(_os.environ.get("FF_TUNABLEOP_FILE", "tunableop_results.csv"), False)
             state = "tune"
         elif _os.path.exists(TUNABLE_CSV):
@@ -177,6 +177,14 @@ def _lib_gemm_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act):
     ext().bias_act_fwd(zbuf, bias, zbuf if bias is not None else None, C, M, N, act)
 
 
+def _lib_gemm_bias_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act):
+    """Library GEMM with the bias in its epilogue (z = x.w^T + b written once), then our activation
+    pass reads z and writes y only: one [M, N] write less than _lib_gemm_act."""
+    zbuf = Z if Z is not None else C
+    _lib_gemm(A, B, zbuf, M, N, K, a_k, b_k, lda, ldb, N, 1.0, 0.0, bias, 1, 0, 0, 0)
+    ext().bias_act_fwd(zbuf, None, None, C, M, N, act)
+
+
 def _time(fn, reps=8):
     fn()
     fn()
@@ -229,6 +237,9 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                     zs = torch.empty_like(C) if Z is not None else None
                     cands["lib_act"] = lambda: _lib_gemm_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda, ldb, bias,
                                                              act)
+                    if bias is not None and act != ACT_NONE:
+                        cands["lib_bias_act"] = lambda: _lib_gemm_bias_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda,
+                                                                           ldb, bias, act)
                 times = {k: _time(f) for k, f in cands.items()}
                 choice = min(times, key=times.get)
                 TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
@@ -238,6 +249,8 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC)
         elif choice == "lib_act":
             _lib_gemm_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act)
+        elif choice == "lib_bias_act":
+            _lib_gemm_bias_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act)
         else:
             ours(IMPLS[choice])
         return C

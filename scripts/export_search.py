@@ -26,5 +26,21 @@ else:
     from flexflow_amd.models import build
     _, _, loss, mets, _ = build(name, ff, batch)
 ff.optimizer = AdamOptimizer(ff, 1e-3)
-ff.compile(loss_type=loss, metrics=mets)
-print(json.dumps({k: v for k, v in (ff.search_report or {}).items() if k != "measured_costs"}, default=str)[:2000])
+if int(os.environ.get("WORLD_SIZE", "1")) >= n:
+    ff.compile(loss_type=loss, metrics=mets)
+    report = ff.search_report
+else:
+    # one process planning for N devices: run compile()'s graph passes and the search only (an
+    # executor for N ranks cannot be built here), then export the strategy
+    import time
+    from flexflow_amd.pcg.search import choose_strategy
+    from flexflow_amd.pcg.strategy import save_strategy
+    from flexflow_amd.pcg.substitutions import optimize_graph
+    t0 = time.perf_counter()
+    subst = optimize_graph(ff)
+    strat, report = choose_strategy(ff)
+    report = dict(report or {}, substitutions=subst, wall_s=round(time.perf_counter() - t0, 2))
+    save_strategy(out, strat, n, {k: v for k, v in report.items() if k != "measured_costs"})
+    multi = sorted({tuple(c.degrees) for c in strat.values() if c.num_parts > 1})
+    report["distinct_degree_vectors"] = [list(d) for d in multi][:20]
+print(json.dumps({k: v for k, v in (report or {}).items() if k != "measured_costs"}, default=str)[:4000])
