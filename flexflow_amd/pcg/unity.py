@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import os
 import time
+from types import SimpleNamespace
 
 import torch
 
@@ -47,6 +48,8 @@ def machine_model(cfg):
     gpn = max(1, min(cfg.local_world_size if cfg.search_num_workers is None else cfg.search_num_workers, n))
     mm.gpus_per_node = gpn
     mm.num_nodes = max(1, n // gpn)
+    if cfg.device_mem and cfg.device_mem > 0:  # -ll:fsize, MiB of device memory per GPU
+        mm.mem_capacity = float(cfg.device_mem) * (1 << 20)
     if cfg.machine_model_file and os.path.exists(cfg.machine_model_file):
         import json
         with open(cfg.machine_model_file) as f:
@@ -134,12 +137,17 @@ def search(model, algo: str):
     dp_choice = [cands[i].index(data_parallel_config(L, n)) for i, L in enumerate(model.layers)]
     dp_sim = core.simulate(prob, dp_choice).makespan_ms
     budget = cfg.search_budget if cfg.search_budget and cfg.search_budget > 0 else None
-    if algo == "mcmc":
-        iters = budget or cfg.mcmc_iterations
-        res = core.search_mcmc(prob, dp_choice, iters, cfg.search_alpha, cfg.seed)
+
+    def run_search():
+        if algo == "mcmc":
+            return core.search_mcmc(prob, dp_choice, budget or cfg.mcmc_iterations, cfg.search_alpha, cfg.seed)
+        return core.search_unity(prob, 4096, budget if budget is not None else 300, cfg.search_alpha, cfg.seed)
+
+    mem_report = None
+    if cfg.perform_memory_search:
+        res, mem_report = memory_search(prob, run_search)
     else:
-        iters = budget if budget is not None else 300
-        res = core.search_unity(prob, 4096, iters, cfg.search_alpha, cfg.seed)
+        res = run_search()
     choice = list(res.choice)
     if res.cost_ms > dp_sim:  # never pick something the simulator thinks is worse than DP
         choice = dp_choice
@@ -150,4 +158,67 @@ def search(model, algo: str):
               "mcmc_iterations": int(res.iterations), "build_s": round(t_build, 3),
               "search_s": round(time.perf_counter() - t0 - t_build, 3), "measured_costs": bool(do_measure),
               "candidates": sum(len(c) for c in cands)}
+    if mem_report is not None:
+        report["memory_search"] = mem_report
     return strat, report
+
+
+def _set_lambda(prob, base, lam):
+    """cost'(candidate) = fwd_ms + lam * GiB the candidate keeps on each of its devices."""
+    nodes = prob.nodes
+    for node, bs in zip(nodes, base):
+        cc = node.cands
+        for oc, (f, m) in zip(cc, bs):
+            oc.fwd_ms = f + lam * m / float(1 << 30)
+        node.cands = cc
+    prob.nodes = nodes
+
+
+def memory_search(prob, run_search, max_iters: int = 10):
+    """Memory-aware search (reference src/runtime/memory_optimization.cc + graph.cc's
+    lambda loop): minimise run time + lambda * per-device memory, with lambda (ms per GiB) raised
+    by doubling and then bisected until the simulated peak per-device memory fits the machine's
+    capacity (-ll:fsize MiB, or mem_capacity of --machine-model-file; 288 GB HBM3E by default).
+    The smallest fitting lambda wins: the fastest strategy that fits. The search's own costs
+    are restored before the final simulation, so reported times are real run-time predictions."""
+    core = _core()
+    cap = prob.machine.mem_capacity
+    base = [[(oc.fwd_ms, oc.mem_bytes) for oc in node.cands] for node in prob.nodes]
+
+    def attempt(lam):
+        _set_lambda(prob, base, lam)
+        r = run_search()
+        _set_lambda(prob, base, 0.0)
+        sim = core.simulate(prob, list(r.choice))
+        return r, sim
+
+    res, sim = attempt(0.0)
+    tried = [(0.0, sim.max_mem)]
+    best = (res, sim, 0.0) if sim.max_mem <= cap else None
+    if best is None:
+        lo, hi = 0.0, 1.0
+        while len(tried) < max_iters:
+            r, s = attempt(hi)
+            tried.append((hi, s.max_mem))
+            if s.max_mem <= cap:
+                best = (r, s, hi)
+                break
+            lo, hi = hi, hi * 8
+        while best is not None and len(tried) < max_iters and hi - lo > 1e-3 * hi:
+            mid = 0.5 * (lo + hi)
+            r, s = attempt(mid)
+            tried.append((mid, s.max_mem))
+            if s.max_mem <= cap:
+                best, hi = (r, s, mid), mid
+            else:
+                lo = mid
+    if best is None:  # nothing fits: keep the least-memory strategy found
+        res, sim = attempt(tried[-1][0])
+        best = (res, sim, tried[-1][0])
+    r, sim, lam = best
+    # the real (lambda-free) simulated time of the chosen strategy
+    res = SimpleNamespace(choice=list(r.choice), cost_ms=sim.makespan_ms, dp_cost_ms=r.dp_cost_ms, states=r.states,
+                          iterations=r.iterations)
+    return res, {"lambda_ms_per_gib": lam, "capacity_gib": round(cap / (1 << 30), 3),
+                 "max_mem_gib": round(sim.max_mem / (1 << 30), 4), "fits": bool(sim.max_mem <= cap),
+                 "iterations": len(tried), "tried": [(round(a, 4), round(b / (1 << 30), 4)) for a, b in tried]}
