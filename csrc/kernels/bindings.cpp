@@ -217,6 +217,13 @@ void init_normal(Tensor out, double mean, double stdv, int64_t seed, int64_t off
   ffk::init_normal(dtcode(out), out.data_ptr(), out.numel(), mean, stdv, seed, offset, cur_stream());
 }
 void fill(Tensor out, double v) { ffk::fill(dtcode(out), out.data_ptr(), out.numel(), v, cur_stream()); }
+void slab_sum(Tensor slabs, Tensor out, int64_t S, double beta) {
+  TORCH_CHECK(slabs.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && slabs.is_contiguous() &&
+              out.is_contiguous());
+  TORCH_CHECK(slabs.numel() == out.numel() * S && out.numel() % 4 == 0);
+  TORCH_CHECK(((uintptr_t)slabs.data_ptr() % 16) == 0 && ((uintptr_t)out.data_ptr() % 16) == 0);
+  ffk::slab_sum(slabs.data_ptr<float>(), out.data_ptr<float>(), out.numel(), (int)S, (float)beta, cur_stream());
+}
 
 // q/k/v/o given with explicit [b,h,s] element strides (d contiguous)
 void attn_fwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
@@ -299,6 +306,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("init_uniform", &init_uniform);
   m.def("init_normal", &init_normal);
   m.def("fill", &fill);
+  m.def("slab_sum", &slab_sum);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_ws", &attn_bwd_ws);

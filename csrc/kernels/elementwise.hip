@@ -345,6 +345,30 @@ void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st)
   col_reduce_add2(part, out, nullptr, R, C, st);
 }
 
+// out[i] = beta * out[i] + sum_s slabs[s][i] (fp32, n % 4 == 0, 16-B aligned): the reduction of a
+// split-K GEMM whose S partial products were written as S slabs by one strided-batched GEMM.
+__global__ void slab_sum_kernel(const float4* __restrict__ slabs, float4* __restrict__ out, int64_t nv, int S,
+                                float beta) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float4 a = slabs[i];
+    for (int s = 1; s < S; ++s) {
+      const float4 b = slabs[(int64_t)s * nv + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (beta != 0.f) {
+      const float4 c = out[i];
+      a.x += beta * c.x; a.y += beta * c.y; a.z += beta * c.z; a.w += beta * c.w;
+    }
+    out[i] = a;
+  }
+}
+void slab_sum(const float* slabs, float* out, int64_t n, int S, float beta, hipStream_t st) {
+  const int64_t nv = n / 4;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(ew_grid(nv, 256)), dim3(256), 0, st, (const float4*)slabs, (float4*)out, nv,
+                     S, beta);
+}
+
 static void bab_geometry(int rows, int cols, int& gx, int& gy, int& rpb) {
   gx = (cols + BAB_COLS - 1) / BAB_COLS;
   // >= ~1024 blocks where the shape allows (4+ per CU), >= 32 rows per block (one 8-row batch

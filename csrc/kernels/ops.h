@@ -37,6 +37,7 @@ void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias,
                   int act, hipStream_t st);
 int bias_act_bwd_chunks(int rows, int cols);
 void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st);
+void slab_sum(const float* slabs, float* out, int64_t n, int S, float beta, hipStream_t st);
 // out0 += colsum(part[0:R]); out1 += colsum(part[R:2R]) (out1 may be null)
 void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st);
 

@@ -185,6 +185,21 @@ def _lib_gemm_bias_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act):
     ext().bias_act_fwd(zbuf, None, None, C, M, N, act)
 
 
+def _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, S):
+    """fp32-output GEMM (a weight gradient: K = tokens, small M x N) as S K-slices of ONE
+    strided-batched library GEMM into fp32 slabs, summed (+ beta * C) by our slab_sum kernel. The
+    single-shot library GEMM leaves most CUs idle on these shapes (<= 256 output tiles, K >= 8k);
+    the batch dimension multiplies its tiles by S."""
+    Af, Bf, _ = _views(A, B, C, M, N, K, a_k, b_k, lda, ldb, N, 1, 0, 0, 0)
+    a2, b2 = Af[0], Bf[0]
+    kc = K // S
+    a3 = a2.as_strided((S, M, kc), (kc * a2.stride(1), a2.stride(0), a2.stride(1)))
+    b3 = b2.as_strided((S, kc, N), (kc * b2.stride(0), b2.stride(0), b2.stride(1)))
+    slabs = torch.empty((S, M, N), device=C.device, dtype=torch.float32)
+    torch.bmm(a3, b3, out_dtype=torch.float32, out=slabs)
+    ext().slab_sum(slabs, C, S, beta)
+
+
 def _time(fn, reps=8):
     fn()
     fn()
@@ -231,6 +246,12 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                 if plain:
                     cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
                                                      bias, batch, sA, sB, sC)
+                    if C.dtype == torch.float32 and batch == 1 and alpha == 1.0 and bias is None and \
+                            C.is_contiguous() and (M * N) % 4 == 0 and M * N <= (1 << 24) and K >= 8192:
+                        for S in (2, 4, 8):
+                            if K % (S * 8) == 0:
+                                cands[f"lib_sk{S}"] = (lambda S=S: _lib_gemm_splitk(A, B, scratch, M, N, K, a_k, b_k,
+                                                                                    lda, ldb, beta, S))
                 if (act != ACT_NONE or bias is not None) and alpha == 1.0 and beta == 0.0 and batch == 1 and \
                         ldc == N and N % 8 == 0 and C.dtype == torch.bfloat16 and \
                         (Z is None or Z.dtype == torch.bfloat16):
@@ -245,7 +266,9 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                 TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
                                  "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
             _tuned[key] = choice
-        if choice == "lib":
+        if isinstance(choice, str) and choice.startswith("lib_sk"):
+            _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, int(choice[6:]))
+        elif choice == "lib":
             _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC)
         elif choice == "lib_act":
             _lib_gemm_act(A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, bias, act)

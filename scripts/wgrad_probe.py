@@ -56,13 +56,24 @@ def main():
         r["lib_bf16_plus_add"] = t_ms(lambda: (torch.mm(dz.t(), x, out=wb), dw.add_(wb)))
         r["tn_gemm_only"] = t_ms(lambda: torch.mm(dzt, xt.t(), out=wb))
         r["transpose_copies"] = t_ms(lambda: (dzt.copy_(dz.t()), xt.copy_(x.t())))
+        for S in (2, 4, 8):  # split-K over the token dim as one strided-batched library GEMM
+            a3 = dz.view(S, T // S, N).transpose(1, 2)
+            b3 = x.view(S, T // S, Kd)
+            try:
+                part = torch.empty(S, N, Kd, device=dev, dtype=torch.float32)
+                r[f"bmm_split{S}_f32"] = t_ms(lambda: (torch.bmm(a3, b3, out_dtype=torch.float32, out=part),
+                                                        torch.sum(part, 0, out=dw)))
+            except (RuntimeError, TypeError) as e:
+                r[f"bmm_split{S}_f32_err"] = str(e)[:80]
+            partb = torch.empty(S, N, Kd, device=dev, dtype=torch.bfloat16)
+            r[f"bmm_split{S}_bf16"] = t_ms(lambda: (torch.bmm(a3, b3, out=partb), dw.add_(partb.float().sum(0))))
         for name, impl in K.IMPLS.items():
             r["ours_" + name] = t_ms(lambda: ours(X, dz, x, dw, N, Kd, T, impl))
         ref = (dz.float().t() @ x.float())
         torch.mm(dz.t(), x, out=wb)
         r["bf16_out_rel_err"] = float((wb.float() - ref).norm() / ref.norm())
         fl = 2.0 * T * N * Kd
-        best = min((v, k) for k, v in r.items() if k.startswith(("lib", "tn", "ours")))
+        best = min((v, k) for k, v in r.items() if k.startswith(("lib", "tn", "ours", "bmm")) and isinstance(v, float))
         r["best"] = best[1]
         r["best_tflops"] = round(fl / best[0] / 1e9, 1)
         print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)

@@ -345,3 +345,21 @@ def test_lib_gemm_bias_act_epilogue(ffC, act, with_bias, with_z):
         assert _rel(C, ref) < 1e-2
         if with_z:
             assert _rel(Z, z) < 1e-2
+
+
+@pytest.mark.parametrize("a_k,b_k", [(False, False), (True, True), (True, False)])
+@pytest.mark.parametrize("S,beta", [(2, 0.0), (4, 1.0), (8, 1.0)])
+def test_lib_splitk_wgrad(ffC, a_k, b_k, S, beta):
+    """Split-K library GEMM (S K-slices in one strided-batched GEMM, fp32 slabs) + slab_sum, fp32
+    out with beta accumulate: the weight-gradient path, against an fp32 reference."""
+    from flexflow_amd import kernels as K
+    M, N, Kd = 768, 512, 8192
+    g = torch.Generator(device=DEV).manual_seed(0)
+    A = (torch.randn(M, Kd, device=DEV, generator=g) if a_k else torch.randn(Kd, M, device=DEV, generator=g)).bfloat16()
+    B = (torch.randn(N, Kd, device=DEV, generator=g) if b_k else torch.randn(Kd, N, device=DEV, generator=g)).bfloat16()
+    C = torch.randn(M, N, device=DEV, generator=g)
+    Af = A.float() if a_k else A.float().t()
+    Bf = B.float().t() if b_k else B.float()
+    ref = Af @ Bf + beta * C
+    K._lib_gemm_splitk(A, B, C, M, N, Kd, a_k, b_k, A.shape[-1], B.shape[-1], beta, S)
+    assert _rel(C, ref) < 2e-3
