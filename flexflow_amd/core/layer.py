@@ -74,3 +74,31 @@ class Layer:
     def __repr__(self):
         return f"Layer({self.name}, {self.op_type.name}, in={[list(t.dims) for t in self.inputs]}, " \
                f"out={[list(t.dims) for t in self.outputs]})"
+
+
+# Per-operator layer classes of the reference Python API (flexflow_cffi.py: Exp, Conv2D, Linear, ...,
+# returned by get_layer_by_id / get_layers through convert_op_handle_to_op). Here every layer is a
+# Layer; the op-specific class is a marker subclass assigned at creation, so isinstance checks and
+# type(layer).__name__ behave as in the reference.
+_OP_CLASS_NAMES = {
+    "OP_EXP": "Exp", "OP_SIN": "Sin", "OP_COS": "Cos", "OP_EW_ADD": "Add", "OP_EW_SUB": "Subtract",
+    "OP_EW_MUL": "Multiply", "OP_EW_DIV": "Divide", "OP_EW_MAX": "Max", "OP_EW_MIN": "Min",
+    "OP_REDUCE_SUM": "ReduceSum", "OP_CONV2D": "Conv2D", "OP_POOL2D": "Pool2D", "OP_LINEAR": "Linear",
+    "OP_FLAT": "Flat", "OP_SOFTMAX": "Softmax", "OP_EMBEDDING": "Embedding", "OP_CONCAT": "Concat",
+    "OP_BATCHNORM": "BatchNorm", "OP_LAYERNORM": "LayerNorm", "OP_DROPOUT": "Dropout",
+    "OP_SCALAR_MULTIPLY": "ScalarMultiply", "OP_SCALAR_ADD": "ScalarAdd", "OP_SCALAR_SUB": "ScalarSub",
+    "OP_SCALAR_TRUE_DIV": "ScalarTrueDiv", "OP_RSQRT": "Rsqrt", "OP_POW": "Pow", "OP_MEAN": "Mean",
+    "OP_RELU": "Relu", "OP_GELU": "Gelu", "OP_SIGMOID": "Sigmoid", "OP_TANH": "Tanh", "OP_ELU": "Elu",
+    "OP_BATCHMATMUL": "Batch_Matmul", "OP_SPLIT": "Split", "OP_RESHAPE": "Reshape", "OP_GATHER": "Gather",
+    "OP_IDENTITY": "Identity", "OP_TRANSPOSE": "Transpose", "OP_REVERSE": "Reverse",
+    "OP_MULTIHEAD_ATTENTION": "MultiHeadAttention",
+}
+OP_CLASSES: Dict[OperatorType, type] = {}
+for _op, _cls in _OP_CLASS_NAMES.items():
+    if hasattr(OperatorType, _op):
+        OP_CLASSES[getattr(OperatorType, _op)] = type(_cls, (Layer,), {"__doc__": f"{_cls} layer (reference flexflow_cffi.{_cls})."})
+Batch_Norm = OP_CLASSES.get(OperatorType.OP_BATCHNORM)
+
+
+def op_class(op_type: OperatorType) -> type:
+    return OP_CLASSES.get(op_type, Layer)

@@ -22,7 +22,7 @@ import torch.distributed as dist
 from ..config import FFConfig
 from ..type import (ActiMode, AggrMode, CompMode, DataType, LossType, MetricsType, OperatorType, PoolType,
                     RegularizerMode)
-from .layer import Layer
+from .layer import Layer, op_class
 from .tensor import Parameter, Tensor
 
 
@@ -97,8 +97,16 @@ class FFModel:
     # ================================================================== graph building
     def _add(self, op_type, inputs, name=None, **attrs):
         L = Layer(self, op_type, name, inputs, attrs)
+        L.__class__ = op_class(op_type)  # reference per-op layer class (Linear, Conv2D, ...)
         self.layers.append(L)
         return L
+
+    def add_layer(self, op_type, name):
+        """reference FFModel.add_layer (flexflow_cffi.py:913): registers the last created op with the
+        Python layer list. Layers are registered as they are built here, so this only renames the
+        last layer when a name is given."""
+        if name and self.layers:
+            self.layers[-1].name = name
 
     def create_tensor(self, dims, data_type=DataType.DT_FLOAT, create_grad=True, name=None):
         L = self._add(OperatorType.OP_INPUT, [], name, dims=tuple(dims), data_type=data_type)

@@ -247,8 +247,8 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                     cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
                                                      bias, batch, sA, sB, sC)
                     if C.dtype == torch.float32 and batch == 1 and alpha == 1.0 and bias is None and \
-                            C.is_contiguous() and (M * N) % 4 == 0 and M * N <= (1 << 24) and K >= 8192:
-                        for S in (2, 4, 8):
+                            C.is_contiguous() and (M * N) % 4 == 0 and M * N <= (1 << 25) and K >= 8192:
+                        for S in ((2, 4, 8) if M * N <= (1 << 24) else (2,)):
                             if K % (S * 8) == 0:
                                 cands[f"lib_sk{S}"] = (lambda S=S: _lib_gemm_splitk(A, B, scratch, M, N, K, a_k, b_k,
                                                                                     lda, ldb, beta, S))

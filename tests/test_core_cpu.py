@@ -147,3 +147,16 @@ def test_reference_rule_file_loads():
     assert len(rules) > 100
     with open(path) as f:
         assert len(json.load(f)["rule"]) == len(rules)
+
+
+def test_reference_op_layer_classes():
+    """get_layer_by_id returns the reference's per-op classes (flexflow_cffi.py Linear, Exp, ...)."""
+    from flexflow_amd import core
+    ff = core.FFModel(core.FFConfig([]))
+    x = ff.create_tensor([4, 8], core.DataType.DT_FLOAT)
+    t = ff.exp(ff.dense(x, 4))
+    ff.add_layer(core.OpType.EXP if hasattr(core, "OpType") else None, "my_exp")
+    l0, l1 = ff.get_layer_by_id(0), ff.get_layer_by_id(1)
+    assert isinstance(l0, core.Linear) and isinstance(l0, core.Layer)
+    assert isinstance(l1, core.Exp) and l1.name == "my_exp"
+    assert l0.get_weight_tensor() is not None and t is l1.get_output_tensor()
