@@ -280,9 +280,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   // LDS: 2 x {Q tile, dO tile, lse, delta} (double-buffered: tile t+1 is fetched into registers
   // while tile t is computed), K block image, dS^T image [KB][QT]
   constexpr int TILE = 2 * QB + 2 * QT * 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + KB * QT * 2];
+  // dQ stage: NTILE (query x d) 32x32 tiles per q-tile; with more waves than tiles, KSPLIT waves
+  // share a tile's key range and the upper parts hand their fp32 partial to part 0 through LDS
+  constexpr int NTILE = 2 * (D / 32);
+  constexpr int KSPLIT = NW > NTILE ? NW / NTILE : 1;
+  constexpr int DQX = KSPLIT > 1 ? NTILE * (KSPLIT - 1) * 32 * 32 * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + KB * QT * 2 + DQX];
   char* k_l = smem + 2 * TILE;
   char* ds_l = k_l + KB * D * 2;
+  float* dqx_l = reinterpret_cast<float*>(ds_l + KB * QT * 2);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
@@ -419,12 +425,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
       }
     }
     lds_barrier();
-    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's 128 keys; wave -> (qt, dt) tiles
-    for (int tile = wave; tile < 2 * (D / 32); tile += NW) {
+    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's KB keys; wave -> (qt, dt) tiles
+    // (and, with KSPLIT > 1, a 1/KSPLIT slice of the keys)
+    for (int tile = wave % NTILE; tile < NTILE; tile += (NW < NTILE ? NW : NTILE)) {
       const int qt = tile / (D / 32), dt = tile % (D / 32);
+      const int part = KSPLIT > 1 ? wave / NTILE : 0;
+      constexpr int KS_PER = KB / 16 / KSPLIT;
       f32x16 acc = f32x16{};
 #pragma unroll
-      for (int ks = 0; ks < KB / 16; ++ks) {
+      for (int ks = part * KS_PER; ks < (part + 1) * KS_PER; ++ks) {
         // A = dS[q][key]: lane q = 32qt + lane&31, keys 16ks + 8h + j -> column reads of dS^T image
         bf16x8 af;
         {
@@ -448,12 +457,36 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
         }
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
       }
-      // acc: col = d (lane&31), row = q
+      if constexpr (KSPLIT > 1) {
+        // parts 1.. park their partial in LDS (lane-major: conflict-free 16-B rows), part 0 adds
+        float* slot = dqx_l + ((part - 1) * NTILE + tile) * 1024;
+        if (part > 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int d = 32 * dt + (lane & 31);
-        if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<float4*>(slot + (r4 * 64 + lane) * 4) =
+                make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
+        }
+        lds_barrier();
+        if (part == 0) {
+#pragma unroll
+          for (int p2 = 1; p2 < KSPLIT; ++p2) {
+            const float* o = dqx_l + ((p2 - 1) * NTILE + tile) * 1024;
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const float4 v = *reinterpret_cast<const float4*>(o + (r4 * 64 + lane) * 4);
+              acc[4 * r4] += v.x; acc[4 * r4 + 1] += v.y; acc[4 * r4 + 2] += v.z; acc[4 * r4 + 3] += v.w;
+            }
+          }
+        }
+      }
+      // acc: col = d (lane&31), row = q
+      if (part == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int d = 32 * dt + (lane & 31);
+          if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
+        }
       }
     }
     if (more) stash(t + 1);  // other buffer: its last readers finished before this tile's first sync
@@ -743,22 +776,27 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
 }
 
 // Backward variant: 0 = attn_bwd_kernel (4 waves x 32 keys, 2 workgroups per CU), 1 = the
-// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64). Settable for A/B
-// runs in one process (attn_set_bwd_variant); default from FF_ATTN_BWD (0 unless set: at
-// B32 H16 S512 D64 variant 0 measured 0.306 ms vs 0.314 ms for variant 1 — the halved dQ slab
-// traffic did not pay for the lost second workgroup per CU; scripts/attn_probe.py).
+// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64), 2 = attn_bwd_kernel
+// with 8 waves x 32 keys (256 keys per workgroup, the dQ stage split over wave halves with an LDS
+// hand-off) at D = 64, variant 0 otherwise. Settable for A/B runs in one process
+// (attn_set_bwd_variant); default from FF_ATTN_BWD, else 2: at B32 H16 S512 D64 (pre + main +
+// dQ finish) variant 0 measured 0.308 ms, variant 1 0.316 ms, variant 2 0.271 ms — half the fp32
+// dQ partial slabs, and Q / dO tiles shared by 8 waves (profiles/attn_bwd_variants_r1.txt).
 static int g_bwd_variant = -1;
 int attn_bwd_variant() {
   if (g_bwd_variant < 0) {
     const char* e = getenv("FF_ATTN_BWD");
-    g_bwd_variant = e ? atoi(e) : 0;
+    g_bwd_variant = e ? atoi(e) : 2;
   }
   return g_bwd_variant;
 }
 void attn_set_bwd_variant(int v) { g_bwd_variant = v; }
 
 // keys per backward workgroup
-static int bwd_keys(int D) { return (attn_bwd_variant() == 1 && D == 64) ? 256 : 128; }
+static int bwd_keys(int D) {
+  const int v = attn_bwd_variant();
+  return ((v == 1 && D == 64) || (v == 2 && D == 64)) ? 256 : 128;
+}
 
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
@@ -773,6 +811,7 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
 
 void attn_bwd(AttnArgs a, hipStream_t st) {
   const int kg = attn_bwd_variant() == 1;
+  const int w8 = attn_bwd_variant() == 2 && a.D == 64;
   const int nkb = (a.Sk + bwd_keys(a.D) - 1) / bwd_keys(a.D);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
@@ -783,6 +822,7 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
 #define FFK_ATTN_BWD(DD)                                                                                 \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, gpre, dim3(256), 0, st, a);                               \
   if (kg) hipLaunchKernelGGL((attn_bwd_kg_kernel<DD, DD == 64 ? 2 : 1>), grid1, dim3(256), 0, st, a, nkb); \
+  else if (w8) hipLaunchKernelGGL((attn_bwd_kernel<DD, DD == 64 ? 8 : 4>), grid, dim3(DD == 64 ? 512 : 256), 0, st, a); \
   else hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                         \
   hipLaunchKernelGGL(attn_dq_finish_kernel<DD>, gfin, dim3(256), 0, st, a, nkb);
   if (a.D == 64) {

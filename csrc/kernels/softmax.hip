@@ -74,7 +74,20 @@ __device__ __forceinline__ void row_visit(const T* __restrict__ xr, int cols, in
   if (lane < head) f(lane, Cvt<T>::to_f(xr[lane]));
   const int nvec = (cols - head) / V;
   const T* body = xr + head;
-  for (int i = lane; i < nvec; i += 64) {
+  int i = lane;
+  // 4 x 16 B per lane in flight before the first use: one row per wave leaves each wave with a
+  // single dependent load stream, which a one-load-per-iteration loop exposes to the full HBM /
+  // Infinity-Cache latency
+  for (; i + 192 < nvec; i += 256) {
+    float v[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load16(body + (int64_t)(i + 64 * u) * V, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < V; ++j) f(head + (i + 64 * u) * V + j, v[u][j]);
+  }
+  for (; i < nvec; i += 64) {
     float v[V];
     load16(body + (int64_t)i * V, v);
 #pragma unroll
@@ -130,7 +143,20 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const T* __restrict__
           dr[lane] = Cvt<T>::from_f((p - (lane == lab ? 1.f : 0.f)) * gscale);
         }
         const int nvec = (cols - head) / V;
-        for (int i = lane; i < nvec; i += 64) {
+        int i = lane;
+        for (; i + 192 < nvec; i += 256) {  // 4 loads in flight per lane (see row_visit)
+          float v[4][V];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) load16(xr + head + (i + 64 * u) * V, v[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c0 = head + (i + 64 * u) * V;
+#pragma unroll
+            for (int j = 0; j < V; ++j) v[u][j] = (__expf(v[u][j] - lse) - (c0 + j == lab ? 1.f : 0.f)) * gscale;
+            store16(dr + c0, v[u]);
+          }
+        }
+        for (; i < nvec; i += 64) {
           float v[V];
           const int c0 = head + i * V;
           load16(xr + c0, v);

@@ -41,18 +41,20 @@ fwd_ms = timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S,
 fl_f = 4.0 * B * H * S * S * D
 print(f"attn fwd B={B} H={H} S={S} D={D}: {fwd_ms:.3f} ms {fl_f / fwd_ms / 1e9:.1f} TFLOPS")
 # backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
-res = {0: [], 1: []}
+default_variant = X.attn_bwd_variant()
+res = {0: [], 1: [], 2: []}
 outs = {}
 for rnd in range(3):
-    for var in (0, 1):
+    for var in (0, 1, 2):
         X.attn_set_bwd_variant(var)
         res[var].append(timed(lambda: Kn.flash_attn_bwd(q, sq, k, sq, v, sq, o, so, do, so, lse, dq, sq, dk, sq,
                                                         dv, sq, B, H, S, S, D, scale, False)))
         outs[var] = dqkv.clone()
 fl_b = 2.5 * fl_f
-for var in (0, 1):
+for var in (0, 1, 2):
     ms = min(res[var])
     print(f"attn bwd variant {var}: {ms:.3f} ms {fl_b / ms / 1e9:.1f} TFLOPS  (rounds {[round(t, 3) for t in res[var]]})")
-d = (outs[0].float() - outs[1].float()).abs().max().item()
-print(f"max |variant0 - variant1| over dq/dk/dv: {d:.4g}")
-X.attn_set_bwd_variant(0)
+for var in (1, 2):
+    d = (outs[0].float() - outs[var].float()).abs().max().item()
+    print(f"max |variant0 - variant{var}| over dq/dk/dv: {d:.4g}")
+X.attn_set_bwd_variant(default_variant)

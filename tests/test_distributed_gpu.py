@@ -97,5 +97,11 @@ def test_bert_two_ranks_match_single(single, search):
         if k == "losses":
             continue
         assert k in par, k
-        d = np.abs(par[k] - v).max()
-        assert d <= 2e-3 + 2e-2 * np.abs(v).max(), f"{search}: {k} max diff {d}"
+        a, b = par[k], v
+        if k.endswith("attn.1") and b.ndim == 3 and b.shape[0] == 3:
+            # the key-projection bias has an exactly zero gradient (adding q.b_k to every score of a
+            # row is softmax-invariant), so its "gradient" is rounding noise whose sign Adam turns
+            # into +-lr steps that differ with any reduction order: compare the q / v biases only
+            a, b = a[[0, 2]], b[[0, 2]]
+        d = np.abs(a - b).max()
+        assert d <= 2e-3 + 2e-2 * np.abs(b).max(), f"{search}: {k} max diff {d}"

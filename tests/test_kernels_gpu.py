@@ -143,13 +143,14 @@ def _attn_ref(q, k, v, scale, causal):
     return torch.einsum("bhqk,bhkd->bhqd", p, v), torch.logsumexp(s, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("S,D,causal", [(512, 64, False), (200, 64, False), (256, 128, False), (384, 64, True),
                                         (640, 64, True), (300, 128, True)])
 def test_flash_attention(ffC, S, D, causal, variant):
     """Both backward structures (variant 0: 4 waves x 32 keys; 1: one wave per SIMD, 64 keys per
     wave at D = 64) against an fp32 PyTorch reference, incl. ragged and causal key blocks."""
     torch.manual_seed(3)
+    prev_variant = ffC.attn_bwd_variant()
     ffC.attn_set_bwd_variant(variant)
     B, H = 2, 3
     q = torch.randn(B, H, S, D, device=DEV).bfloat16()
@@ -172,7 +173,7 @@ def test_flash_attention(ffC, S, D, causal, variant):
     assert _rel(dv, vf.grad) < 3e-2
     assert _rel(dk, kf.grad) < 3e-2
     assert _rel(dq, qf.grad) < 3e-2
-    ffC.attn_set_bwd_variant(0)
+    ffC.attn_set_bwd_variant(prev_variant)
 
 
 def test_flash_attention_strided_qkv(ffC):
