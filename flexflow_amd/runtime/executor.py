@@ -75,6 +75,11 @@ class Executor:
         self.config = cfg
         self.hooks = []  # per-op context managers: OpProfiler, NonFiniteGuard (runtime/profiler.py, health.py)
         self.rank, self.world = cfg.rank, cfg.world_size
+        if torch.cuda.is_available() and os.environ.get("FF_CONV_BENCHMARK", "0") == "1":
+            # opt-in MIOpen find mode (time every solver once per convolution shape). Off by
+            # default: its exhaustive search ran > 3 min for ResNet-50's shapes on a fresh box,
+            # while immediate mode measured the same AlexNet step time (7.0 ms at batch 256)
+            torch.backends.cudnn.benchmark = True
         self.device = _device_for(cfg)
         self.training = training
         self.cdt = DataType.DT_BF16 if cfg.compute_dtype == DataType.DT_BF16 else DataType.DT_FLOAT

@@ -2,7 +2,7 @@
 `begin_trace/end_trace` around forward/backward, examples/cpp/*).
 
 A BERT-Large step is ~1.5k kernel launches; eager Python dispatch would dominate the GPU time.
-After two eager warm-up steps (so every buffer of the torch caching allocator exists), the
+After three eager warm-up steps (so every buffer of the torch caching allocator exists), the
 zero-grad + forward + backward of one step is captured once into a hipGraph and replayed; the
 optimizer update (one fused kernel per arena, with host-side bias-corrected scalars) and the
 bucket all-reduces that belong to it run after the replay. Multi-rank steps with in-step
@@ -53,10 +53,13 @@ class StepGraph:
             ex.backward()
             ex.update(m.optimizer)
             return
-        if self.warm < 2:
+        if self.warm < 3:
             self.warm += 1
             auto = m.config.hip_graphs == "auto"
-            if auto and self.warm == 2:  # the first step pays autotuning; time the second
+            # the first step pays autotuning, the second can still pay MIOpen's first-use kernel
+            # compiles: time steps 2 and 3 and decide on the faster (AlexNet's step 2 landed on
+            # either side of the threshold from box to box: 7.0 vs 13.4 ms steady state)
+            if auto and self.warm >= 2:
                 torch.cuda.synchronize()
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
@@ -64,12 +67,12 @@ class StepGraph:
             ex.forward()
             ex.backward()
             ex.update(m.optimizer)
-            if auto and self.warm == 2:
+            if auto and self.warm >= 2:
                 en.record()
                 en.synchronize()
                 ms = st.elapsed_time(en)
                 self.eager_ms.append(ms)
-                self.decision = ms < float(m.config.graph_min_step_ms)
+                self.decision = min(self.eager_ms) < float(m.config.graph_min_step_ms)
             return
         if self.graph is None:
             torch.cuda.synchronize()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run the strategy search for a model in ONE process planning for N devices and export the chosen
 strategy (+ search report) as a strategy file, e.g. to replay a GPU-measured search on CPU ranks.
-usage: export_search.py MODEL N OUT.json [search] [batch]   (MODEL: bert-tiny-test | zoo name)"""
+usage: export_search.py MODEL N OUT.json [search] [batch] [extra FFConfig flags...]
+(MODEL: bert-tiny-test | zoo name)"""
 import json
 import os
 import sys
@@ -14,7 +15,8 @@ from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, Metric
 name, n, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 algo = sys.argv[4] if len(sys.argv) > 4 else "unity"
 batch = int(sys.argv[5]) if len(sys.argv) > 5 else 8
-cfg = FFConfig(["--dtype", "bf16", "--search", algo, "--search-num-workers", str(n), "--export-strategy", out])
+cfg = FFConfig(["--dtype", "bf16", "--search", algo, "--search-num-workers", str(n), "--export-strategy", out]
+               + sys.argv[6:])
 cfg.batch_size = batch
 ff = FFModel(cfg)
 if name == "bert-tiny-test":
