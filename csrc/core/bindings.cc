@@ -91,7 +91,32 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("hbm_gbps", &MachineModel::hbm_gbps)
       .def_readwrite("mem_capacity", &MachineModel::mem_capacity)
       .def("num_devices", &MachineModel::num_devices)
-      .def("ring_busbw", &MachineModel::ring_busbw);
+      .def("ring_busbw", &MachineModel::ring_busbw)
+      .def("p2p_gbps", &MachineModel::p2p_gbps)
+      .def("set_topology", [](MachineModel& mm, const NetworkTopology& t) {
+        mm.topo = std::make_shared<const NetworkTopology>(t);
+      })
+      .def("clear_topology", [](MachineModel& mm) { mm.topo.reset(); })
+      .def_property_readonly("has_topology", [](const MachineModel& mm) { return (bool)mm.topo; });
+
+  py::class_<NetworkTopology>(m, "NetworkTopology")
+      .def(py::init<>())
+      .def_readwrite("num_gpus", &NetworkTopology::num_gpus)
+      .def_readonly("num_nodes", &NetworkTopology::num_nodes)
+      .def("add_node", &NetworkTopology::add_node)
+      .def("add_link", &NetworkTopology::add_link)
+      .def("build_routes", &NetworkTopology::build_routes)
+      .def("route", &NetworkTopology::route)
+      .def("hops", &NetworkTopology::hops)
+      .def("path_gbps", &NetworkTopology::path_gbps)
+      .def("transfers_ms", &NetworkTopology::transfers_ms)
+      .def("allreduce_ms", &NetworkTopology::allreduce_ms)
+      .def("allgather_ms", &NetworkTopology::allgather_ms)
+      .def("ring_busbw", &NetworkTopology::ring_busbw)
+      .def_property_readonly("num_links", [](const NetworkTopology& t) { return t.links.size(); });
+  m.def("make_mi355x_cluster", &make_mi355x_cluster, py::arg("nodes"), py::arg("gpus_per_node"),
+        py::arg("xgmi_gbps") = 64.0, py::arg("nic_gbps") = 50.0, py::arg("kind") = "fat_tree",
+        py::arg("oversub") = 1.0);
 
   py::class_<Problem>(m, "Problem")
       .def(py::init<>())

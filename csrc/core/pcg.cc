@@ -32,6 +32,7 @@ std::vector<int> Layout::replica_group(const std::vector<int>& blk) const {
 double MachineModel::ring_busbw(const std::vector<int>& ranks) const {
   const int r = (int)ranks.size();
   if (r <= 1) return 1e30;
+  if (topo) return coll_eff * topo->ring_busbw(ranks);
   bool one_node = true;
   for (int x : ranks)
     if (!same_node(x, ranks[0])) one_node = false;
@@ -215,6 +216,15 @@ XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const 
         if (src != dq) link[{src, dq}] += (double)n * eb;
       }
     }
+  }
+  if (mm.topo) {  // routed, per-link contention
+    std::vector<std::tuple<int, int, double>> xs;
+    for (auto& kv : link) {
+      xs.emplace_back(kv.first.first, kv.first.second, kv.second);
+      x.bytes += kv.second;
+    }
+    x.ms = link.empty() ? 0.0 : mm.topo->transfers_ms(xs) / mm.coll_eff + lat;
+    return x;
   }
   std::map<int, double> egress, ingress;
   double worst_link = 0;

@@ -12,11 +12,14 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <memory>
 #include <random>
 #include <string>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
+
+#include "network.h"
 
 namespace ffcore {
 
@@ -85,11 +88,16 @@ struct MachineModel {
   double latency_us = 8.0;         // per collective / P2P batch
   double hbm_gbps = 5800.0;        // achievable HBM bandwidth (local copies)
   double mem_capacity = 288e9;     // HBM3E per GPU
+  // machine_model_version 1: explicit topology (routes, per-link contention); null = analytic
+  std::shared_ptr<const NetworkTopology> topo;
   int num_devices() const { return num_nodes * gpus_per_node; }
   bool same_node(int a, int b) const { return a / gpus_per_node == b / gpus_per_node; }
   // bus bandwidth (GB/s) of a ring collective over `ranks`
   double ring_busbw(const std::vector<int>& ranks) const;
-  double p2p_gbps(int a, int b) const { return same_node(a, b) ? link_gbps : inter_node_gbps; }
+  double p2p_gbps(int a, int b) const {
+    if (topo) return topo->path_gbps(a, b);
+    return same_node(a, b) ? link_gbps : inter_node_gbps;
+  }
 };
 
 // Collective classification of a layout conversion (mirror of flexflow_amd.parallel.comm.Transfer).

@@ -50,14 +50,37 @@ def machine_model(cfg):
     mm.num_nodes = max(1, n // gpn)
     if cfg.device_mem and cfg.device_mem > 0:  # -ll:fsize, MiB of device memory per GPU
         mm.mem_capacity = float(cfg.device_mem) * (1 << 20)
+    d = {}
     if cfg.machine_model_file and os.path.exists(cfg.machine_model_file):
         import json
         with open(cfg.machine_model_file) as f:
             d = json.load(f)
         for k, v in d.items():
-            if hasattr(mm, k):
+            if hasattr(mm, k) and not callable(getattr(mm, k)) and k != "has_topology":
                 setattr(mm, k, v)
+    if cfg.machine_model_version == 1 or "links" in d or "topology" in d:
+        mm.set_topology(network_topology(mm, d))
     return mm
+
+
+def network_topology(mm, d: dict):
+    """machine_model_version 1 (reference NetworkedMachineModel, src/runtime/network.cc): an explicit
+    link graph with shortest-path routing and per-link contention. From the machine-model JSON either
+    "links": [[a, b, GB/s], ...] over GPUs 0..N-1 plus "switches": K extra vertices N..N+K-1, or a
+    generated MI355X cluster, "topology": "fat_tree" | "big_switch" (default fat_tree) with
+    "oversub" (leaf-to-spine oversubscription), using link_gbps / inter_node_gbps of the model."""
+    core = _core()
+    if "links" in d:
+        t = core.NetworkTopology()
+        t.num_gpus = mm.num_devices()
+        for _ in range(mm.num_devices() + int(d.get("switches", 0))):
+            t.add_node()
+        for a, b, g in d["links"]:
+            t.add_link(int(a), int(b), float(g))
+        t.build_routes()
+        return t
+    return core.make_mi355x_cluster(mm.num_nodes, mm.gpus_per_node, mm.link_gbps, mm.inter_node_gbps,
+                                    d.get("topology", "fat_tree"), float(d.get("oversub", 1.0)))
 
 
 def allowed_kinds(cfg):
