@@ -231,10 +231,13 @@ class FFModel:
         return L.outputs[0]
 
     def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
-               pool_type=PoolType.POOL_MAX, activation=ActiMode.AC_MODE_NONE, name=None):
+               pool_type=PoolType.POOL_MAX, activation=ActiMode.AC_MODE_NONE, name=None, count_include_pad=True):
+        """count_include_pad (average pooling only): divide by the full window including padding
+        (the reference's cuDNN mode, default) or by the valid elements (ONNX's default)."""
+        kw = {} if count_include_pad else {"count_include_pad": False}
         return self._add(OperatorType.OP_POOL2D, [input], name, kernel_h=kernel_h, kernel_w=kernel_w,
                          stride_h=stride_h, stride_w=stride_w, padding_h=padding_h, padding_w=padding_w,
-                         pool_type=pool_type, activation=activation).outputs[0]
+                         pool_type=pool_type, activation=activation, **kw).outputs[0]
 
     def batch_norm(self, input, relu=True, name=None):
         return self._add(OperatorType.OP_BATCHNORM, [input], name, relu=relu).outputs[0]

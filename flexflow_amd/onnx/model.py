@@ -30,7 +30,7 @@ def _attr_value(a):
             v = getattr(a, f, None)
             if v:
                 return list(v)
-        for f in ("i", "f", "s"):
+        for f in ("i", "f", "s", "t"):
             v = getattr(a, f, None)
             if v is not None:
                 return v
@@ -53,22 +53,29 @@ def _init_array(t):
 
 class ONNXModel:
     def __init__(self, filename_or_model):
-        if isinstance(filename_or_model, str):
+        if isinstance(filename_or_model, (str, bytes, bytearray)):
             try:
                 import onnx  # type: ignore
-            except ImportError as e:
-                raise ImportError("loading an .onnx file needs the `onnx` package (not installed here); "
-                                  "pass an onnx.ModelProto-shaped object instead") from e
-            filename_or_model = onnx.load(filename_or_model)
+                filename_or_model = onnx.load(filename_or_model) if isinstance(filename_or_model, str) else \
+                    onnx.load_from_string(bytes(filename_or_model))
+            except ImportError:  # no onnx package: our protobuf reader (flexflow_amd/onnx/proto.py)
+                from .proto import load_model
+                filename_or_model = load_model(filename_or_model)
         self.model = filename_or_model
         g = self.model.graph
         self.inits = {t.name: t for t in getattr(g, "initializer", [])}
+        self.opset = max([int(getattr(o, "version", 0) or 0) for o in getattr(self.model, "opset_import", [])
+                          if getattr(o, "domain", "") in ("", "ai.onnx")] or [13])
         self.symbol_table: Dict[str, object] = {}
         self._layer_weights = {}  # ff layer -> [initializer names]
 
     def _dims(self, name):
-        t = self.inits[name]
-        return tuple(int(d) for d in t.dims)
+        if name in self.inits:
+            return tuple(int(d) for d in self.inits[name].dims)
+        for vi in getattr(self.model.graph, "input", []):  # weight passed as a graph input
+            if getattr(vi, "name", None) == name and getattr(vi, "shape", None):
+                return tuple(int(d) for d in vi.shape)
+        raise KeyError(f"no initializer or shaped graph input named {name}")
 
     # ------------------------------------------------------------------ handlers
     def handleAdd(self, ff, n):
@@ -97,7 +104,29 @@ class ONNXModel:
         k = list(at["kernel_shape"])
         s = list(at.get("strides", [1, 1]))
         p = list(at.get("pads", [0, 0, 0, 0]))
-        return ff.pool2d(self.symbol_table[n.input[0]], k[0], k[1], s[0], s[1], p[0], p[1], pt, name=n.name or None)
+        x = self.symbol_table[n.input[0]]
+        auto = at.get("auto_pad", b"NOTSET")
+        auto = auto.decode() if isinstance(auto, bytes) else str(auto)
+        if auto in ("SAME_UPPER", "SAME_LOWER"):
+            p = []
+            for d, (kk, ss) in enumerate(zip(k, s)):
+                size = x.dims[2 + d]
+                tot = max((-(-size // ss) - 1) * ss + kk - size, 0)
+                lo = tot // 2 if auto == "SAME_UPPER" else tot - tot // 2
+                p.append((lo, tot - lo))
+            p = [p[0][0], p[1][0], p[0][1], p[1][1]]
+        elif auto == "VALID":
+            p = [0, 0, 0, 0]
+        if int(at.get("ceil_mode", 0)):
+            raise NotImplementedError(f"{n.op_type}: ceil_mode=1 is not supported (floor output sizes only)")
+        if any(int(d) != 1 for d in at.get("dilations", [1, 1])):
+            raise NotImplementedError(f"{n.op_type}: dilations != 1 are not supported")
+        if p[0] != p[2] or p[1] != p[3]:
+            raise NotImplementedError(f"{n.op_type}: asymmetric padding {p} is not supported")
+        kw = {}
+        if pt == PoolType.POOL_AVG:  # ONNX default excludes the padding from the divisor
+            kw["count_include_pad"] = bool(int(at.get("count_include_pad", 0)))
+        return ff.pool2d(x, k[0], k[1], s[0], s[1], p[0], p[1], pt, name=n.name or None, **kw)
 
     def handleMaxPool(self, ff, n):
         return self._pool(ff, n, PoolType.POOL_MAX)
@@ -166,8 +195,24 @@ class ONNXModel:
 
     def handleSoftmax(self, ff, n):
         x = self.symbol_table[n.input[0]]
-        ax = int(_attrs(n).get("axis", -1))
-        return ff.softmax(x, ax if ax >= 0 else len(x.dims) + ax, name=n.name or None)
+        at = _attrs(n)
+        ax = int(at.get("axis", -1 if self.opset >= 13 else 1))
+        ax = ax if ax >= 0 else len(x.dims) + ax
+        if self.opset < 13 and ax != len(x.dims) - 1:
+            # opset < 13: softmax over the flattened trailing dims [ax:] (one 2-D row per prefix)
+            lead = [int(d) for d in x.dims[:ax]]
+            flat = ff.reshape(x, lead + [int(np.prod(x.dims[ax:]))])
+            return ff.reshape(ff.softmax(flat, len(lead), name=n.name or None), list(x.dims))
+        return ff.softmax(x, ax, name=n.name or None)
+
+    def handleSqrt(self, ff, n):
+        return ff.pow(self.symbol_table[n.input[0]], 0.5, name=n.name or None)
+
+    def handleReciprocal(self, ff, n):
+        return ff.pow(self.symbol_table[n.input[0]], -1.0, name=n.name or None)
+
+    def handleExp(self, ff, n):
+        return ff.exp(self.symbol_table[n.input[0]], name=n.name or None)
 
     def handleReshape(self, ff, n):
         x = self.symbol_table[n.input[0]]

@@ -1,0 +1,238 @@
+"""Minimal reader for ONNX ModelProto files (protobuf wire format), so `ONNXModel("model.onnx")`
+works without the `onnx` package (not installed in this image).
+
+Only the fields the converter uses are decoded (onnx/onnx.proto numbering):
+  ModelProto     1 ir_version, 2 producer_name, 7 graph, 8 opset_import
+  GraphProto     1 node, 2 name, 5 initializer, 11 input, 12 output
+  NodeProto      1 input, 2 output, 3 name, 4 op_type, 5 attribute, 7 domain
+  AttributeProto 1 name, 2 f, 3 i, 4 s, 5 t, 7 floats, 8 ints, 9 strings, 20 type
+  TensorProto    1 dims, 2 data_type, 4 float_data, 5 int32_data, 7 int64_data, 8 name, 9 raw_data,
+                 10 double_data
+  ValueInfoProto 1 name, 2 type -> TypeProto 1 tensor_type -> 1 elem_type, 2 shape -> 1 dim ->
+                 1 dim_value | 2 dim_param
+The result is plain Python objects with the same attribute names as the onnx classes
+(`model.graph.node[i].op_type`, `tensor.dims`, ...); a TensorProto also carries `.array` (numpy).
+Nothing from the file is executed: it is parsed as data only.
+"""
+from __future__ import annotations
+
+import struct
+from types import SimpleNamespace
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+# TensorProto.DataType -> numpy
+ONNX_DTYPES = {1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
+               9: np.bool_, 10: np.float16, 11: np.float64, 12: np.uint32, 13: np.uint64}
+
+
+def _varint(b: bytes, i: int) -> Tuple[int, int]:
+    r = s = 0
+    while True:
+        c = b[i]
+        i += 1
+        r |= (c & 0x7F) << s
+        if c < 0x80:
+            return r, i
+        s += 7
+
+
+def _fields(b: bytes) -> List[Tuple[int, int, object]]:
+    """(field number, wire type, value) for every field of one message."""
+    out, i, n = [], 0, len(b)
+    while i < n:
+        key, i = _varint(b, i)
+        f, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(b, i)
+        elif wt == 1:
+            v = b[i:i + 8]
+            i += 8
+        elif wt == 2:
+            ln, i = _varint(b, i)
+            v = b[i:i + ln]
+            i += ln
+        elif wt == 5:
+            v = b[i:i + 4]
+            i += 4
+        else:
+            raise ValueError(f"unsupported protobuf wire type {wt}")
+        out.append((f, wt, v))
+    return out
+
+
+def _signed(v: int) -> int:
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _packed_varints(v, wt) -> List[int]:
+    if wt == 0:
+        return [_signed(v)]
+    vals, i = [], 0
+    while i < len(v):
+        x, i = _varint(v, i)
+        vals.append(_signed(x))
+    return vals
+
+
+def _packed_f32(v, wt) -> List[float]:
+    if wt == 5:
+        return [struct.unpack("<f", v)[0]]
+    return list(struct.unpack(f"<{len(v) // 4}f", v))
+
+
+def parse_tensor(b: bytes):
+    t = SimpleNamespace(dims=[], data_type=1, name="", raw_data=b"", float_data=[], int32_data=[], int64_data=[],
+                        double_data=[])
+    for f, wt, v in _fields(b):
+        if f == 1:
+            t.dims += _packed_varints(v, wt)
+        elif f == 2:
+            t.data_type = v
+        elif f == 4:
+            t.float_data += _packed_f32(v, wt)
+        elif f == 5:
+            t.int32_data += _packed_varints(v, wt)
+        elif f == 7:
+            t.int64_data += _packed_varints(v, wt)
+        elif f == 8:
+            t.name = v.decode()
+        elif f == 9:
+            t.raw_data = bytes(v)
+        elif f == 10:
+            t.double_data += list(struct.unpack(f"<{len(v) // 8}d", v)) if wt == 2 else [struct.unpack("<d", v)[0]]
+    dt = ONNX_DTYPES.get(t.data_type, np.float32)
+    shape = tuple(int(d) for d in t.dims)
+    if t.raw_data:
+        arr = np.frombuffer(t.raw_data, dtype=dt).copy()
+    elif t.float_data:
+        arr = np.asarray(t.float_data, dtype=dt)
+    elif t.int64_data:
+        arr = np.asarray(t.int64_data, dtype=dt)
+    elif t.int32_data:
+        arr = np.asarray(t.int32_data, dtype=dt)
+    elif t.double_data:
+        arr = np.asarray(t.double_data, dtype=dt)
+    else:
+        arr = np.zeros(shape, dtype=dt)
+    t.array = arr.reshape(shape)
+    return t
+
+
+def _parse_attribute(b: bytes):
+    a = SimpleNamespace(name="", f=None, i=None, s=None, t=None, floats=[], ints=[], strings=[], type=0)
+    for f, wt, v in _fields(b):
+        if f == 1:
+            a.name = v.decode()
+        elif f == 2:
+            a.f = struct.unpack("<f", v)[0]
+        elif f == 3:
+            a.i = _signed(v)
+        elif f == 4:
+            a.s = bytes(v)
+        elif f == 5:
+            a.t = parse_tensor(v)
+        elif f == 7:
+            a.floats += _packed_f32(v, wt)
+        elif f == 8:
+            a.ints += _packed_varints(v, wt)
+        elif f == 9:
+            a.strings.append(bytes(v))
+        elif f == 20:
+            a.type = v
+    return a
+
+
+def _parse_node(b: bytes):
+    n = SimpleNamespace(input=[], output=[], name="", op_type="", attribute=[], domain="")
+    for f, wt, v in _fields(b):
+        if f == 1:
+            n.input.append(v.decode())
+        elif f == 2:
+            n.output.append(v.decode())
+        elif f == 3:
+            n.name = v.decode()
+        elif f == 4:
+            n.op_type = v.decode()
+        elif f == 5:
+            n.attribute.append(_parse_attribute(v))
+        elif f == 7:
+            n.domain = v.decode()
+    return n
+
+
+def _parse_value_info(b: bytes):
+    vi = SimpleNamespace(name="", elem_type=0, shape=[])
+    for f, wt, v in _fields(b):
+        if f == 1:
+            vi.name = v.decode()
+        elif f == 2:  # TypeProto
+            for f2, _, v2 in _fields(v):
+                if f2 != 1:  # tensor_type
+                    continue
+                for f3, _, v3 in _fields(v2):
+                    if f3 == 1:
+                        vi.elem_type = v3
+                    elif f3 == 2:  # TensorShapeProto
+                        for f4, _, v4 in _fields(v3):
+                            if f4 != 1:
+                                continue
+                            d = None
+                            for f5, _, v5 in _fields(v4):
+                                if f5 == 1:
+                                    d = int(v5)
+                                elif f5 == 2:
+                                    d = v5.decode()
+                            vi.shape.append(d)
+    return vi
+
+
+def _parse_graph(b: bytes):
+    g = SimpleNamespace(node=[], name="", initializer=[], input=[], output=[])
+    for f, wt, v in _fields(b):
+        if f == 1:
+            g.node.append(_parse_node(v))
+        elif f == 2:
+            g.name = v.decode()
+        elif f == 5:
+            g.initializer.append(parse_tensor(v))
+        elif f == 11:
+            g.input.append(_parse_value_info(v))
+        elif f == 12:
+            g.output.append(_parse_value_info(v))
+    return g
+
+
+def load_model(path_or_bytes) -> SimpleNamespace:
+    """Parse an .onnx file (or its bytes) into a ModelProto-shaped object."""
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        b = bytes(path_or_bytes)
+    else:
+        with open(path_or_bytes, "rb") as f:
+            b = f.read()
+    m = SimpleNamespace(ir_version=0, producer_name="", graph=None, opset_import=[])
+    for f, wt, v in _fields(b):
+        if f == 1:
+            m.ir_version = v
+        elif f == 2:
+            m.producer_name = v.decode()
+        elif f == 7:
+            m.graph = _parse_graph(v)
+        elif f == 8:
+            ver = dom = None
+            for f2, _, v2 in _fields(v):
+                if f2 == 1:
+                    dom = v2.decode()
+                elif f2 == 2:
+                    ver = v2
+            m.opset_import.append(SimpleNamespace(domain=dom or "", version=ver))
+    if m.graph is None:
+        raise ValueError("not an ONNX ModelProto (no graph)")
+    return m
+
+
+def input_shapes(model) -> Dict[str, list]:
+    """Graph inputs that are not initializers -> declared shape."""
+    inits = {t.name for t in model.graph.initializer}
+    return {vi.name: vi.shape for vi in model.graph.input if vi.name not in inits}

@@ -200,7 +200,8 @@ class Pool2D(_Spatial):
                 xp = F.pad(xr, (pad[1], pad[1], pad[0], pad[0]), value=float("-inf")) if any(pad) else xr
                 y = F.max_pool2d(xp, (kh, kw), (sh, sw))
             else:
-                y = F.avg_pool2d(xr, (kh, kw), (sh, sw), pad, count_include_pad=True)
+                y = F.avg_pool2d(xr, (kh, kw), (sh, sw), pad,
+                                 count_include_pad=self.attrs.get("count_include_pad", True))
             y = K.act_ref(y, act)
         if ctx.training:
             ctx.saved.update(xr=xr, y=y, x_shape=x.shape)
