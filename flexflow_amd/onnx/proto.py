@@ -18,68 +18,18 @@ from __future__ import annotations
 
 import struct
 from types import SimpleNamespace
-from typing import Dict, List, Tuple
+from typing import Dict
 
 import numpy as np
+
+from ..utils.protowire import fields as _fields
+from ..utils.protowire import packed_f32 as _packed_f32
+from ..utils.protowire import packed_varints as _packed_varints
+from ..utils.protowire import signed as _signed
 
 # TensorProto.DataType -> numpy
 ONNX_DTYPES = {1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
                9: np.bool_, 10: np.float16, 11: np.float64, 12: np.uint32, 13: np.uint64}
-
-
-def _varint(b: bytes, i: int) -> Tuple[int, int]:
-    r = s = 0
-    while True:
-        c = b[i]
-        i += 1
-        r |= (c & 0x7F) << s
-        if c < 0x80:
-            return r, i
-        s += 7
-
-
-def _fields(b: bytes) -> List[Tuple[int, int, object]]:
-    """(field number, wire type, value) for every field of one message."""
-    out, i, n = [], 0, len(b)
-    while i < n:
-        key, i = _varint(b, i)
-        f, wt = key >> 3, key & 7
-        if wt == 0:
-            v, i = _varint(b, i)
-        elif wt == 1:
-            v = b[i:i + 8]
-            i += 8
-        elif wt == 2:
-            ln, i = _varint(b, i)
-            v = b[i:i + ln]
-            i += ln
-        elif wt == 5:
-            v = b[i:i + 4]
-            i += 4
-        else:
-            raise ValueError(f"unsupported protobuf wire type {wt}")
-        out.append((f, wt, v))
-    return out
-
-
-def _signed(v: int) -> int:
-    return v - (1 << 64) if v >= 1 << 63 else v
-
-
-def _packed_varints(v, wt) -> List[int]:
-    if wt == 0:
-        return [_signed(v)]
-    vals, i = [], 0
-    while i < len(v):
-        x, i = _varint(v, i)
-        vals.append(_signed(x))
-    return vals
-
-
-def _packed_f32(v, wt) -> List[float]:
-    if wt == 5:
-        return [struct.unpack("<f", v)[0]]
-    return list(struct.unpack(f"<{len(v) // 4}f", v))
 
 
 def parse_tensor(b: bytes):

@@ -18,7 +18,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from .strategy import (OpConfig, data_parallel_strategy, load_strategy, valid_config)
+from .strategy import (OpConfig, data_parallel_strategy, load_strategy, load_strategy_pb, valid_config)
 
 
 def _broadcast_strategy(model, strategy):
@@ -35,7 +35,10 @@ def choose_strategy(model):
     n = cfg.num_devices
     report = {"algo": None}
     if cfg.import_strategy_file:
-        strat, nd = load_strategy(cfg.import_strategy_file)
+        if cfg.import_strategy_file.endswith(".pb"):  # the reference's protobuf strategy files
+            strat = load_strategy_pb(cfg.import_strategy_file, layers, n)
+        else:
+            strat, nd = load_strategy(cfg.import_strategy_file)
         missing = [L.name for L in layers if L.name not in strat]
         for L in layers:
             if L.name in strat and not valid_config(L, strat[L.name]):

@@ -221,3 +221,56 @@ def load_strategy(path: str) -> Tuple[Dict[str, OpConfig], int]:
     with open(path) as f:
         doc = json.load(f)
     return {k: OpConfig.from_json(v) for k, v in doc["ops"].items()}, int(doc.get("num_devices", 1))
+
+
+def load_strategy_pb(path: str, layers, num_devices: int) -> Dict[str, OpConfig]:
+    """The reference's legacy protobuf strategy files (src/runtime/strategy.proto: Strategy { repeated
+    Op ops = 1 }, Op { name = 1; device_type = 2; repeated dims = 3; repeated device_ids = 4 }, e.g.
+    examples/cpp/DLRM/strategies/*.pb), read as data with our wire decoder.
+
+    `dims` are per-output-dim parallel degrees in Legion order (innermost first); `device_ids` the
+    devices of the parts. An entry applies to the layer of that exact name, else to the k-th layer of
+    that type when named "<type><k>" (the reference named its ops "embedding0", "embedding1", ...),
+    else to every layer of that type when named by the bare type ("linear", "concat"). Layers with
+    no entry, or whose entry is not a valid config for them here, are left out (data parallel)."""
+    from ..utils.protowire import fields, packed_varints
+    with open(path, "rb") as f:
+        data = f.read()
+    table = {}
+    for fno, _, v in fields(data):
+        if fno != 1:
+            continue
+        name, dims, devs = "", [], []
+        for f2, wt2, v2 in fields(v):
+            if f2 == 1:
+                name = v2.decode()
+            elif f2 == 3:
+                dims += packed_varints(v2, wt2)
+            elif f2 == 4:
+                devs += packed_varints(v2, wt2)
+        table[name] = (dims, devs)
+    out: Dict[str, OpConfig] = {}
+    per_type: Dict[str, int] = {}
+    for L in layers:
+        base = L.op_type.name[3:].lower()
+        k = per_type.get(base, 0)
+        per_type[base] = k + 1
+        ent = table.get(L.name) or table.get(f"{base}{k}") or table.get(base)
+        if ent is None:
+            continue
+        dims, devs = ent
+        n_axes = len(data_parallel_config(L, num_devices).degrees)
+        n_out = len(L.outputs[0].dims) if L.outputs else n_axes
+        outer_first = list(reversed(dims))
+        deg = [1] * n_axes
+        if outer_first:
+            deg[0] = int(outer_first[0])  # sample dim
+            inner = outer_first[1:]
+            for j, d in enumerate(reversed(inner)):  # innermost dims align with our last output dims
+                if n_out - 1 - j >= 1:
+                    deg[n_out - 1 - j] = int(d)
+        cfg = OpConfig(tuple(deg), tuple(int(d) for d in devs[:math.prod(deg)]))
+        if len(cfg.devices) == cfg.num_parts and all(0 <= d < num_devices for d in cfg.devices) and \
+                valid_config(L, cfg):
+            out[L.name] = cfg
+    return out
