@@ -390,7 +390,24 @@ __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __
                                     bf16_t* zout, bf16_t* y, int64_t rows, int cols, int act) {
   const int64_t nv = rows * (int64_t)cols / 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // two 16-B vectors per lane in flight (the 2048-block grid alone leaves ~32 KB in flight per CU,
+  // under what hides an HBM round trip); only the plain activation pass takes this path
+  if (!bias) {
+    for (; v + stride < nv; v += 2 * stride) {
+      float x0[8], x1[8];
+      load16(z + v * 8, x0);
+      load16(z + (v + stride) * 8, x1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        x0[j] = act_fwd(act, x0[j]);
+        x1[j] = act_fwd(act, x1[j]);
+      }
+      store16(y + v * 8, x0);
+      store16(y + (v + stride) * 8, x1);
+    }
+  }
+  for (; v < nv; v += stride) {
     const int64_t e = v * 8;
     const int c = (int)(e % cols);
     float x[8];
