@@ -377,15 +377,23 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
       }
-      // P = exp2(S*sl2 - lse2), dS = P * (dP - delta)
+      // P = exp2(S*sl2 - lse2), dS = P * (dP - delta); accumulator rows 4g..4g+3 are 4 consecutive
+      // queries, so their lse / delta come in as one 16-B LDS read each (not 16 scalar reads)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int q = qbase + ql;
-        float p = exp2f(sacc[r] * sl2 - lse_l[ql]);
-        if (key >= a.Sk || (a.causal && key > q)) p = 0.f;
-        sacc[r] = p;
-        pacc[r] = p * (pacc[r] - dl_l[ql]);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int q0l = 32 * qt + 8 * g4 + 4 * h;
+        const float4 L4 = *reinterpret_cast<const float4*>(lse_l + q0l);
+        const float4 D4 = *reinterpret_cast<const float4*>(dl_l + q0l);
+        const float lv[4] = {L4.x, L4.y, L4.z, L4.w}, dv4[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g4 + j;
+          const int q = qbase + q0l + j;
+          float p = exp2f(sacc[r] * sl2 - lv[j]);
+          if (key >= a.Sk || (a.causal && key > q)) p = 0.f;
+          sacc[r] = p;
+          pacc[r] = p * (pacc[r] - dv4[j]);
+        }
       }
       const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
       const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
