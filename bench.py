@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
     ap.add_argument("--no-hip-graphs", action="store_true")
+    ap.add_argument("--zero", action="store_true",
+                    help="ZeRO-1 sharded optimizer on data-parallel weights (reduce-scatter + all-gather)")
     ap.add_argument("--compare-dp", action="store_true", help="also time pure data parallel (speedup vs DP)")
     ap.add_argument("--verify-steps", type=int, default=4,
                     help="N>1: time the searched strategy and data parallel for this many steps each and keep "
@@ -63,6 +65,8 @@ def build(args, search):
     flags = ["--dtype", args.dtype, "--search", search]
     if args.no_hip_graphs:
         flags.append("--no-hip-graphs")
+    if args.zero:
+        flags.append("--zero")
     cfg = FFConfig(flags)
     bert = args.model.startswith("bert")
     bpg = args.batch_per_gpu or (32 if bert else 64)

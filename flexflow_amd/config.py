@@ -70,6 +70,7 @@ class FFConfig:
         self.search_algo = "unity"  # unity | mcmc | dp (data-parallel only) | none
         self.mcmc_iterations = 2000
         self.grad_bucket_mb = 64.0
+        self.zero_optimizer = False   # --zero: ZeRO-1 sharded optimizer state / update on DP arenas
         self.seed = 1234
         self.trace_dir = ""
         self.check_nan_every = 0      # --check-nan N: loss finite-check every N steps (0 = off)
@@ -195,6 +196,8 @@ class FFConfig:
                 self.search_algo = nxt()
             elif a == "--mcmc-iterations":
                 self.mcmc_iterations = int(nxt())
+            elif a == "--zero":
+                self.zero_optimizer = True
             elif a == "--grad-bucket-mb":
                 self.grad_bucket_mb = float(nxt())
             elif a == "--seed":

@@ -32,6 +32,10 @@ class Optimizer:
     def step(self, arena):
         raise NotImplementedError
 
+    def step_range(self, arena, lo, hi):
+        """Update elements [lo, hi) of the arena only (sharded optimizer: this rank's chunk)."""
+        raise NotImplementedError
+
 
 class SGDOptimizer(Optimizer):
     def __init__(self, ffmodel=None, lr=0.01, momentum=0.0, nesterov=False, weight_decay=0.0):
@@ -47,6 +51,12 @@ class SGDOptimizer(Optimizer):
     def step(self, arena):
         K.sgd_update(arena.master, arena.grad, self.state.get(id(arena)), arena.lowp, self.lr, self.momentum,
                      self.nesterov, self.weight_decay)
+
+    def step_range(self, arena, lo, hi):
+        mom = self.state.get(id(arena))
+        K.sgd_update(arena.master[lo:hi], arena.grad[lo:hi], mom[lo:hi] if mom is not None else None,
+                     arena.lowp[lo:hi] if arena.lowp is not None else None, self.lr, self.momentum, self.nesterov,
+                     self.weight_decay)
 
 
 class AdamOptimizer(Optimizer):
@@ -76,4 +86,10 @@ class AdamOptimizer(Optimizer):
     def step(self, arena):
         m, v = self.state[id(arena)]
         K.adam_update(arena.master, arena.grad, m, v, arena.lowp, self.alpha_t, self.beta1, self.beta2,
+                      self.weight_decay, self.epsilon)
+
+    def step_range(self, arena, lo, hi):
+        m, v = self.state[id(arena)]
+        K.adam_update(arena.master[lo:hi], arena.grad[lo:hi], m[lo:hi], v[lo:hi],
+                      arena.lowp[lo:hi] if arena.lowp is not None else None, self.alpha_t, self.beta1, self.beta2,
                       self.weight_decay, self.epsilon)

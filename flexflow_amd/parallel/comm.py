@@ -324,7 +324,37 @@ class GradBucketer:
         self.bucket_bytes = bucket_bytes
         self.arenas = []  # (group_ranks, flat_grad, [buckets]) ; bucket = dict(lo, hi, params:set, ready:set)
         self.param_bucket = {}
+        self.param_buckets = {}  # sharded arenas: a parameter may straddle bucket boundaries
         self.handles = []
+
+    def add_sharded_arena(self, group_ranks, flat, segments, rank):
+        """ZeRO-1 arena (flexflow_amd/runtime/executor.py 'sharded optimizer'): buckets are fixed
+        element ranges whose length is a multiple of R x 16 (R = replicas), each reduce-SCATTERED
+        so rank r keeps the summed gradient of chunk r of every bucket. Returns the buckets."""
+        R = len(group_ranks)
+        unit = 16 * R
+        n = flat.numel()
+        assert n % unit == 0, (n, unit)
+        be = max(unit, (self.bucket_bytes // 4 + unit - 1) // unit * unit)
+        me = list(group_ranks).index(rank)
+        buckets = []
+        for lo in range(0, n, be):
+            hi = min(n, lo + be)
+            c = (hi - lo) // R
+            b = dict(lo=lo, hi=hi, params=set(), ready=set(), flat=flat, group=group_ranks, sharded=True,
+                     own=(lo + me * c, lo + (me + 1) * c))
+            buckets.append(b)
+        for key, lo, hi in segments:
+            for b in buckets:
+                if lo < b["hi"] and hi > b["lo"]:
+                    b["params"].add(key)
+                    self.param_buckets.setdefault(key, []).append(b)
+        for b in buckets:
+            if not b["params"]:  # padding only: nothing to wait for
+                b["params"] = {("pad", b["lo"])}
+                b["ready"] = set(b["params"])
+        self.arenas.append((group_ranks, flat, buckets))
+        return buckets
 
     def add_arena(self, group_ranks, flat, segments):
         """segments: list of (param_key, lo, hi) in gradient-completion order."""
@@ -343,22 +373,29 @@ class GradBucketer:
     def reset(self):
         for _, _, buckets in self.arenas:
             for b in buckets:
-                b["ready"] = set()
+                b["ready"] = {k for k in b["params"] if isinstance(k, tuple) and k[:1] == ("pad",)}
         self.handles = []
 
     def mark_ready(self, key):
-        b = self.param_bucket.get(key)
-        if b is None:
-            return
-        b["ready"].add(key)
-        if len(b["ready"]) == len(b["params"]):
-            self._launch(b)
+        bs = self.param_buckets.get(key)
+        if bs is None:
+            b = self.param_bucket.get(key)
+            bs = [b] if b is not None else []
+        for b in bs:
+            b["ready"].add(key)
+            if len(b["ready"]) == len(b["params"]):
+                self._launch(b)
 
     def _launch(self, b):
         if len(b["group"]) <= 1 or not self.comm.distributed:
             return
         view = b["flat"][b["lo"]:b["hi"]]
-        h = dist.all_reduce(view, group=self.comm.group(b["group"]), async_op=True)
+        g = self.comm.group(b["group"])
+        if b.get("sharded"):  # in-place reduce-scatter: this rank's chunk of the bucket gets the sum
+            out = b["flat"][b["own"][0]:b["own"][1]]
+            h = dist.reduce_scatter_tensor(out, view, group=g, async_op=True)
+        else:
+            h = dist.all_reduce(view, group=g, async_op=True)
         self.handles.append(h)
 
     def flush(self):

@@ -25,6 +25,8 @@ def _arenas(ex):
 
 def save_checkpoint(model, path: str):
     ex = model.executor
+    if getattr(ex, "zero", False):  # sharded optimizer: every rank saves the full master
+        ex.sync_master()
     opt = model.optimizer
     cfg = model.config
     os.makedirs(path, exist_ok=True)

@@ -199,14 +199,33 @@ class Executor:
                 ar = self.arenas.setdefault(grp, WeightArena(grp, self.device, lowp))
                 ar.add(w, wl.local_shape(p))
                 self.weight_loc[w.guid] = (ar, len(ar.entries) - 1)
-        for ar in self.arenas.values():
+        # ZeRO-1 sharded optimizer (opt-in --zero / FF_ZERO=1): replicated (data-parallel) arenas
+        # reduce-SCATTER their gradient buckets, each rank runs the optimizer on its 1/R chunk of
+        # every bucket, and the updated compute copy is all-gathered back, per bucket, while the
+        # next forward runs (each layer waits only for the buckets holding its weights)
+        self.zero = bool(getattr(self.config, "zero_optimizer", False) or os.environ.get("FF_ZERO") == "1") \
+            and self.comm.distributed
+        for grp, ar in self.arenas.items():
+            if self.zero and len(grp) > 1:
+                unit = 16 * len(grp)
+                ar.size = (ar.size + unit - 1) // unit * unit
             ar.materialize()
         self._rank_sets += [g for g in self.arenas.keys()]
         bucket_bytes = int(self.config.grad_bucket_mb * (1 << 20))
         self.bucketer = GradBucketer(self.comm, bucket_bytes)
+        self.zero_buckets = {}  # arena group -> sharded buckets
+        self._w_buckets = {}    # weight guid -> [(arena group, bucket index)]
+        self._ag_pending = {}   # (arena group, bucket index) -> async all-gather handle
+        self._master_stale = False
         for grp, ar in self.arenas.items():
             segs = [(w.guid, off, off + n) for (w, off, n, _) in ar.entries]
-            self.bucketer.add_arena(grp, ar.grad, segs)
+            if self.zero and len(grp) > 1:
+                bs = self.bucketer.add_sharded_arena(grp, ar.grad, segs, self.rank)
+                self.zero_buckets[grp] = bs
+                for key, lo, hi in segs:
+                    self._w_buckets[key] = [(grp, i) for i, b in enumerate(bs) if lo < b["hi"] and hi > b["lo"]]
+            else:
+                self.bucketer.add_arena(grp, ar.grad, segs)
         for L in self.layers:
             if L.name in self.ctx:
                 self.ctx[L.name].extra["wgrad_overwrite"] = bool(L.weights) and all(
@@ -329,6 +348,8 @@ class Executor:
                 ctx = self.ctx[L.name]
                 ctx.training = tr
                 ctx.step = self.step_idx
+                if self._ag_pending:
+                    self._wait_weights(L)
                 ws = [self.weight_tensor(w) for w in L.weights]
                 if self.hooks:
                     with self._hooked(L, "fwd"):
@@ -428,6 +449,8 @@ class Executor:
                 self._metric_acc[6] += d.numel()
 
     def backward(self):
+        if self._ag_pending:  # sharded optimizer: weights of layers this rank did not run
+            self.wait_all_gathers()
         self.bucketer.reset()
         self._wdone = {}
         grads: Dict[int, torch.Tensor] = {}
@@ -560,13 +583,54 @@ class Executor:
                 g.add_(torch.sign(m), alpha=l1)
 
     def update(self, optimizer):
+        if self._ag_pending:
+            self.wait_all_gathers()
         self.bucketer.flush()
         self._apply_regularizers()
         optimizer.next()
-        for ar in self.arenas.values():
-            if ar.size:
+        for grp, ar in self.arenas.items():
+            if not ar.size:
+                continue
+            bs = self.zero_buckets.get(grp)
+            if bs is None:
                 optimizer.step(ar)
+                continue
+            g = self.comm.group(grp)
+            for i, b in enumerate(bs):
+                lo, hi = b["own"]
+                optimizer.step_range(ar, lo, hi)
+                # the compute copy (bf16, or the fp32 master itself) of the whole bucket, in place
+                src = ar.lowp if ar.lowp is not None else ar.master
+                self._ag_pending[(grp, i)] = dist.all_gather_into_tensor(src[b["lo"]:b["hi"]], src[lo:hi], group=g,
+                                                                          async_op=True)
+            self._master_stale = ar.lowp is not None
         self.step_idx += 1
+
+    def _wait_weights(self, L):
+        """Sharded optimizer: the all-gathers of the buckets holding L's weights must land first."""
+        for w in L.weights:
+            for k in self._w_buckets.get(w.guid, ()):
+                h = self._ag_pending.pop(k, None)
+                if h is not None:
+                    h.wait()
+
+    def wait_all_gathers(self):
+        for h in self._ag_pending.values():
+            h.wait()
+        self._ag_pending = {}
+
+    def sync_master(self):
+        """Sharded optimizer: rank r's fp32 master is current only on its chunks; gather the full
+        master before reading weights (get_weights, checkpoints)."""
+        self.wait_all_gathers()
+        if not self._master_stale:
+            return
+        for grp, bs in self.zero_buckets.items():
+            ar = self.arenas[grp]
+            g = self.comm.group(grp)
+            for b in bs:
+                dist.all_gather_into_tensor(ar.master[b["lo"]:b["hi"]], ar.master[b["own"][0]:b["own"][1]], group=g)
+        self._master_stale = False
 
     def init_optimizer(self, optimizer):
         for ar in self.arenas.values():
@@ -598,6 +662,8 @@ class Executor:
         return full
 
     def get_weight(self, w):
+        if self.zero:
+            self.sync_master()
         loc = self.weight_tensor(w) if w.guid in self.weight_loc else None
         if loc is not None and w.guid in self.weight_loc:
             loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[0]
@@ -610,6 +676,8 @@ class Executor:
         return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False), dtype=torch.float32)
 
     def set_weight(self, w, value: np.ndarray):
+        if self.zero:
+            self.sync_master()
         if w.guid not in self.weight_loc:
             return
         ar, idx = self.weight_loc[w.guid]
