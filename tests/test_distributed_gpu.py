@@ -32,7 +32,8 @@ def _train(search, steps=3):
     import torch
     from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
     from flexflow_amd.models.bert import BertConfig, build_bert
-    cfg = FFConfig(["--dtype", "bf16", "--search", search])
+    extra = ["--zero"] if search.endswith("+zero") else []
+    cfg = FFConfig(["--dtype", "bf16", "--search", search.replace("+zero", "")] + extra)
     bc = BertConfig(hidden=256, heads=4, layers=2, ffn=1024, vocab=512, max_pos=128, seq=128)
     cfg.batch_size = B
     ff = FFModel(cfg)
@@ -87,7 +88,7 @@ def single():
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("search", ["dp", "unity"])
+@pytest.mark.parametrize("search", ["dp", "unity", "dp+zero"])
 def test_bert_two_ranks_match_single(single, search):
     par = _run_world(search)
     # per-token losses: bf16 activations, fp32 master weights and fp32 gradient sums
