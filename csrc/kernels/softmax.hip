@@ -183,6 +183,99 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const T* __restrict__
   }
 }
 
+// Register-resident variant for bf16 vocab-sized rows (2k..32k classes, even count): one 256-thread
+// workgroup per row holds the whole row in registers (NPT packed bf16 pairs per thread), so the
+// logits are read from HBM once instead of twice — the two-pass kernel above re-reads every row
+// in its gradient pass, and with thousands of 61 KB rows in flight the re-read misses every cache
+// (3.0 GB moved per call for 16384 x 30522 against 2.0 GB here; profiles/bert_large_hbm_bw_r1.txt).
+template <int NPT>
+__global__ void __launch_bounds__(256) softmax_xent_reg_kernel(const bf16_t* __restrict__ logits,
+                                                               const int* __restrict__ labels,
+                                                               float* __restrict__ loss, bf16_t* __restrict__ dlogits,
+                                                               int rows, int cols, float gscale,
+                                                               float* __restrict__ acc3) {
+  __shared__ float red_m[4], red_s[4];
+  __shared__ int red_i[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ndw = cols >> 1;
+  float correct = 0.f, ce = 0.f, cnt = 0.f;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const uint32_t* xr = reinterpret_cast<const uint32_t*>(logits + (int64_t)row * cols);
+    uint32_t v[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int d = tid + i * 256;
+      v[i] = d < ndw ? xr[d] : 0u;
+    }
+    // pass 1 (registers): max with first-index argmax, then sum of exp
+    float m = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int d = tid + i * 256;
+      if (d < ndw) {
+        const float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
+        if (lo > m) { m = lo; bi = 2 * d; }
+        if (hi > m) { m = hi; bi = 2 * d + 1; }
+      }
+    }
+    float sm = 0.f;
+    if (m != -INFINITY) {
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int d = tid + i * 256;
+        if (d < ndw) {
+          sm += __expf(__uint_as_float(v[i] << 16) - m) + __expf(__uint_as_float(v[i] & 0xffff0000u) - m);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(sm, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (m2 > m || (m2 == m && i2 < bi)) bi = i2;
+      online_merge(m, sm, m2, s2);
+    }
+    if (lane == 0) { red_m[w] = m; red_s[w] = sm; red_i[w] = bi; }
+    __syncthreads();
+    m = red_m[0]; sm = red_s[0]; bi = red_i[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      if (red_m[k] > m || (red_m[k] == m && red_i[k] < bi)) bi = red_i[k];
+      online_merge(m, sm, red_m[k], red_s[k]);
+    }
+    __syncthreads();  // red_* is rewritten by the next row
+    const int lab = labels[row];
+    const float lse = m + __logf(sm);
+    const bool valid = lab >= 0 && lab < cols;
+    if (tid == 0) {
+      const float xl = valid ? Cvt<bf16_t>::to_f(logits[(int64_t)row * cols + lab]) : 0.f;
+      const float l = valid ? lse - xl : 0.f;
+      if (loss) loss[row] = l;
+      correct += (bi == lab) ? 1.f : 0.f;
+      ce += l;
+      cnt += 1.f;
+    }
+    if (dlogits) {  // pass 2 (registers): (softmax - onehot) * gscale, packed bf16 pairs
+      uint32_t* dr = reinterpret_cast<uint32_t*>(dlogits + (int64_t)row * cols);
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int d = tid + i * 256;
+        if (d < ndw) {
+          const float p0 = (__expf(__uint_as_float(v[i] << 16) - lse) - (2 * d == lab ? 1.f : 0.f)) * gscale;
+          const float p1 = (__expf(__uint_as_float(v[i] & 0xffff0000u) - lse) - (2 * d + 1 == lab ? 1.f : 0.f)) * gscale;
+          dr[d] = (uint32_t)f2bf(p0) | ((uint32_t)f2bf(p1) << 16);
+        }
+      }
+    }
+  }
+  if (acc3 && tid == 0 && cnt > 0.f) {
+    atomicAdd(acc3 + 0, correct);
+    atomicAdd(acc3 + 1, ce);
+    atomicAdd(acc3 + 2, cnt);
+  }
+}
+
 // Reference semantics (src/loss_functions/loss_functions.cu): the model ends in a Softmax op,
 // the loss gradient w.r.t. the softmax INPUT is (p - y) * scale and Softmax::backward passes it
 // through. dprobs here is that gradient.
@@ -297,6 +390,21 @@ void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int 
 void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
                           int cols, float gscale, float* acc3, hipStream_t st) {
   if (rows == 0) return;
+  // opt-in (FF_XENT_REG=1): despite moving 1 GB less per call, the register-resident kernel measured
+  // 0.6 ms/step SLOWER in a same-box A/B of the BERT-Large step (53.2 vs 52.6 ms, profiles/
+  // softmax_xent_ab_r1.txt): one row per 256-thread workgroup with 4-B loads leaves too little
+  // memory-level parallelism, which the two-pass kernel's 16-B x 4-deep loads have
+  static const int reg_ok = getenv("FF_XENT_REG") ? atoi(getenv("FF_XENT_REG")) : 0;
+  if (reg_ok && dt == DT_BF16 && cols % 2 == 0 && cols >= 4096 && cols <= 2 * 256 * 64) {
+    const int g = std::min(rows, 2048);
+    if (cols <= 2 * 256 * 32)
+      hipLaunchKernelGGL(softmax_xent_reg_kernel<32>, dim3(g), dim3(256), 0, st, (const bf16_t*)logits, labels, loss,
+                         (bf16_t*)dlogits, rows, cols, gscale, acc3);
+    else
+      hipLaunchKernelGGL(softmax_xent_reg_kernel<64>, dim3(g), dim3(256), 0, st, (const bf16_t*)logits, labels, loss,
+                         (bf16_t*)dlogits, rows, cols, gscale, acc3);
+    return;
+  }
   DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st,
                                      (const T*)logits, labels, loss, (T*)dlogits, rows, cols, gscale, acc3));
 }

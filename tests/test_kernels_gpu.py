@@ -243,7 +243,7 @@ def test_softmax_and_xent(ffC):
     assert _rel(dl, xr.grad) < 1e-4
 
 
-@pytest.mark.parametrize("cols", [30522, 1001, 64])
+@pytest.mark.parametrize("cols", [30522, 1001, 64, 8192, 16386, 32768])
 def test_softmax_xent_bf16_metrics(ffC, cols):
     """Fused softmax-xent on bf16 logits whose rows start at every 4-B offset (odd vocab), with the
     accuracy / CE metrics folded into the same pass."""
