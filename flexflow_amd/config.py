@@ -9,6 +9,7 @@ is accepted and used only when no launcher environment is present.
 from __future__ import annotations
 
 import os
+import warnings
 import sys
 import time
 
@@ -107,109 +108,114 @@ class FFConfig:
 
         while i < n:
             a = argv[i]
-            if a in ("-e", "--epochs"):
-                self.epochs = int(nxt())
-            elif a in ("-b", "--batch-size"):
-                self.batch_size = int(nxt())
-            elif a in ("--lr", "--learning-rate"):
-                self.learning_rate = float(nxt())
-            elif a in ("--wd", "--weight-decay"):
-                self.weight_decay = float(nxt())
-            elif a in ("-p", "--print-freq"):
-                self.print_freq = int(nxt())
-            elif a in ("-d", "--dataset"):
-                self.dataset_path = nxt()
-            elif a in ("--budget", "--search-budget"):
-                self.search_budget = int(nxt())
-            elif a in ("--alpha", "--search-alpha"):
-                self.search_alpha = float(nxt())
-            elif a in ("--import", "--import-strategy"):
-                self.import_strategy_file = nxt()
-            elif a in ("--export", "--export-strategy"):
-                self.export_strategy_file = nxt()
-            elif a == "--only-data-parallel":
-                self.only_data_parallel = True
-            elif a == "--enable-parameter-parallel":
-                self.enable_parameter_parallel = True
-            elif a == "--enable-attribute-parallel":
-                self.enable_attribute_parallel = True
-            elif a == "-ll:gpu":
-                v = int(nxt())
-                if "WORLD_SIZE" not in os.environ:
-                    self.workers_per_node = v
-            elif a == "-ll:fsize":
-                self.device_mem = float(nxt())
-            elif a == "--nodes":
-                self.num_nodes = int(nxt())
-            elif a == "-ll:cpu":
-                self.cpus_per_node = int(nxt())
-            elif a == "--profiling":
-                self.profiling = True
-            elif a == "--allow-tensor-op-math-conversion":
-                self.allow_tensor_op_math_conversion = True
-            elif a == "--fusion":
-                self.perform_fusion = True
-            elif a == "--overlap":
-                self.search_overlap_backward_update = True
-            elif a == "--taskgraph":
-                self.export_strategy_task_graph_file = nxt()
-            elif a == "--include-costs-dot-graph":
-                self.include_costs_dot_graph = True
-            elif a == "--compgraph":
-                self.export_strategy_computation_graph_file = nxt()
-            elif a == "--machine-model-version":
-                self.machine_model_version = int(nxt())
-            elif a == "--machine-model-file":
-                self.machine_model_file = nxt()
-            elif a == "--simulator-segment-size":
-                self.simulator_segment_size = int(nxt())
-            elif a == "--simulator-max-num-segments":
-                self.simulator_max_num_segments = int(nxt())
-            elif a == "--enable-propagation":
-                self.enable_propagation = True
-            elif a == "--enable-inplace-optimizations":
-                self.enable_inplace_optimizations = True
-            elif a == "--search-num-nodes":
-                self.search_num_nodes = int(nxt())
-            elif a == "--search-num-workers":
-                self.search_num_workers = int(nxt())
-            elif a == "--base-optimize-threshold":
-                self.base_optimize_threshold = int(nxt())
-            elif a == "--disable-control-replication":
-                self.enable_control_replication = False
-            elif a == "--python-data-loader-type":
-                self.python_data_loader_type = int(nxt())
-            elif a == "--substitution-json":
-                self.substitution_json_path = nxt()
-            elif a == "--memory-search":
-                self.perform_memory_search = True
-            # ---- MI355X-native flags
-            elif a == "--dtype":
-                v = nxt()
-                self.compute_dtype = {"bf16": DataType.DT_BF16, "fp32": DataType.DT_FLOAT,
-                                      "float": DataType.DT_FLOAT}[v]
-            elif a == "--no-hip-graphs":
-                self.hip_graphs = False
-            elif a == "--hip-graphs":
-                self.hip_graphs = True
-            elif a == "--search":
-                self.search_algo = nxt()
-            elif a == "--mcmc-iterations":
-                self.mcmc_iterations = int(nxt())
-            elif a == "--zero":
-                self.zero_optimizer = True
-            elif a == "--grad-bucket-mb":
-                self.grad_bucket_mb = float(nxt())
-            elif a == "--seed":
-                self.seed = int(nxt())
-            elif a == "--trace-dir":
-                self.trace_dir = nxt()
-            elif a == "--check-nan":
-                self.check_nan_every = int(nxt())
-            elif a == "--watchdog":
-                self.watchdog_s = float(nxt())
-            elif a == "--dist-timeout":
-                self.dist_timeout_s = float(nxt())
+            try:
+                if a in ("-e", "--epochs"):
+                    self.epochs = int(nxt())
+                elif a in ("-b", "--batch-size"):
+                    self.batch_size = int(nxt())
+                elif a in ("--lr", "--learning-rate"):
+                    self.learning_rate = float(nxt())
+                elif a in ("--wd", "--weight-decay"):
+                    self.weight_decay = float(nxt())
+                elif a in ("-p", "--print-freq"):
+                    self.print_freq = int(nxt())
+                elif a in ("-d", "--dataset"):
+                    self.dataset_path = nxt()
+                elif a in ("--budget", "--search-budget"):
+                    self.search_budget = int(nxt())
+                elif a in ("--alpha", "--search-alpha"):
+                    self.search_alpha = float(nxt())
+                elif a in ("--import", "--import-strategy"):
+                    self.import_strategy_file = nxt()
+                elif a in ("--export", "--export-strategy"):
+                    self.export_strategy_file = nxt()
+                elif a == "--only-data-parallel":
+                    self.only_data_parallel = True
+                elif a == "--enable-parameter-parallel":
+                    self.enable_parameter_parallel = True
+                elif a == "--enable-attribute-parallel":
+                    self.enable_attribute_parallel = True
+                elif a == "-ll:gpu":
+                    v = int(nxt())
+                    if "WORLD_SIZE" not in os.environ:
+                        self.workers_per_node = v
+                elif a == "-ll:fsize":
+                    self.device_mem = float(nxt())
+                elif a == "--nodes":
+                    self.num_nodes = int(nxt())
+                elif a == "-ll:cpu":
+                    self.cpus_per_node = int(nxt())
+                elif a == "--profiling":
+                    self.profiling = True
+                elif a == "--allow-tensor-op-math-conversion":
+                    self.allow_tensor_op_math_conversion = True
+                elif a == "--fusion":
+                    self.perform_fusion = True
+                elif a == "--overlap":
+                    self.search_overlap_backward_update = True
+                elif a == "--taskgraph":
+                    self.export_strategy_task_graph_file = nxt()
+                elif a == "--include-costs-dot-graph":
+                    self.include_costs_dot_graph = True
+                elif a == "--compgraph":
+                    self.export_strategy_computation_graph_file = nxt()
+                elif a == "--machine-model-version":
+                    self.machine_model_version = int(nxt())
+                elif a == "--machine-model-file":
+                    self.machine_model_file = nxt()
+                elif a == "--simulator-segment-size":
+                    self.simulator_segment_size = int(nxt())
+                elif a == "--simulator-max-num-segments":
+                    self.simulator_max_num_segments = int(nxt())
+                elif a == "--enable-propagation":
+                    self.enable_propagation = True
+                elif a == "--enable-inplace-optimizations":
+                    self.enable_inplace_optimizations = True
+                elif a == "--search-num-nodes":
+                    self.search_num_nodes = int(nxt())
+                elif a == "--search-num-workers":
+                    self.search_num_workers = int(nxt())
+                elif a == "--base-optimize-threshold":
+                    self.base_optimize_threshold = int(nxt())
+                elif a == "--disable-control-replication":
+                    self.enable_control_replication = False
+                elif a == "--python-data-loader-type":
+                    self.python_data_loader_type = int(nxt())
+                elif a == "--substitution-json":
+                    self.substitution_json_path = nxt()
+                elif a == "--memory-search":
+                    self.perform_memory_search = True
+                # ---- MI355X-native flags
+                elif a == "--dtype":
+                    v = nxt()
+                    self.compute_dtype = {"bf16": DataType.DT_BF16, "fp32": DataType.DT_FLOAT,
+                                          "float": DataType.DT_FLOAT}[v]
+                elif a == "--no-hip-graphs":
+                    self.hip_graphs = False
+                elif a == "--hip-graphs":
+                    self.hip_graphs = True
+                elif a == "--search":
+                    self.search_algo = nxt()
+                elif a == "--mcmc-iterations":
+                    self.mcmc_iterations = int(nxt())
+                elif a == "--zero":
+                    self.zero_optimizer = True
+                elif a == "--grad-bucket-mb":
+                    self.grad_bucket_mb = float(nxt())
+                elif a == "--seed":
+                    self.seed = int(nxt())
+                elif a == "--trace-dir":
+                    self.trace_dir = nxt()
+                elif a == "--check-nan":
+                    self.check_nan_every = int(nxt())
+                elif a == "--watchdog":
+                    self.watchdog_s = float(nxt())
+                elif a == "--dist-timeout":
+                    self.dist_timeout_s = float(nxt())
+            except (TypeError, ValueError):
+                # a flag meant for another program (pytest, torchrun, a launcher) whose value is not
+                # ours to parse: keep the default, as the reference's atoi-based parser does
+                warnings.warn(f"FFConfig: ignoring flag {a!r} (unparsable value)")
             i += 1
         if self.only_data_parallel:
             self.search_algo = "dp"
