@@ -16,6 +16,10 @@ import time
 from .type import CompMode, DataType
 
 
+# short flags we share with launchers that may leave their argv in sys.argv (pytest: -p plugin)
+_FOREIGN_COLLISIONS = frozenset({"-p"})
+
+
 class FFConfig:
     # reference DefaultConfig (model.cc:3470-3499)
     DEFAULT_BATCH_SIZE = 64
@@ -213,9 +217,15 @@ class FFConfig:
                 elif a == "--dist-timeout":
                     self.dist_timeout_s = float(nxt())
             except (TypeError, ValueError):
-                # a flag meant for another program (pytest, torchrun, a launcher) whose value is not
-                # ours to parse: keep the default, as the reference's atoi-based parser does
-                warnings.warn(f"FFConfig: ignoring flag {a!r} (unparsable value)")
+                v = argv[i] if i < n else None
+                if v is not None and not v.startswith("-") and a not in _FOREIGN_COLLISIONS:
+                    raise ValueError(f"FFConfig: bad value {v!r} for flag {a!r}") from None
+                # a flag of another program (pytest's `-p no:cacheprovider`) or a flag whose value
+                # is missing / is the next flag: keep the default and re-read the next flag. (The
+                # reference's atoi/atof parser would set 0 instead, src/runtime/model.cc:3567-3580.)
+                warnings.warn(f"FFConfig: ignoring flag {a!r} (value {v!r} not ours to parse)")
+                if v is not None and v.startswith("-"):
+                    i -= 1
             i += 1
         if self.only_data_parallel:
             self.search_algo = "dp"

@@ -23,12 +23,20 @@ def _arenas(ex):
     return [(i, ar) for i, ar in enumerate(ex.arenas.values()) if ar.size]
 
 
+def _used(ar) -> int:
+    """Elements of the arena actually holding weights (the rest is alignment / ZeRO padding)."""
+    return max((int(e[1]) + int(e[2]) for e in ar.entries), default=0)
+
+
 def save_checkpoint(model, path: str):
     ex = model.executor
-    if getattr(ex, "zero", False):  # sharded optimizer: every rank saves the full master
-        ex.sync_master()
     opt = model.optimizer
     cfg = model.config
+    if getattr(ex, "zero", False):
+        # sharded optimizer: every rank saves the full master AND the full optimizer state, so
+        # the checkpoint is independent of the sharding geometry it was written under
+        ex.sync_master()
+        ex.sync_optimizer_state(opt)
     os.makedirs(path, exist_ok=True)
     tensors = {}
     layout = []
@@ -38,12 +46,16 @@ def save_checkpoint(model, path: str):
         if st is not None:
             for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
                 tensors[f"arena{i}.opt{j}"] = t.detach().contiguous().cpu()
-        layout.append({"arena": i, "size": int(ar.size), "entries": [[getattr(e[0], "name", str(e[0])), int(e[1]), int(e[2])] for e in ar.entries]})
+        layout.append({"arena": i, "size": int(ar.size), "used": _used(ar),
+                       "entries": [[getattr(e[0], "name", str(e[0])), int(e[1]), int(e[2])] for e in ar.entries]})
     save_file(tensors, os.path.join(path, f"rank{cfg.rank}.safetensors"))
     if cfg.rank == 0:
         meta = {
             "step": int(ex.step_idx),
             "world_size": int(cfg.world_size),
+            # informational: the state above is gathered, so resuming under another sharding is fine
+            "zero": bool(getattr(ex, "zero", False)),
+            "grad_bucket_bytes": int(getattr(ex.bucketer, "bucket_bytes", 0) or 0),
             # positional (layer order), so a rebuilt model whose auto-generated names differ still matches
             "strategy": [[L.name, L.op_type.name, model.strategy[L.name].to_json()] for L in model.layers],
             "optimizer": {k: v for k, v in vars(opt).items() if isinstance(v, (int, float, bool, str))},
@@ -70,11 +82,15 @@ def load_checkpoint(model, path: str, strict: bool = True):
             raise ValueError("checkpoint strategy differs from the compiled strategy (import it with "
                              "--import-strategy to resume)")
     tensors = load_file(os.path.join(path, f"rank{cfg.rank}.safetensors"))
+    saved = {a["arena"]: a for a in meta.get("arenas", [])}
     for i, ar in _arenas(ex):
         m = tensors[f"arena{i}.master"]
-        if m.numel() != ar.master.numel():
-            raise ValueError(f"arena {i} size mismatch")
-        ar.master.copy_(m.to(ar.master.device))
+        used = _used(ar)
+        # arenas are padded to a multiple of 16*R under --zero; only the used prefix must agree
+        if used != saved.get(i, {}).get("used", m.numel()) or m.numel() < used:
+            raise ValueError(f"arena {i} size mismatch ({m.numel()} saved, {used} used by this job)")
+        ar.master.zero_()
+        ar.master[:used].copy_(m[:used].to(ar.master.device))
         if ar.lowp is not None:
             ar.lowp.copy_(ar.master.to(ar.lowp.dtype))
         st = getattr(opt, "state", {}).get(id(ar))
@@ -82,9 +98,11 @@ def load_checkpoint(model, path: str, strict: bool = True):
             for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
                 key = f"arena{i}.opt{j}"
                 if key in tensors:
-                    t.copy_(tensors[key].to(t.device))
+                    t.zero_()
+                    t[:used].copy_(tensors[key][:used].to(t.device))
     for k, v in meta.get("optimizer", {}).items():
         if hasattr(opt, k) and not callable(getattr(opt, k)):
             setattr(opt, k, v)
+    ex._master_stale = False  # every rank now holds the full master
     ex.step_idx = int(meta["step"])
     return meta["step"]

@@ -588,6 +588,7 @@ class Executor:
         self.bucketer.flush()
         self._apply_regularizers()
         optimizer.next()
+        self._master_stale = False
         for grp, ar in self.arenas.items():
             if not ar.size:
                 continue
@@ -603,7 +604,7 @@ class Executor:
                 src = ar.lowp if ar.lowp is not None else ar.master
                 self._ag_pending[(grp, i)] = dist.all_gather_into_tensor(src[b["lo"]:b["hi"]], src[lo:hi], group=g,
                                                                           async_op=True)
-            self._master_stale = ar.lowp is not None
+            self._master_stale |= ar.lowp is not None
         self.step_idx += 1
 
     def _wait_weights(self, L):
@@ -631,6 +632,21 @@ class Executor:
             for b in bs:
                 dist.all_gather_into_tensor(ar.master[b["lo"]:b["hi"]], ar.master[b["own"][0]:b["own"][1]], group=g)
         self._master_stale = False
+
+    def sync_optimizer_state(self, optimizer):
+        """Sharded optimizer: each rank's Adam m/v (SGD momentum) is current only on its own chunk
+        of every bucket; gather the full state so a checkpoint does not depend on the sharding
+        (world size, --grad-bucket-mb, --zero on or off at resume time)."""
+        self.wait_all_gathers()
+        for grp, bs in self.zero_buckets.items():
+            ar = self.arenas[grp]
+            st = getattr(optimizer, "state", {}).get(id(ar))
+            if st is None:
+                continue
+            g = self.comm.group(grp)
+            for t in (st if isinstance(st, (tuple, list)) else (st,)):
+                for b in bs:
+                    dist.all_gather_into_tensor(t[b["lo"]:b["hi"]], t[b["own"][0]:b["own"][1]], group=g)
 
     def init_optimizer(self, optimizer):
         for ar in self.arenas.values():

@@ -34,6 +34,10 @@ class StepGraph:
     def enabled(self) -> bool:
         m = self.model
         ex = m.executor
+        # ZeRO-1: update() leaves async all-gathers of the compute copy in flight and forward waits
+        # for them layer by layer from Python; a replayed graph would never run those waits
+        if getattr(ex, "zero", False):
+            return False
         if not (m.config.hip_graphs and torch.cuda.is_available() and ex.device.type == "cuda"):
             return False
         if self.decision is False:

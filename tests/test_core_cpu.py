@@ -160,3 +160,20 @@ def test_reference_op_layer_classes():
     assert isinstance(l0, core.Linear) and isinstance(l0, core.Layer)
     assert isinstance(l1, core.Exp) and l1.name == "my_exp"
     assert l0.get_weight_tensor() is not None and t is l1.get_output_tensor()
+
+
+def test_config_flag_values():
+    """Our own flags raise on a malformed value; a foreign `-p no:plugin` (pytest) or a flag whose
+    value is the next flag is ignored with a warning and the next flag is still parsed."""
+    import pytest
+    from flexflow_amd.config import FFConfig
+    with pytest.raises(ValueError):
+        FFConfig(["-b", "32x"])
+    with pytest.raises(ValueError):
+        FFConfig(["--lr", "1e-3,"])
+    with pytest.warns(UserWarning):
+        c = FFConfig(["-p", "no:cacheprovider", "-b", "48"])
+    assert c.batch_size == 48
+    with pytest.warns(UserWarning):
+        c = FFConfig(["--lr", "--zero", "-b", "16"])
+    assert c.batch_size == 16 and c.zero_optimizer

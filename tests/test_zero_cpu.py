@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _train(flags, steps=3, ckpt=None):
+def _train(flags, steps=3, ckpt=None, resume=None):
     from flexflow_amd.core import (ActiMode, AdamOptimizer, DataType, FFConfig, FFModel, LossType,
                                    MetricsType)
     cfg = FFConfig(["--search", "dp", "--grad-bucket-mb", "0.02"] + flags)  # many small buckets
@@ -38,6 +38,8 @@ def _train(flags, steps=3, ckpt=None):
     rng = np.random.default_rng(0)
     x.set_tensor(ff, rng.standard_normal((B, 40)).astype(np.float32))
     ff.label_tensor.set_tensor(ff, rng.integers(0, 10, (B, 1)).astype(np.int32))
+    if resume:
+        ff.load_checkpoint(resume)
     for _ in range(steps):
         ff.train_step()
     res = {}
@@ -50,24 +52,24 @@ def _train(flags, steps=3, ckpt=None):
     return res
 
 
-def _worker(rank, world, port, flags, out_file, ckpt):
+def _worker(rank, world, port, flags, out_file, ckpt, steps=3, resume=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), FF_DIST_BACKEND="gloo")
     os.environ["CUDA_VISIBLE_DEVICES"] = ""
     sys.path.insert(0, os.path.dirname(HERE))
     import torch
     torch.set_num_threads(1)
-    res = _train(flags, ckpt=ckpt)
+    res = _train(flags, steps=steps, ckpt=ckpt, resume=resume)
     np.savez(out_file.replace(".npz", f"{rank}.npz"), **res)
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(flags, world=2, ckpt=None):
+def _run(flags, world=2, ckpt=None, steps=3, resume=None):
     tmp = tempfile.mkdtemp()
     out = os.path.join(tmp, "out.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), flags, out, ckpt), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), flags, out, ckpt, steps, resume), nprocs=world, join=True,
                        start_method="spawn")
     return [dict(np.load(out.replace(".npz", f"{r}.npz"))) for r in range(world)]
 
@@ -116,3 +118,32 @@ def test_sharded_bucket_geometry(R, n):
     for key, lo, hi in segs:
         touched = [b for b in bs if lo < b["hi"] and hi > b["lo"]]
         assert bk.param_buckets[key] == touched
+
+
+def test_zero_checkpoint_resume_under_other_sharding(tmp_path):
+    """A --zero checkpoint holds the gathered Adam state, so resuming it under a different bucket
+    size, or without --zero, continues exactly like an uninterrupted run (advisor finding: the
+    per-rank m/v used to be valid only on that rank's chunk of each bucket)."""
+    ck = str(tmp_path / "ck")
+    straight = _train([], steps=5)
+    _run(["--zero"], ckpt=ck, steps=3)
+    other_buckets = _run(["--zero", "--grad-bucket-mb", "0.005"], steps=2, resume=ck)
+    no_zero = _run([], steps=2, resume=ck)
+    for k, v in straight.items():
+        if k == "zero":
+            continue
+        for r in range(2):
+            np.testing.assert_allclose(other_buckets[r][k], v, rtol=1e-4, atol=1e-5, err_msg=f"zero->zero' rank{r} {k}")
+            np.testing.assert_allclose(no_zero[r][k], v, rtol=1e-4, atol=1e-5, err_msg=f"zero->dp rank{r} {k}")
+
+
+def test_zero_never_captured_in_hip_graph(monkeypatch):
+    """--zero with FF_GRAPH_COLLECTIVES=1 must run eagerly: the per-layer all-gather waits live in
+    Python and a replayed graph would read half-gathered weights."""
+    from types import SimpleNamespace
+    from flexflow_amd.runtime.graph import StepGraph
+    monkeypatch.setenv("FF_GRAPH_COLLECTIVES", "1")
+    ex = SimpleNamespace(zero=True, hooks=[], comm=SimpleNamespace(distributed=True),
+                         device=SimpleNamespace(type="cuda"))
+    m = SimpleNamespace(executor=ex, config=SimpleNamespace(hip_graphs=True))
+    assert StepGraph(m).enabled() is False
