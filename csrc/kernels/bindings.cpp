@@ -6,6 +6,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "attention.h"
+#include "blaslt.h"
 #include "gemm.h"
 #include "ops.h"
 
@@ -270,6 +271,28 @@ void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
   ffk::attn_bwd(a, cur_stream());
 }
 
+
+// ---- hipBLASLt with fused epilogues (blaslt.h)
+std::tuple<int64_t, int64_t> lt_plan(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
+                                     int64_t batch, int64_t sA, int64_t sB, int64_t sC, bool a_k, bool b_k,
+                                     bool out_f32, bool bias_f32, bool beta_nz, int64_t epi, int64_t aux_ld,
+                                     int64_t max_algos, bool all_algos, int64_t max_ws, optional<Tensor> bias,
+                                     optional<Tensor> aux) {
+  ffk::lt::PlanKey k{M, N, K, lda, ldb, ldc, batch, sA, sB, sC, a_k, b_k, out_f32, bias_f32, beta_nz, (int)epi, aux_ld};
+  int n = 0;
+  int64_t id = ffk::lt::plan(k, (int)max_algos, all_algos, (size_t)max_ws, ptr(bias), ptr(aux), &n);
+  return {id, n};
+}
+
+int64_t lt_run(int64_t plan, int64_t algo, Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> aux,
+               double alpha, double beta, optional<Tensor> ws) {
+  check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "lt_run: A/B must be bf16");
+  size_t wsb = (ws.has_value() && ws->defined()) ? (size_t)ws->numel() * ws->element_size() : 0;
+  return ffk::lt::run(plan, (int)algo, A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr(bias), ptr(aux), (float)alpha,
+                      (float)beta, ptr(ws), wsb, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -278,6 +301,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
         py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2);
+  m.def("lt_plan", &lt_plan);
+  m.def("lt_run", &lt_run);
+  m.def("lt_num_algos", [](int64_t p) { return ffk::lt::num_algos(p); });
+  m.def("lt_algo_index", [](int64_t p, int64_t a) { return ffk::lt::algo_index(p, (int)a); });
+  m.def("lt_find_algo", [](int64_t p, int64_t sol, int64_t max_ws) { return ffk::lt::find_algo(p, (int)sol, (size_t)max_ws); });
+  m.def("lt_algo_ws", [](int64_t p, int64_t a) { return (int64_t)ffk::lt::algo_ws(p, (int)a); });
+  m.def("lt_algo_name", [](int64_t p, int64_t a) { return ffk::lt::algo_name(p, (int)a); });
   m.def("gemm_pick_splitk", &gemm_pick_splitk, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("batch"),
         py::arg("impl") = 2);
   m.def("unary_fwd", &unary_fwd);

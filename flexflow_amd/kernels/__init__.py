@@ -200,6 +200,117 @@ def _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, S):
     ext().slab_sum(slabs, C, S, beta)
 
 
+# ------------------------------------------------------------------ hipBLASLt, called directly
+# torch.mm reaches hipBLASLt through its heuristic (or TunableOp's table). csrc/kernels/blaslt.cpp
+# calls the library directly: it enumerates every solution the library accepts for a call site
+# (bias in the epilogue), and gemm() times them once next to our kernels, keeping the fastest.
+# Measured on MI355X (profiles/lt_probe_r2.txt): in isolation the best solution beat torch.mm by
+# 10-15 % on FFN shapes, but inside the BERT-Large step the TunableOp table already picks as well
+# (same-box A/B 50.36/50.58 ms without vs 50.49/50.75 ms with, profiles/lt_ab_r2.txt), and the
+# GELU-with-aux and dGELU epilogues that would remove our activation passes have no bf16
+# solution on gfx950 in this library build. Kept opt-in (FF_LT=1) for other shapes and models.
+LT_WS_BYTES = 64 << 20
+EPI_NONE, EPI_BIAS = 0, 1
+_LT = _os.environ.get("FF_LT", "0") == "1"  # opt-in: no in-step gain measured (profiles/lt_ab_r2.txt)
+_lt_ok = [None]
+
+
+def _lt_ws(dev):
+    from ..runtime.device import DeviceContext
+    return DeviceContext.get(dev).workspace("hipblaslt", LT_WS_BYTES, torch.uint8)
+
+
+def _lt_plan(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC, bias, beta, epi, max_algos=512):
+    X = ext()
+    pid, n = X.lt_plan(M, N, K, lda, ldb, ldc, batch, sA, sB, sC, a_k, b_k, C.dtype == torch.float32,
+                       bias is not None and bias.dtype == torch.float32, beta != 0.0, epi, ldc, max_algos, True,
+                       LT_WS_BYTES, bias, None)
+    return pid, n
+
+
+def _lt_run(pid, algo, A, B, C, bias, alpha, beta):
+    st = ext().lt_run(pid, algo, A, B, C, bias, None, float(alpha), float(beta), _lt_ws(C.device))
+    if st != 0:
+        raise RuntimeError(f"hipBLASLt matmul failed (status {st})")
+
+
+def _lt_tune(pid, n, A, B, C, bias, alpha, beta):
+    """Best (algo, ms) among the plan's candidates: one quick pass, the 6 fastest re-timed."""
+    X = ext()
+    ws = _lt_ws(C.device)
+    quick = []
+    for a in range(n):
+        if X.lt_run(pid, a, A, B, C, bias, None, float(alpha), float(beta), ws) != 0:
+            continue
+        quick.append((_time(lambda a=a: X.lt_run(pid, a, A, B, C, bias, None, float(alpha), float(beta), ws), 3), a))
+    if not quick:
+        return None, float("inf")
+    quick.sort()
+    fine = [(_time(lambda a=a: X.lt_run(pid, a, A, B, C, bias, None, float(alpha), float(beta), ws), 10), a)
+            for _, a in quick[:6]]
+    t, a = min(fine)
+    return a, t
+
+
+def _lt_candidates(A, B, C, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, Z, act, batch, sA, sB,
+                   sC, plain, times):
+    """Adds hipBLASLt candidates to an autotune table: the GEMM as called (bias in the epilogue), the
+    split-K strided-batched form for weight gradients, and GEMM+bias then our activation pass for
+    activation epilogues (the library has no GELU-with-aux epilogue for bf16 on gfx950)."""
+    try:
+        if plain:
+            pid, n = _lt_plan(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC, bias, beta,
+                              EPI_BIAS if bias is not None else EPI_NONE)
+            a, t = _lt_tune(pid, n, A, B, scratch, bias, alpha, beta)
+            if a is not None:
+                times[("lt", pid, a)] = t
+            if C.dtype == torch.float32 and batch == 1 and alpha == 1.0 and bias is None and ldc == N and \
+                    (M * N) % 4 == 0 and M * N <= (1 << 25) and K >= 8192:
+                for S in ((2, 4, 8) if M * N <= (1 << 24) else (2,)):
+                    if K % (S * 8):
+                        continue
+                    kc = K // S
+                    slabs = torch.empty((S, M, N), device=C.device, dtype=torch.float32)
+                    pid, n = _lt_plan(A, B, slabs, M, N, kc, a_k, b_k, lda, ldb, N, S, kc if a_k else kc * lda,
+                                      kc if b_k else kc * ldb, M * N, None, 0.0, EPI_NONE)
+                    a, _ = _lt_tune(pid, n, A, B, slabs, None, 1.0, 0.0)
+                    if a is not None:
+                        times[("lt_sk", pid, a, S)] = _time(lambda: _lt_splitk(pid, a, A, B, scratch, M, N, S, beta))
+        elif (act != ACT_NONE or bias is not None) and alpha == 1.0 and beta == 0.0 and batch == 1 and ldc == N and \
+                N % 8 == 0 and C.dtype == torch.bfloat16 and (Z is None or Z.dtype == torch.bfloat16):
+            zs = torch.empty_like(C) if Z is not None else scratch
+            pid, n = _lt_plan(A, B, zs, M, N, K, a_k, b_k, lda, ldb, ldc, 1, 0, 0, 0, bias, 0.0,
+                              EPI_BIAS if bias is not None else EPI_NONE)
+            a, _ = _lt_tune(pid, n, A, B, zs, bias, 1.0, 0.0)
+            if a is not None:
+                times[("lt_act", pid, a)] = _time(lambda: _lt_act(pid, a, A, B, scratch, Z is not None and zs, M, N,
+                                                                  bias, act))
+    except RuntimeError as e:  # a library refusal is a missing candidate, never a failed step
+        TUNE_LOG.append({"M": M, "N": N, "K": K, "lt_error": str(e)})
+
+
+def _lt_splitk(pid, a, A, B, C, M, N, S, beta):
+    slabs = torch.empty((S, M, N), device=C.device, dtype=torch.float32)
+    _lt_run(pid, a, A, B, slabs, None, 1.0, 0.0)
+    ext().slab_sum(slabs, C, S, beta)
+
+
+def _lt_act(pid, a, A, B, C, Z, M, N, bias, act):
+    zbuf = Z if Z is not None and Z is not False else C
+    _lt_run(pid, a, A, B, zbuf, bias, 1.0, 0.0)
+    ext().bias_act_fwd(zbuf, None, None, C, M, N, act)
+
+
+def _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act):
+    kind = choice[0]
+    if kind == "lt":
+        _lt_run(choice[1], choice[2], A, B, C, bias, alpha, beta)
+    elif kind == "lt_sk":
+        _lt_splitk(choice[1], choice[2], A, B, C, M, N, choice[3], beta)
+    else:  # "lt_act"
+        _lt_act(choice[1], choice[2], A, B, C, Z, M, N, bias, act)
+
+
 def _time(fn, reps=8):
     fn()
     fn()
@@ -262,11 +373,16 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                         cands["lib_bias_act"] = lambda: _lib_gemm_bias_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda,
                                                                            ldb, bias, act)
                 times = {k: _time(f) for k, f in cands.items()}
-                choice = min(times, key=times.get)
+                if _LT and C.dtype in (torch.bfloat16, torch.float32):
+                    _lt_candidates(A, B, C, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, Z, act,
+                                   batch, sA, sB, sC, plain, times)
+                choice = min(times, key=lambda k: times[k])
                 TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
-                                 "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
+                                 "times_ms": {str(k): round(v, 4) for k, v in times.items()}, "choice": str(choice)})
             _tuned[key] = choice
-        if isinstance(choice, str) and choice.startswith("lib_sk"):
+        if isinstance(choice, tuple):
+            _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
+        elif isinstance(choice, str) and choice.startswith("lib_sk"):
             _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, int(choice[6:]))
         elif choice == "lib":
             _lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, batch, sA, sB, sC)

@@ -364,3 +364,52 @@ def test_lib_splitk_wgrad(ffC, a_k, b_k, S, beta):
     ref = Af @ Bf + beta * C
     K._lib_gemm_splitk(A, B, C, M, N, Kd, a_k, b_k, A.shape[-1], B.shape[-1], beta, S)
     assert _rel(C, ref) < 2e-3
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("out_f32,beta,with_bias", [(False, 0.0, False), (False, 0.0, True), (True, 1.0, False),
+                                                    (False, 1.0, False)])
+def test_hipblaslt_direct(ffC, a_k, b_k, out_f32, beta, with_bias):
+    """Direct hipBLASLt plans (csrc/kernels/blaslt.cpp): every candidate the tuner may pick computes
+    the same GEMM (row-major <-> column-major mapping, bias epilogue, beta accumulate, fp32 out)."""
+    from flexflow_amd import kernels as Kn
+    torch.manual_seed(3)
+    M, N, K = 640, 384, 320
+    Am = torch.randn(M, K, device=DEV).bfloat16()
+    Bn = torch.randn(N, K, device=DEV).bfloat16()
+    A = Am if a_k else Am.t().contiguous()
+    B = Bn if b_k else Bn.t().contiguous()
+    bias = torch.randn(N, device=DEV).bfloat16() if with_bias else None
+    C0 = torch.randn(M, N, device=DEV).to(torch.float32 if out_f32 else torch.bfloat16)
+    ref = Am.float() @ Bn.float().t() + beta * C0.float() + (bias.float() if with_bias else 0.0)
+    C = C0.clone()
+    pid, n = Kn._lt_plan(A, B, C, M, N, K, a_k, b_k, A.shape[-1], B.shape[-1], N, 1, 0, 0, 0, bias, beta,
+                         Kn.EPI_BIAS if with_bias else Kn.EPI_NONE, max_algos=64)
+    assert n > 0
+    for a in sorted({0, n // 2, n - 1}):
+        C.copy_(C0)
+        Kn._lt_run(pid, a, A, B, C, bias, 1.0, beta)
+        assert _rel(C, ref) < 1e-2, (a, ffC.lt_algo_name(pid, a))
+
+
+def test_hipblaslt_splitk_and_tuned_choice(ffC):
+    """Split-K strided-batched hipBLASLt GEMM into fp32 slabs + slab_sum (weight-gradient form), and
+    gemm()'s autotuner with the hipBLASLt candidates enabled on a BERT-shaped wgrad."""
+    from flexflow_amd import kernels as Kn
+    g = torch.Generator(device=DEV).manual_seed(1)
+    M, N, Kd, S = 1024, 768, 8192, 4
+    A = torch.randn(Kd, M, device=DEV, generator=g).bfloat16()   # dz^T layout: a_k = False
+    B = torch.randn(Kd, N, device=DEV, generator=g).bfloat16()   # x layout: b_k = False
+    C0 = torch.randn(M, N, device=DEV, generator=g)
+    ref = A.float().t() @ B.float() + C0
+    kc = Kd // S
+    slabs = torch.empty((S, M, N), device=DEV, dtype=torch.float32)
+    pid, n = Kn._lt_plan(A, B, slabs, M, N, kc, False, False, M, N, N, S, kc * M, kc * N, M * N, None, 0.0,
+                         Kn.EPI_NONE, max_algos=16)
+    assert n > 0
+    C = C0.clone()
+    Kn._lt_splitk(pid, 0, A, B, C, M, N, S, 1.0)
+    assert _rel(C, ref) < 2e-3
+    C = C0.clone()
+    Kn.gemm(A, B, C, M, N, Kd, False, False, M, N, N, beta=1.0)
+    assert _rel(C, ref) < 2e-3
