@@ -6,6 +6,7 @@
 #include "dataloader.h"
 #include "graph_utils.h"
 #include "pcg.h"
+#include "request_queue.h"
 
 namespace py = pybind11;
 using namespace ffcore;
@@ -280,4 +281,13 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("start_gpu_id", &MachineResource::start_gpu_id)
       .def("is_valid_machine_view", &MachineResource::is_valid_machine_view)
       .def("enumerate_views", &MachineResource::enumerate_views, py::arg("max_parts") = 0);
+  py::class_<RequestQueue>(m, "RequestQueue")
+      .def(py::init<int64_t, int64_t, std::vector<int64_t>>(), py::arg("max_rows"), py::arg("max_delay_us"),
+           py::arg("preferred") = std::vector<int64_t>{})
+      .def("push", &RequestQueue::push)
+      .def("pop", &RequestQueue::pop, py::arg("timeout_us") = -1, py::call_guard<py::gil_scoped_release>())
+      .def("close", &RequestQueue::close)
+      .def("queued_requests", &RequestQueue::queued_requests)
+      .def("queued_rows", &RequestQueue::queued_rows)
+      .def("stats", &RequestQueue::stats);
 }

@@ -77,6 +77,7 @@ class FFConfig:
         self.grad_bucket_mb = 64.0
         self.zero_optimizer = False   # --zero: ZeRO-1 sharded optimizer state / update on DP arenas
         self.seed = 1234
+        self.cpu_only = False  # -ll:gpu 0 / --device cpu: run on the host even with a GPU present
         self.trace_dir = ""
         self.check_nan_every = 0      # --check-nan N: loss finite-check every N steps (0 = off)
         self.watchdog_s = 0.0         # --watchdog S: dump all stacks if a step exceeds S seconds
@@ -141,8 +142,12 @@ class FFConfig:
                     self.enable_attribute_parallel = True
                 elif a == "-ll:gpu":
                     v = int(nxt())
-                    if "WORLD_SIZE" not in os.environ:
+                    if v == 0:  # the reference's CPU-only run (-ll:gpu 0)
+                        self.cpu_only = True
+                    elif "WORLD_SIZE" not in os.environ:
                         self.workers_per_node = v
+                elif a == "--device":
+                    self.cpu_only = nxt() == "cpu"
                 elif a == "-ll:fsize":
                     self.device_mem = float(nxt())
                 elif a == "--nodes":

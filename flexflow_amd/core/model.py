@@ -90,6 +90,7 @@ class FFModel:
         self._compiled = False
         self._output = None
         self._pending_values = {}
+        self._tensor_remap = {}  # guid -> replacement tensor (graph substitutions at compile)
         self.iter_config_seq_length = None
         self._recompile = None
         self._step_graph = None
@@ -634,8 +635,15 @@ class FFModel:
             return
         self.executor.feed(t, np.asarray(arr))
 
+    def resolve_tensor(self, t):
+        """The live tensor playing `t`'s role after compile-time graph substitutions (a fused
+        layer replaces the tensors of the layers it absorbed)."""
+        while t.guid in self._tensor_remap:
+            t = self._tensor_remap[t.guid]
+        return t
+
     def _get_tensor_value(self, t):
-        v = self.executor.get_value(t)
+        v = self.executor.get_value(self.resolve_tensor(t))
         return (v.float() if v.is_floating_point() else v).detach().cpu().numpy().copy()
 
     def _get_tensor_grad(self, t):

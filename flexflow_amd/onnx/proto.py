@@ -186,3 +186,62 @@ def input_shapes(model) -> Dict[str, list]:
     """Graph inputs that are not initializers -> declared shape."""
     inits = {t.name for t in model.graph.initializer}
     return {vi.name: vi.shape for vi in model.graph.input if vi.name not in inits}
+
+
+# ------------------------------------------------------------------------------- writer
+_NP_TO_ONNX = {"float32": 1, "uint8": 2, "int8": 3, "int32": 6, "int64": 7, "bool": 9, "float16": 10, "float64": 11}
+
+
+def _enc_tensor(name, arr) -> bytes:
+    import numpy as np
+    from ..utils.protowire import enc_bytes, enc_int
+    a = np.ascontiguousarray(arr)
+    out = b"".join(enc_int(1, d) for d in a.shape)
+    out += enc_int(2, _NP_TO_ONNX[str(a.dtype)]) + enc_bytes(8, name) + enc_bytes(9, a.tobytes())
+    return out
+
+
+def _enc_value_info(name, shape, elem=1) -> bytes:
+    from ..utils.protowire import enc_bytes, enc_int
+    dims = b"".join(enc_bytes(1, enc_int(1, d) if isinstance(d, int) and d >= 0 else enc_bytes(2, str(d)))
+                    for d in shape)
+    tensor_type = enc_int(1, elem) + enc_bytes(2, dims)
+    return enc_bytes(1, name) + enc_bytes(2, enc_bytes(1, tensor_type))
+
+
+def _enc_attr(name, v) -> bytes:
+    from ..utils.protowire import enc_bytes, enc_f32, enc_int
+    out = enc_bytes(1, name)
+    if isinstance(v, bool) or isinstance(v, int):
+        return out + enc_int(3, int(v)) + enc_int(20, 2)
+    if isinstance(v, float):
+        return out + enc_f32(2, v) + enc_int(20, 1)
+    if isinstance(v, (str, bytes)):
+        return out + enc_bytes(4, v) + enc_int(20, 3)
+    if isinstance(v, (list, tuple)) and all(isinstance(x, int) for x in v):
+        return out + b"".join(enc_int(8, x) for x in v) + enc_int(20, 7)
+    if isinstance(v, (list, tuple)):
+        return out + b"".join(enc_f32(7, x) for x in v) + enc_int(20, 6)
+    raise TypeError(f"attribute {name}: unsupported value {v!r}")
+
+
+def make_model_bytes(nodes, inputs, outputs, initializers=None, opset=13, name="graph") -> bytes:
+    """Serialize a small ONNX ModelProto (no onnx package needed): nodes = [(op_type, [in], [out],
+    {attr: value}), ...], inputs/outputs = {name: shape}, initializers = {name: ndarray}. Used to
+    build test models and model-repository fixtures."""
+    from ..utils.protowire import enc_bytes, enc_int
+    g = b""
+    for k, (op, ins, outs, attrs) in enumerate(nodes):
+        nb = b"".join(enc_bytes(1, i) for i in ins) + b"".join(enc_bytes(2, o) for o in outs)
+        nb += enc_bytes(3, f"{op}_{k}") + enc_bytes(4, op)
+        nb += b"".join(enc_bytes(5, _enc_attr(a, v)) for a, v in (attrs or {}).items())
+        g += enc_bytes(1, nb)
+    g += enc_bytes(2, name)
+    for n, a in (initializers or {}).items():
+        g += enc_bytes(5, _enc_tensor(n, a))
+    for n, shp in inputs.items():
+        g += enc_bytes(11, _enc_value_info(n, shp))
+    for n, shp in outputs.items():
+        g += enc_bytes(12, _enc_value_info(n, shp))
+    return enc_int(1, 7) + enc_bytes(2, "flexflow_amd") + enc_bytes(7, g) + enc_bytes(8, enc_bytes(1, "") +
+                                                                                     enc_int(2, opset))

@@ -18,7 +18,8 @@ import os
 import torch
 import torch.distributed as dist
 
-from .strategy import (OpConfig, data_parallel_strategy, load_strategy, load_strategy_pb, valid_config)
+from .strategy import (OpConfig, data_parallel_strategy, load_strategy, load_strategy_pb, load_strategy_text,
+                       valid_config)
 
 
 def _broadcast_strategy(model, strategy):
@@ -37,6 +38,8 @@ def choose_strategy(model):
     if cfg.import_strategy_file:
         if cfg.import_strategy_file.endswith(".pb"):  # the reference's protobuf strategy files
             strat = load_strategy_pb(cfg.import_strategy_file, layers, n)
+        elif cfg.import_strategy_file.endswith(".strategy"):  # the reference Triton backend's text form
+            strat = load_strategy_text(cfg.import_strategy_file, layers, n)
         else:
             strat, nd = load_strategy(cfg.import_strategy_file)
         missing = [L.name for L in layers if L.name not in strat]

@@ -249,6 +249,44 @@ def load_strategy_pb(path: str, layers, num_devices: int) -> Dict[str, OpConfig]
             elif f2 == 4:
                 devs += packed_varints(v2, wt2)
         table[name] = (dims, devs)
+    return _table_configs(table, layers, num_devices)
+
+
+def load_strategy_text(path: str, layers, num_devices: int) -> Dict[str, OpConfig]:
+    """The text strategy files of the reference's Triton backend (triton/src/strategy.cc
+    `PartitionStrategy::LoadStrategy`; e.g. triton/qa/L0_e2e/models/add/1/model.strategy):
+
+        <num_ops>
+        <op_name> <device_type 0=GPU|1=CPU> <ndims> <dim_{n-1}> ... <dim_0> <num_ids> <id> ...
+
+    The dims are listed outermost first (the loader fills dim[n-1] first). Same per-layer matching
+    and validation as the protobuf form."""
+    with open(path) as f:
+        tok = f.read().split()
+    pos = 0
+
+    def nxt():
+        nonlocal pos
+        pos += 1
+        return tok[pos - 1]
+
+    table = {}
+    for _ in range(int(nxt())):
+        name = nxt()
+        dev_type = int(nxt())
+        if dev_type not in (0, 1):
+            raise ValueError(f"{path}: unsupported device type {dev_type} for {name}")
+        nd = int(nxt())
+        outer_first = [int(nxt()) for _ in range(nd)]
+        nids = int(nxt())
+        ids = [int(nxt()) for _ in range(nids)]
+        if nids and nids != math.prod(outer_first):
+            raise ValueError(f"{path}: {name} lists {nids} devices for {math.prod(outer_first)} parts")
+        table[name] = (list(reversed(outer_first)), ids)  # Legion order, like the protobuf files
+    return _table_configs(table, layers, num_devices)
+
+
+def _table_configs(table, layers, num_devices: int) -> Dict[str, OpConfig]:
     out: Dict[str, OpConfig] = {}
     per_type: Dict[str, int] = {}
     for L in layers:

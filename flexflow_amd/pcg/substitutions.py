@@ -164,6 +164,8 @@ def apply_rule(model, rule, match) -> bool:
     kept = [L for L in layers if id(L) not in removed]
     for L in kept:
         L.inputs = [remap.get(t.guid, t) for t in L.inputs]
+    # tensors a user still holds (e.g. an ONNX graph output served by name) resolve through this
+    getattr(model, "_tensor_remap", {}).update(remap)
     if model._output is not None and model._output.guid in remap:
         model._output = remap[model._output.guid]
     # the final output tensor object changes: keep `output_tensor()` pointing at the same role

@@ -63,7 +63,7 @@ class WeightArena:
 
 
 def _device_for(config):
-    if torch.cuda.is_available():
+    if torch.cuda.is_available() and not getattr(config, "cpu_only", False):
         return torch.device("cuda", config.local_rank % max(1, torch.cuda.device_count()))
     return torch.device("cpu")
 
@@ -264,6 +264,9 @@ class Executor:
     def _setup_loss(self):
         self.loss_layout = None
         self.label_layout = None
+        self.softmax_fused = False  # inference-only models (no loss) keep plain softmax outputs
+        self._softmax_last_dim = False
+        self._fwd_training = self.training
         out = self.output_tensor
         if out is None or self.loss_type is None:
             return

@@ -60,3 +60,35 @@ def packed_f32(v, wt) -> List[float]:
     if wt == 5:
         return [struct.unpack("<f", v)[0]]
     return list(struct.unpack(f"<{len(v) // 4}f", v))
+
+
+# ------------------------------------------------------------------------------- encoding
+def enc_varint(v: int) -> bytes:
+    v &= (1 << 64) - 1  # negative int64 -> two's complement, 10 bytes
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def enc_key(field: int, wire_type: int) -> bytes:
+    return enc_varint((field << 3) | wire_type)
+
+
+def enc_int(field: int, v: int) -> bytes:
+    return enc_key(field, 0) + enc_varint(int(v))
+
+
+def enc_bytes(field: int, v) -> bytes:
+    b = v.encode() if isinstance(v, str) else bytes(v)
+    return enc_key(field, 2) + enc_varint(len(b)) + b
+
+
+def enc_f32(field: int, v: float) -> bytes:
+    import struct
+    return enc_key(field, 5) + struct.pack("<f", float(v))
