@@ -285,7 +285,59 @@ class ONNXModel:
 
 
 class ONNXModelKeras(ONNXModel):
-    """Models exported by keras2onnx (reference ONNXModelKeras): MatMul + Add pairs, Transpose."""
+    """Models exported by keras2onnx (reference ONNXModelKeras, python/flexflow/onnx/model.py):
+    a Dense layer arrives as MatMul(x, W[in, out]) followed by Add(., b); the pair becomes one
+    dense layer with bias (weights transposed into our [out, in] layout)."""
 
     def __init__(self, filename_or_model, ffconfig=None, ffmodel=None):
         super().__init__(filename_or_model)
+        self.ffconfig, self.ffmodel = ffconfig, ffmodel
+
+    def _dense_pairs(self):
+        nodes = list(self.model.graph.node)
+        users = {}
+        for n in nodes:
+            for i in n.input:
+                users.setdefault(i, []).append(n)
+        pairs = {}
+        for n in nodes:
+            if n.op_type != "MatMul" or n.input[1] not in self.inits or len(self._dims(n.input[1])) != 2:
+                continue
+            us = users.get(n.output[0], [])
+            if len(us) != 1 or us[0].op_type != "Add":
+                continue
+            add = us[0]
+            other = add.input[1] if add.input[0] == n.output[0] else add.input[0]
+            if other in self.inits and tuple(self._dims(other)) == (self._dims(n.input[1])[1],):
+                pairs[id(n)] = (add, other)
+        return pairs
+
+    def apply(self, ffmodel, input_dict):
+        pairs = self._dense_pairs()
+        skip = {id(a) for a, _ in pairs.values()}
+        self.symbol_table = dict(input_dict)
+        out = None
+        for n in self.model.graph.node:
+            if id(n) in skip:
+                continue
+            if id(n) in pairs:
+                add, bias = pairs[id(n)]
+                wd = self._dims(n.input[1])
+                res = ffmodel.dense(self.symbol_table[n.input[0]], wd[1], ActiMode.AC_MODE_NONE, True,
+                                    name=n.name or None)
+                L = ffmodel.get_last_layer()
+                self._layer_weights[L.name] = (list(L.weights), [n.input[1], bias, "__T__"])
+                self.symbol_table[add.output[0]] = res
+                out = res
+                continue
+            h = getattr(self, "handle" + n.op_type, None)
+            if h is None:
+                raise NotImplementedError(f"ONNX op {n.op_type} is not supported")
+            res = h(ffmodel, n)
+            if isinstance(res, (list, tuple)):
+                for name, r in zip(n.output, res):
+                    self.symbol_table[name] = r
+            else:
+                self.symbol_table[n.output[0]] = res
+            out = res
+        return out

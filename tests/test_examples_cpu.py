@@ -27,6 +27,11 @@ CASES = [
     ("keras/func_mnist_mlp_concat.py", ["--samples", "512"]),
     ("keras/seq_reuters_mlp.py", ["--samples", "1024"]),
     ("pytorch/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-a"]),
+    ("keras_exp/func_mnist_mlp.py", ["--samples", "2048", "-a"]),
+    ("keras_exp/func_mnist_mlp_concat.py", ["--samples", "256"]),
+    ("keras_exp/func_cifar10_cnn.py", ["--samples", "128"]),
+    ("keras_exp/func_cifar10_cnn_concat.py", ["--samples", "128"]),
+    ("keras_exp/func_cifar10_cnn_nested.py", ["--samples", "128"]),
 ]
 
 
