@@ -28,6 +28,12 @@ CASES = [
     ("keras/seq_reuters_mlp.py", ["--samples", "1024"]),
     ("pytorch/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-a"]),
     ("keras_exp/func_mnist_mlp.py", ["--samples", "2048", "-a"]),
+    ("onnx/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-b", "64", "-a"]),
+    ("onnx/mnist_mlp.py", ["--test_type", "0", "--samples", "1024", "-e", "2", "-b", "64", "-a"]),
+    ("onnx/cifar10_cnn.py", ["--samples", "128", "-b", "32"]),
+    ("onnx/cifar10_cnn.py", ["--test_type", "0", "--samples", "128", "-b", "32"]),
+    ("onnx/alexnet.py", ["--small", "--samples", "32", "-b", "16"]),
+    ("onnx/resnet.py", ["--small", "--samples", "32", "-b", "16"]),
     ("keras_exp/func_mnist_mlp_concat.py", ["--samples", "256"]),
     ("keras_exp/func_cifar10_cnn.py", ["--samples", "128"]),
     ("keras_exp/func_cifar10_cnn_concat.py", ["--samples", "128"]),
@@ -35,7 +41,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("script,args", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("script,args", CASES, ids=[f"{c[0]}:{i}" for i, c in enumerate(CASES)])
 def test_example_runs(script, args, tmp_path):
     env = dict(os.environ, FF_TUNABLEOP="off")
     r = subprocess.run([sys.executable, os.path.join(EX, script)] + args, cwd=tmp_path, env=env,
