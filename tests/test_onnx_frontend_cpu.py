@@ -82,7 +82,7 @@ def test_export_torch_roundtrip_matches_torch():
             return torch.softmax(self.fc(torch.flatten(self.gap(y), 1)), dim=1)
 
     torch.manual_seed(0)
-    m = Net().train()  # batch statistics, as FFModel's BatchNorm
+    m = Net().eval()
     x = torch.randn(4, 3, 16, 16)
     om = ONNXModel(export_torch(m, x))
     assert [n.op_type for n in om.model.graph.node] == ["Conv", "BatchNormalization", "Relu", "MaxPool", "Conv", "Add",
