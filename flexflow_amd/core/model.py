@@ -91,13 +91,22 @@ class FFModel:
         self._output = None
         self._pending_values = {}
         self._tensor_remap = {}  # guid -> replacement tensor (graph substitutions at compile)
+        self._names = set()
         self.iter_config_seq_length = None
         self._recompile = None
         self._step_graph = None
 
     # ================================================================== graph building
     def _add(self, op_type, inputs, name=None, **attrs):
+        if name is not None:  # layer names key the strategy and executor state: keep them unique
+            taken = self._names
+            if name in taken:
+                k = 1
+                while f"{name}_{k}" in taken:
+                    k += 1
+                name = f"{name}_{k}"
         L = Layer(self, op_type, name, inputs, attrs)
+        self._names.add(L.name)
         L.__class__ = op_class(op_type)  # reference per-op layer class (Linear, Conv2D, ...)
         self.layers.append(L)
         return L

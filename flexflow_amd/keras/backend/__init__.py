@@ -67,6 +67,61 @@ class BatchMatmul(Layer):
         return [self._track(ff, ff.batch_matmul(xs[0], xs[1]))]
 
 
+class Gather(Layer):
+    """torch.gather semantics along a non-batch `axis` (keras axes count the batch dim):
+    out[b, i, j] = x[b, idx[b, i, j], j] for axis 1 (reference keras/backend/internal.py gather)."""
+
+    def __init__(self, axis=1, **kw):
+        super().__init__(**kw)
+        self.axis = int(axis)
+
+    def compute_output_shape(self, in_shapes):
+        return [tuple(in_shapes[1])]
+
+    def output_dtypes(self, in_dtypes):
+        return [in_dtypes[0]]
+
+    def _lower(self, ff, xs):
+        ax = self.axis if self.axis >= 0 else len(xs[0].dims) + self.axis
+        return [self._track(ff, ff.gather(xs[0], xs[1], ax))]
+
+
+def gather(x, index, axis=1):
+    return Gather(axis)([x, index])
+
+
+def backend():
+    return "flexflow_amd"
+
+
+_IMAGE_DATA_FORMAT = ["channels_first"]
+
+
+def image_data_format():
+    return _IMAGE_DATA_FORMAT[0]
+
+
+def set_image_data_format(fmt):
+    if fmt != "channels_first":
+        raise NotImplementedError("only channels_first (NCHW) tensors, as the reference")
+    _IMAGE_DATA_FORMAT[0] = fmt
+
+
+def get_value(x):
+    """Weights of a layer / the value of a weight as numpy (tensors are symbolic until compiled)."""
+    import numpy as np
+    if hasattr(x, "get_weights"):
+        return x.get_weights()
+    return np.asarray(x)
+
+
+def set_value(x, value):
+    if hasattr(x, "set_weights"):
+        x.set_weights(value if isinstance(value, (list, tuple)) else [value])
+        return
+    raise TypeError("set_value: expects a layer")
+
+
 def batch_dot(x, y):
     return BatchMatmul()([x, y])
 

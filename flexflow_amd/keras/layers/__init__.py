@@ -53,6 +53,19 @@ class KTensor:
     def __repr__(self):
         return f"KTensor({self.name}, shape={self.batch_shape}, dtype={self.dtype.name})"
 
+    # elementwise arithmetic records merge layers (tf.keras-style `x + y`)
+    def __add__(self, other):
+        return Add()([self, other])
+
+    def __sub__(self, other):
+        return Subtract()([self, other])
+
+    def __mul__(self, other):
+        return Multiply()([self, other])
+
+    def __truediv__(self, other):
+        return Divide()([self, other])
+
 
 class Layer:
     """Base layer: __call__ records (inputs -> outputs); _lower builds FFModel ops."""
@@ -91,18 +104,35 @@ class Layer:
         self.ff_layers.append(ff.get_last_layer())
         return out
 
+    def _shared(self, ff):
+        """The FFModel layer this layer already lowered to in `ff` (a layer called twice shares its
+        weights, as in Keras); None on the first call."""
+        for L in self.ff_layers:
+            if L.model is ff:
+                return L
+        return None
+
     # ---- weights (after compile)
     def get_weights(self, ffmodel=None):
         import numpy as np
         if not self.ff_layers:
             return []
-        L = self.ff_layers[0]
         m = ffmodel or self._model.ffmodel
+        L = self._shared(m) or self.ff_layers[-1]
         return [np.asarray(w.get_weights(m)) for w in L.weights]
 
-    def set_weights(self, weights, ffmodel=None):
-        L = self.ff_layers[0]
+    def set_weights(self, *args, ffmodel=None):
+        """set_weights([kernel, bias], ffmodel=None) (Keras) or set_weights(ffmodel, kernel, bias)
+        (reference keras/layers/core.py:105)."""
+        from ...core.model import FFModel
+        if args and isinstance(args[0], FFModel):
+            ffmodel, weights = args[0], list(args[1:])
+        else:
+            weights = list(args[0]) if args else []
+            if len(args) > 1:
+                ffmodel = args[1]
         m = ffmodel or self._model.ffmodel
+        L = self._shared(m) or self.ff_layers[-1]
         for w, v in zip(L.weights, weights):
             w.set_weights(m, v)
 
@@ -151,7 +181,7 @@ class Dense(Layer):
         return [in_shapes[0][:-1] + (self.units,)]
 
     def _lower(self, ff, xs):
-        t = ff.dense(xs[0], self.units, self.activation, self.use_bias,
+        t = ff.dense(xs[0], self.units, self.activation, self.use_bias, shared_op=self._shared(ff),
                      kernel_initializer=self.kernel_initializer.ff() if self.kernel_initializer else None,
                      bias_initializer=self.bias_initializer.ff() if self.bias_initializer else None,
                      kernel_regularizer=self.kernel_regularizer, name=self.name)
@@ -289,7 +319,7 @@ class Conv2D(Layer):
     def _lower(self, ff, xs):
         t = ff.conv2d(xs[0], self.filters, self.kernel[0], self.kernel[1], self.strides[0], self.strides[1],
                       self.pads[0], self.pads[1], self.activation, self.groups, self.use_bias,
-                      kernel_initializer=self.kernel_initializer.ff() if self.kernel_initializer else None,
+                      shared_op=self._shared(ff), kernel_initializer=self.kernel_initializer.ff() if self.kernel_initializer else None,
                       bias_initializer=self.bias_initializer.ff() if self.bias_initializer else None, name=self.name)
         return [self._track(ff, t)]
 
@@ -367,6 +397,10 @@ class Concatenate(_Merge):
 class _Binary(_Merge):
     fn = "add"
 
+    def compute_output_shape(self, in_shapes):
+        import numpy as np
+        return [tuple(np.broadcast_shapes(*[tuple(s) for s in in_shapes]))]
+
     def _lower(self, ff, xs):
         t = xs[0]
         for y in xs[1:]:
@@ -385,6 +419,10 @@ class Subtract(_Binary):
 
 class Multiply(_Binary):
     fn = "multiply"
+
+
+class Divide(_Binary):
+    fn = "divide"
 
 
 class Maximum(_Binary):

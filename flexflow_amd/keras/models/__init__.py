@@ -41,7 +41,8 @@ class Model(Layer):
     # ---------------------------------------------------------------- properties
     @property
     def input(self):
-        return self._inputs if len(self._inputs) != 1 else self._inputs[0]
+        """The model's input tensors, always a list (reference keras/models/base_model.py:66)."""
+        return list(self._inputs)
 
     @property
     def output(self):

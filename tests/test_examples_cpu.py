@@ -26,6 +26,32 @@ CASES = [
     ("keras/seq_mnist_mlp.py", ["--samples", "1024", "-a"]),
     ("keras/func_mnist_mlp_concat.py", ["--samples", "512"]),
     ("keras/seq_reuters_mlp.py", ["--samples", "1024"]),
+    ("keras/gather.py", []),
+    ("keras/identity_loss.py", []),
+    ("keras/reduce_sum.py", []),
+    ("keras/rsqrt.py", []),
+    ("keras/unary.py", []),
+    ("keras/elementwise_mul_broadcast.py", []),
+    ("keras/elementwise_max_min.py", []),
+    ("keras/regularizer.py", []),
+    ("keras/reshape.py", ["--samples", "256"]),
+    ("keras/callback.py", ["--samples", "128"]),
+    ("keras/func_mnist_mlp.py", ["--samples", "2048", "-a"]),
+    ("keras/func_mnist_mlp_concat2.py", ["--samples", "128"]),
+    ("keras/func_mnist_cnn.py", ["--samples", "128"]),
+    ("keras/func_mnist_cnn_concat.py", ["--samples", "128"]),
+    ("keras/seq_mnist_cnn.py", ["--samples", "128"]),
+    ("keras/seq_mnist_cnn_nested.py", ["--samples", "128"]),
+    ("keras/seq_cifar10_cnn.py", ["--samples", "128"]),
+    ("keras/func_cifar10_cnn_nested.py", ["--samples", "128"]),
+    ("keras/func_cifar10_cnn_concat_model.py", ["--samples", "128"]),
+    ("keras/func_cifar10_cnn_concat_seq_model.py", ["--samples", "128"]),
+    ("keras/func_cifar10_alexnet.py", ["--small", "--samples", "64"]),
+    ("keras/func_mnist_mlp_net2net.py", ["--samples", "256"]),
+    ("keras/seq_mnist_mlp_net2net.py", ["--samples", "256"]),
+    ("keras/seq_mnist_cnn_net2net.py", ["--samples", "128"]),
+    ("keras/func_cifar10_cnn_net2net.py", ["--samples", "128"]),
+    ("keras/candle_uno/candle_uno.py", ["--small", "--samples", "256"]),
     ("pytorch/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-a"]),
     ("keras_exp/func_mnist_mlp.py", ["--samples", "2048", "-a"]),
     ("onnx/mnist_mlp.py", ["--samples", "1024", "-e", "2", "-b", "64", "-a"]),

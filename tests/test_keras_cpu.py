@@ -99,3 +99,26 @@ def test_cifar_shapes_and_errors():
     assert x.shape == (64, 3, 32, 32) and y.shape == (64, 1) and x.dtype == np.uint8
     with pytest.raises(ValueError):
         Sequential([layers.Dense(4)])  # first layer without input shape
+
+
+def test_keras_shared_layer_and_submodel_reuse():
+    """A layer (or nested model) called on two inputs lowers to two FFModel ops that SHARE weights
+    (Keras semantics, FFModel shared_op), with unique op names; training runs through both uses."""
+    import numpy as np
+    from flexflow_amd.keras import optimizers
+    from flexflow_amd.keras.layers import Concatenate, Dense, Input
+    from flexflow_amd.keras.models import Model
+    from flexflow_amd.type import OperatorType
+    sub_in = Input(shape=(6,))
+    enc = Model(sub_in, Dense(4, activation="relu", name="enc_dense")(sub_in))
+    a, b = Input(shape=(6,)), Input(shape=(6,))
+    out = Dense(1, name="head")(Concatenate(axis=1)([enc(a), enc(b)]))
+    model = Model([a, b], out)
+    model.compile(optimizer=optimizers.SGD(learning_rate=0.01), loss="mean_squared_error",
+                  metrics=["mean_squared_error"], batch_size=8)
+    lin = [L for L in model.ffmodel.layers if L.op_type == OperatorType.OP_LINEAR and L.name.startswith("enc_dense")]
+    assert len(lin) == 2 and len({L.name for L in lin}) == 2
+    assert [w.guid for w in lin[0].weights] == [w.guid for w in lin[1].weights]
+    x = np.random.default_rng(0).standard_normal((32, 6)).astype(np.float32)
+    hist = model.fit([x, x[::-1].copy()], x[:, :1].copy(), epochs=2)
+    assert np.isfinite(hist.history["loss"][-1])
