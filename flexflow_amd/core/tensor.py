@@ -88,6 +88,14 @@ class Tensor:
         self.mapped = False
 
     def get_array(self, ffmodel, ffconfig=None):
+        """The tensor's values as numpy. Before compile (or when called with an FFConfig, as the
+        reference's `get_array(ffconfig, dtype)` after `inline_map`) this is the host array the
+        tensor is attached to — writable, and fed to the model at compile."""
+        if not getattr(ffmodel, "_compiled", False):
+            if self._attached is None:
+                self._attached = np.zeros(tuple(self.dims), dtype=np.int32 if self.data_type in (
+                    DataType.DT_INT32, DataType.DT_INT64) else np.float32)
+            return self._attached
         return self.get_tensor(ffmodel)
 
     def get_flat_array(self, ffmodel, ffconfig=None):

@@ -23,6 +23,19 @@ CASES = [
     ("native/dlrm.py", ["-b", "16", "--iterations", "2", "--small"]),
     ("native/transformer.py", ["-b", "2", "--iterations", "1", "--small"]),
     ("native/mixture_of_experts.py", ["-b", "16", "--iterations", "2", "--small"]),
+    ("native/tensor_attach.py", []),
+    ("native/print_input.py", ["-b", "4"]),
+    ("native/print_weight.py", ["-b", "16"]),
+    ("native/split.py", ["-b", "32", "--samples", "64"]),
+    ("native/demo_gather.py", ["-b", "4"]),
+    ("native/mnist_mlp_attach.py", ["-b", "64", "--samples", "2048", "-e", "2", "-a"]),
+    ("native/cifar10_cnn_attach.py", ["-b", "32", "--samples", "64"]),
+    ("pytorch/cifar10_cnn.py", ["-b", "32", "--samples", "64"]),
+    ("pytorch/resnet.py", ["--small", "-b", "8", "--samples", "16"]),
+    ("pytorch/torch_vision.py", ["--small", "-b", "8", "--samples", "16"]),
+    ("pytorch/regnet.py", ["--small", "-b", "8", "--samples", "16"]),
+    ("pytorch/mnist_mlp_torch2.py", ["-b", "64", "--samples", "2048", "-e", "2", "-a"]),
+    ("pytorch/resnet152_training.py", ["--small"]),
     ("keras/seq_mnist_mlp.py", ["--samples", "1024", "-a"]),
     ("keras/func_mnist_mlp_concat.py", ["--samples", "512"]),
     ("keras/seq_reuters_mlp.py", ["--samples", "1024"]),
