@@ -143,12 +143,15 @@ void layernorm_fwd(Tensor x, optional<Tensor> res, optional<Tensor> sum_out, opt
 }
 void layernorm_bwd(Tensor dy, Tensor x, optional<Tensor> gamma, Tensor mean, Tensor rstd, Tensor dx,
                    optional<Tensor> dres, optional<Tensor> dgamma, optional<Tensor> dbeta, int64_t rows,
-                   int64_t cols, bool acc) {
+                   int64_t cols, bool acc, optional<Tensor> dsum) {
   TORCH_CHECK(dy.numel() == rows * cols && dx.numel() == rows * cols);
-  Tensor ws = at::empty({2 * (int64_t)ffk::layernorm_bwd_waves(rows) * cols}, dy.options().dtype(at::kFloat));
+  TORCH_CHECK(!dsum || (dsum->scalar_type() == at::kFloat && dsum->numel() >= cols), "layernorm_bwd: dsum");
+  const int64_t nw = ffk::layernorm_bwd_waves(rows);
+  Tensor ws = at::empty({3 * nw * cols + ffk::bias_act_bwd_chunks(rows, cols) * cols},
+                        dy.options().dtype(at::kFloat));
   ffk::layernorm_bwd(dtcode(dy), dy.data_ptr(), x.data_ptr(), ptr(gamma), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dx.data_ptr(), ptr(dres), ptr<float>(dgamma), ptr<float>(dbeta),
-                     ws.data_ptr<float>(), rows, cols, acc, cur_stream());
+                     ptr<float>(dsum), ws.data_ptr<float>(), rows, cols, acc, cur_stream());
 }
 void softmax_fwd(Tensor x, Tensor y, int64_t rows, int64_t cols, double scale) {
   TORCH_CHECK(x.numel() == rows * cols);
@@ -320,7 +323,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("rows"),
+        py::arg("cols"), py::arg("acc"), py::arg("dsum") = py::none());
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
   m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("loss"), py::arg("dlogits"),

@@ -313,13 +313,16 @@ __global__ void __launch_bounds__(256) bias_act_bwd_kernel(const T* __restrict__
   }
 }
 
-// out_z[c] += sum_{r < R} part[z*R*C + r*C + c] for z < gridDim.z (LN folds dgamma and dbeta in one
-// launch). Block = 64 columns x 4 row lanes; gridDim.y row chunks (<= 32 adders per address).
-__global__ void col_reduce_add_kernel(const float* __restrict__ part, float* __restrict__ out0,
-                                      float* __restrict__ out1, int R, int C) {
+// out_k[c] += sum_{r < R} part[k*R*C + r*C + c] for the non-null outputs k < 3 (LN folds dgamma,
+// dbeta and the fused bias-gradient colsum in one launch; gridDim.z = number of non-null outputs,
+// mapped to their slab index through `which`). Block = 64 columns x 4 row lanes; gridDim.y row
+// chunks (<= 32 adders per address).
+struct Outs3 { float* p[3]; int which[3]; };
+__global__ void col_reduce_add_kernel(const float* __restrict__ part, Outs3 o, int R, int C) {
   __shared__ float red[4][64];
-  const float* p = part + (int64_t)blockIdx.z * R * C;
-  float* out = blockIdx.z ? out1 : out0;
+  const int k = o.which[blockIdx.z];
+  const float* p = part + (int64_t)k * R * C;
+  float* out = o.p[k];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
   const int per = (R + gridDim.y - 1) / gridDim.y;
@@ -335,11 +338,18 @@ __global__ void col_reduce_add_kernel(const float* __restrict__ part, float* __r
   }
 }
 
-void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st) {
+void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st) {
   if (R == 0 || C == 0) return;
+  Outs3 o{{out0, out1, out2}, {0, 0, 0}};
+  int nz = 0;
+  for (int k = 0; k < 3; ++k)
+    if (o.p[k]) o.which[nz++] = k;
+  if (!nz) return;
   const int gy = std::max(1, std::min(32, R / 8));
-  hipLaunchKernelGGL(col_reduce_add_kernel, dim3((C + 63) / 64, gy, out1 ? 2 : 1), dim3(256), 0, st, part, out0,
-                     out1, R, C);
+  hipLaunchKernelGGL(col_reduce_add_kernel, dim3((C + 63) / 64, gy, nz), dim3(256), 0, st, part, o, R, C);
+}
+void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st) {
+  col_reduce_add3(part, out0, out1, nullptr, R, C, st);
 }
 void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st) {
   col_reduce_add2(part, out, nullptr, R, C, st);

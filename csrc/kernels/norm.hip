@@ -108,16 +108,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const T* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                      const T* __restrict__ dres_in, float* __restrict__ pgam,
-                                                     float* __restrict__ pbet, int rows, int cols, int accumulate) {
+                                                     float* __restrict__ pbet, float* __restrict__ pdx, int rows,
+                                                     int cols, int accumulate) {
   constexpr int V = 16 / sizeof(T);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  float pg[NCH][V], pb[NCH][V];
+  float pg[NCH][V], pb[NCH][V], pd[NCH][V];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int j = 0; j < V; ++j) { pg[c][j] = 0.f; pb[c][j] = 0.f; }
+    for (int j = 0; j < V; ++j) { pg[c][j] = 0.f; pb[c][j] = 0.f; pd[c][j] = 0.f; }
   for (int row = wave; row < rows; row += nwaves) {
     const int64_t base = (int64_t)row * cols;
     const float mean = mean_in[row], rstd = rstd_in[row];
@@ -166,6 +167,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
           for (int j = 0; j < V; ++j) o[j] += r[j];
         }
+        // colsum of the input gradient: the bias gradient of the Linear producing this input,
+        // fused here instead of a separate pass over the same [rows, cols] tensor
+#pragma unroll
+        for (int j = 0; j < V; ++j) pd[c][j] += o[j];
         store16(dx + base + col, o);
       }
     }
@@ -175,15 +180,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
   extern __shared__ float lds_red[];
   const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    float* slab = pass ? pbet : pgam;
+  for (int pass = 0; pass < 3; ++pass) {
+    float* slab = pass == 2 ? pdx : (pass ? pbet : pgam);
     if (!slab) continue;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * 64 + lane) * V;
       if (col < cols)
 #pragma unroll
-        for (int j = 0; j < V; ++j) lds_red[w * cols + col + j] = pass ? pb[c][j] : pg[c][j];
+        for (int j = 0; j < V; ++j) lds_red[w * cols + col + j] = pass == 2 ? pd[c][j] : (pass ? pb[c][j] : pg[c][j]);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < cols; k += 256)
@@ -258,8 +263,8 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 int layernorm_bwd_waves(int rows) { return std::max(1, std::min((rows + 15) / 16, 1024)); }  // slab rows = blocks
 
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
-                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
-                   int accumulate, hipStream_t st) {
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* dsum, float* ws, int rows,
+                   int cols, int accumulate, hipStream_t st) {
   if (rows == 0) return;
   const int esz = dt == DT_BF16 ? 2 : 4;
   const int V = 16 / esz;
@@ -269,11 +274,14 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   // ~4 rows per wave: enough waves in flight to cover HBM latency, slab partials stay small
   const int blocks = std::max(1, std::min((rows + 15) / 16, 1024));
   const int nw = blocks;
+  // slab layout: [dgamma | dbeta | dsum] partials, nw rows each (absent ones skipped)
   float* pg = dgamma ? ws : nullptr;
   float* pb = dbeta ? ws + (int64_t)nw * cols : nullptr;
+  float* pd = dsum ? ws + 2 * (int64_t)nw * cols : nullptr;
   bool used_slab = false;
+  const bool fused_ok = vec && nch <= 4;
 #define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 4 * cols * sizeof(float), st, (const T*)dy, (const T*)x, \
-                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, rows, cols, accumulate); } while (0)
+                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, pd, rows, cols, accumulate); } while (0)
   if (dt == DT_BF16) {
     using T = bf16_t;
     if (vec && nch <= 1) LNB(T, 1); else if (vec && nch <= 2) LNB(T, 2); else if (vec && nch <= 4) LNB(T, 4);
@@ -287,10 +295,12 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   }
 #undef LNB
   if (used_slab) {
-    if (dgamma && dbeta) col_reduce_add2(pg, dgamma, dbeta, nw, cols, st);  // pb = pg + nw * cols
-    else if (dgamma) col_reduce_add(pg, dgamma, nw, cols, st);
-    else if (dbeta) col_reduce_add(pb, dbeta, nw, cols, st);
+    col_reduce_add3(ws, dgamma, dbeta, dsum, nw, cols, st);
+  } else if (dsum) {
+    // generic path (unaligned / very wide rows): the colsum as its own pass over the written dx
+    bias_act_bwd(dt, dx, nullptr, nullptr, dsum, ws + 2 * (int64_t)nw * cols, rows, cols, ACT_NONE, st);
   }
+  (void)fused_ok;
 }
 
 }  // namespace ffk

@@ -40,14 +40,17 @@ void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st)
 void slab_sum(const float* slabs, float* out, int64_t n, int S, float beta, hipStream_t st);
 // out0 += colsum(part[0:R]); out1 += colsum(part[R:2R]) (out1 may be null)
 void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st);
+// out_k += colsum(part[k*R:(k+1)*R]) for each non-null out_k, k < 3 (slab k at offset k*R*C)
+void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st);
 
 // norm.hip
 void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st);
-// ws: fp32 slab of 2 * layernorm_bwd_waves(rows) * cols floats (dgamma / dbeta partials)
+// ws: fp32 slab of 3 * layernorm_bwd_waves(rows) * cols floats (dgamma / dbeta / dsum partials).
+// dsum (optional) += colsum(dx): the bias gradient of the Linear that produced the LN input.
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
-                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* ws, int rows, int cols,
-                   int accumulate, hipStream_t st);
+                   void* dx, const void* dres_in, float* dgamma, float* dbeta, float* dsum, float* ws, int rows,
+                   int cols, int accumulate, hipStream_t st);
 int layernorm_bwd_waves(int rows);
 
 // softmax.hip

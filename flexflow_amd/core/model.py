@@ -434,6 +434,7 @@ class FFModel:
         self.executor.init_weights(cfg.seed)
         if os.environ.get("FF_NO_INPLACE") != "1":
             self.executor._plan_inplace()
+        self.executor._plan_bias_grad_fusion()
         if self.optimizer is not None and training:
             self.executor.init_optimizer(self.optimizer)
         for guid, v in self._pending_values.items():

@@ -551,11 +551,13 @@ def layernorm_fwd(x2d, res2d, gamma, beta, eps, save_sum):
     return y.to(x2d.dtype), xs.to(x2d.dtype), mean, rstd
 
 
-def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None):
+def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None, dsum=None):
+    """dx of LayerNorm; dgamma/dbeta += their column sums; dsum (fp32 [cols]) += colsum(dx), the bias
+    gradient of the Linear feeding this LayerNorm, computed in the same pass."""
     rows, cols = dy2d.shape
     if native(dy2d):
         dx = torch.empty_like(dy2d)
-        ext().layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False)
+        ext().layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False, dsum)
         return dx
     xh = (xs2d.float() - mean[:, None]) * rstd[:, None]
     dy = dy2d.float()
@@ -569,7 +571,10 @@ def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None):
         dgamma.add_((dy * xh).sum(0))
     if dbeta is not None:
         dbeta.add_(dy.sum(0))
-    return dx.to(dy2d.dtype)
+    dxo = dx.to(dy2d.dtype)
+    if dsum is not None:
+        dsum.add_(dxo.float().sum(0))
+    return dxo
 
 
 # ----------------------------------------------------------------------------- softmax/loss

@@ -168,7 +168,7 @@ class MultiHeadAttention(OpImpl):
         o = s["o"]
         o2 = o.view(B * Sq, Hl * vd)
         dwo = gw("o_weight")
-        dbo = gw("o_bias") if s["has_bo"] else None
+        dbo = gw("o_bias") if (s["has_bo"] and not ctx.extra.get("bias_grad_fused")) else None
         wb = 0.0 if ctx.extra.get("wgrad_overwrite") else 1.0
         do2 = K.linear_bwd(dy2, o2, s["wo"], None, K.ACT_NONE,
                            dwo.view(E, Hl * vd) if dwo is not None else None, dbo, dw_beta=wb)

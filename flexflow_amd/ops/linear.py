@@ -88,6 +88,8 @@ class Linear(OpImpl):
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         dw = ctx.wgrads[0] if ctx.wgrads else None
         db = ctx.wgrads[1] if (len(ctx.wgrads) > 1 and ctx.saved["has_b"]) else None
+        if ctx.extra.get("bias_grad_fused"):  # the consuming LayerNorm's backward already summed it
+            db = None
         acc = (ctx.extra.get("dx_accum") or {}).get(0)
         dx = K.linear_bwd(dy2, x2, w, z, self.act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
                           dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0,

@@ -75,7 +75,10 @@ class LayerNorm(OpImpl):
         x2 = s.pop("x")
         dg = ctx.wgrads[0].reshape(-1) if ctx.wgrads else None
         db = ctx.wgrads[1].reshape(-1) if ctx.wgrads else None
-        dx = K.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, s.pop("g"), s.pop("mean"), s.pop("rstd"), dg, db)
+        # fused bias gradient of the Linear that produced an input (executor pass fuse_bias_grads)
+        dsum = ctx.extra.get("colsum_out")
+        dx = K.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, s.pop("g"), s.pop("mean"), s.pop("rstd"), dg, db,
+                             dsum=dsum)
         dx = dx.reshape(dy.shape)
         return [dx, dx] if len(self.layer.inputs) > 1 else [dx]
 

@@ -532,6 +532,47 @@ class Executor:
             n += 1
         return n
 
+    def _plan_bias_grad_fusion(self):
+        """Cross-op fusion for the backward: a LayerNorm whose input comes straight (same layout,
+        sole consumer) from a Linear without activation — or the output projection of a
+        multi-head attention — computes that producer's bias gradient, colsum(dx), inside its own
+        backward kernel (ops/norm.py -> csrc/kernels/norm.hip ln_bwd_kernel). The producer then
+        skips its separate column-reduction pass over the same [tokens, hidden] gradient (BERT:
+        the out-projection and FFN2 biases of every layer)."""
+        if not self.training or os.environ.get("FF_NO_BIAS_FUSION") == "1":
+            return 0
+        consumers = {}
+        for L in self.layers:
+            for t in L.inputs:
+                consumers[t.guid] = consumers.get(t.guid, 0) + 1
+        prod = {o.guid: L for L in self.layers for o in L.outputs}
+        out_guid = self.output_tensor.guid if self.output_tensor is not None else None
+        n = 0
+        for L in self.layers:
+            if L.op_type != OperatorType.OP_LAYERNORM or L.name not in self.ctx or not self.layer_bwd.get(L.name):
+                continue
+            for j, t in enumerate(L.inputs):
+                P = prod.get(t.guid)
+                if P is None or P.name not in self.ctx or consumers.get(t.guid, 0) != 1 or t.guid == out_guid:
+                    continue
+                if not self.in_grad.get((L.name, j)) or self.fwd_tx[(L.name, j)].kind != "identity":
+                    continue
+                pctx = self.ctx[P.name]
+                db = None
+                if P.op_type == OperatorType.OP_LINEAR and P.impl.act == K.ACT_NONE and len(P.weights) > 1:
+                    db = pctx.wgrads[1] if pctx.wgrads and len(pctx.wgrads) > 1 else None
+                elif P.op_type == OperatorType.OP_MULTIHEAD_ATTENTION:
+                    gi = P.impl._grad_index()
+                    if "o_bias" in gi and pctx.wgrads:
+                        db = pctx.wgrads[gi["o_bias"]]
+                if db is None or db.dtype != torch.float32 or db.numel() != t.dims[-1]:
+                    continue
+                self.ctx[L.name].extra["colsum_out"] = db.reshape(-1)
+                pctx.extra["bias_grad_fused"] = True
+                n += 1
+                break
+        return n
+
     def _hooked(self, L, phase):
         """Nest every attached hook's op(L, phase) context (profiler, non-finite guard)."""
         from contextlib import ExitStack

@@ -217,6 +217,14 @@ def test_layernorm(ffC, cols, rows):
     assert _rel(dx, xs.grad) < 2e-2
     assert _rel(dg, gf.grad) < 2e-2
     assert _rel(db, bf.grad) < 1e-2
+    # fused bias gradient of the producing Linear: dsum += colsum(dx), same launch (plus dgamma/dbeta
+    # accumulate again on top of the first call's values)
+    dsum = torch.full((cols,), 0.5, device=DEV)
+    dx2 = torch.empty_like(x)
+    ffC.layernorm_bwd(dy, s, g, mean, rstd, dx2, None, dg, db, rows, cols, False, dsum)
+    assert torch.equal(dx2, dx)
+    assert _rel(dsum - 0.5, dx.float().sum(0)) < 5e-3  # kernel sums the fp32 values before bf16 rounding
+    assert _rel(db, 2 * bf.grad) < 1e-2
 
 
 def test_softmax_and_xent(ffC):

@@ -47,3 +47,39 @@ def test_big_cnn_builds_and_steps(name):
 def test_loss_decreases(name):
     losses = _run(name, steps=5, batch=4, lr=0.05)
     assert losses[-1] < losses[0], losses
+
+
+def test_bias_grad_fusion_into_layernorm_matches_unfused(monkeypatch):
+    """The out-projection and FFN2 bias gradients summed inside the following LayerNorm's backward
+    (executor._plan_bias_grad_fusion) train exactly like the separate column-reduction pass."""
+    import numpy as np
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(fused):
+        if fused:
+            monkeypatch.delenv("FF_NO_BIAS_FUSION", raising=False)
+        else:
+            monkeypatch.setenv("FF_NO_BIAS_FUSION", "1")
+        cfg = FFConfig(["--device", "cpu"])
+        bc = BertConfig.tiny(16)
+        cfg.batch_size = 2
+        ff = FFModel(cfg)
+        ids, pos, _ = build_bert(ff, 2, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        n = sum(1 for c in ff.executor.ctx.values() if c.extra.get("bias_grad_fused"))
+        rng = np.random.default_rng(0)
+        ids.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(16, dtype=np.int32), (2, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16, 1), dtype=np.int32))
+        for _ in range(2):
+            ff.train_step()
+        ws = {f"{L.name}.{i}": np.asarray(w.get_weights(ff)) for L in ff.layers for i, w in enumerate(L.weights)}
+        return n, ws
+
+    n1, a = run(True)
+    n0, b = run(False)
+    assert n0 == 0 and n1 == 2 * BertConfig.tiny(16).layers  # out-proj + FFN2 of every layer
+    for k in a:
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6, err_msg=k)
