@@ -296,6 +296,27 @@ int64_t lt_run(int64_t plan, int64_t algo, Tensor A, Tensor B, Tensor C, optiona
                       (float)beta, ptr(ws), wsb, cur_stream());
 }
 
+
+// ---- LSTM step (rnn.hip); tensors may be strided views: pointers + explicit row strides
+void lstm_fwd_cell(Tensor G, int64_t ldg, Tensor c_prev, Tensor c_out, Tensor h_out, int64_t ldh, int64_t B,
+                   int64_t H) {
+  check_dev(G, "G");
+  TORCH_CHECK(c_prev.scalar_type() == at::kFloat && c_out.scalar_type() == at::kFloat, "lstm: c must be fp32");
+  TORCH_CHECK(c_prev.numel() >= B * H && c_out.numel() >= B * H, "lstm: c too small");
+  TORCH_CHECK(G.scalar_type() == h_out.scalar_type(), "lstm: G / h dtype");
+  ffk::lstm_fwd_cell(dtcode(G), G.data_ptr(), ldg, c_prev.data_ptr<float>(), c_out.data_ptr<float>(), h_out.data_ptr(),
+                     ldh, B, H, cur_stream());
+}
+void lstm_bwd_cell(Tensor G, int64_t ldg, Tensor c, Tensor c_prev, optional<Tensor> dy, int64_t lddy,
+                   optional<Tensor> dh_rec, Tensor dc, Tensor dG, int64_t B, int64_t H) {
+  check_dev(G, "G");
+  TORCH_CHECK(c.scalar_type() == at::kFloat && c_prev.scalar_type() == at::kFloat && dc.scalar_type() == at::kFloat,
+              "lstm: c / dc must be fp32");
+  TORCH_CHECK(dc.numel() >= B * H && c.numel() >= B * H && c_prev.numel() >= B * H, "lstm: state too small");
+  ffk::lstm_bwd_cell(dtcode(G), G.data_ptr(), ldg, c.data_ptr<float>(), c_prev.data_ptr<float>(), ptr(dy), lddy,
+                     ptr(dh_rec), dc.data_ptr<float>(), dG.data_ptr(), B, H, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -304,6 +325,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
         py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2);
+  m.def("lstm_fwd_cell", &lstm_fwd_cell);
+  m.def("lstm_bwd_cell", &lstm_bwd_cell);
   m.def("lt_plan", &lt_plan);
   m.def("lt_run", &lt_run);
   m.def("lt_num_algos", [](int64_t p) { return ffk::lt::num_algos(p); });

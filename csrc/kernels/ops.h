@@ -97,4 +97,10 @@ void reduce_rows(int dt, const void* x, void* y, int64_t outer, int64_t red, int
 void metrics_classify(int dt, const void* probs, const int* labels, int rows, int cols, float* out /*[3]*/,
                       hipStream_t st);
 
+// rnn.hip: pointwise LSTM step (gate order i, f, g, o; G rows of stride ldg; c in fp32)
+void lstm_fwd_cell(int dt, void* G, int64_t ldg, const float* c_prev, float* c_out, void* h_out, int64_t ldh, int B,
+                   int H, hipStream_t st);
+void lstm_bwd_cell(int dt, const void* G, int64_t ldg, const float* c, const float* c_prev, const void* dy,
+                   int64_t lddy, const void* dh_rec, float* dc, void* dG, int B, int H, hipStream_t st);
+
 }  // namespace ffk

@@ -124,6 +124,18 @@ class FFModel:
         t.create_grad = create_grad
         return t
 
+    def lstm(self, input, hidden_size, hx=None, cx=None, kernel_initializer=None, name=None):
+        """LSTM over input [B, L, E] -> (y [B, L, H], hy [B, H], cy [B, H]); hx / cx default to
+        zeros (ops/rnn.py; the reference's LSTM lives in its separate nmt/ application)."""
+        B = input.dims[0]
+        if hx is None:
+            hx = self.create_constant([B, hidden_size], 0.0)
+        if cx is None:
+            cx = self.create_constant([B, hidden_size], 0.0)
+        L = self._add(OperatorType.OP_LSTM, [input, hx, cx], name, hidden_size=int(hidden_size),
+                      kernel_init=kernel_initializer)
+        return tuple(L.outputs)
+
     def create_constant(self, dims, value, data_type=DataType.DT_FLOAT):
         t = self.create_tensor(dims, data_type, False)
         self._pending_values[t.guid] = np.full(dims, value, dtype=np.float32 if data_type == DataType.DT_FLOAT else np.int32)

@@ -799,6 +799,44 @@ def embedding_bwd(idx, dout2d, dtable, bag, avg):
     dtable.index_add_(0, ii[valid], g.repeat_interleave(bag, 0)[valid])
 
 
+# ----------------------------------------------------------------------------------- LSTM
+def lstm_fwd_cell(G, ldg, c_prev, c_out, h_out, ldh, B, H):
+    """One LSTM step in place on the gate rows G (pre-activations -> activated i, f, g, o), c_out
+    (fp32) and h_out rows; G / h_out are row views with row strides ldg / ldh (elements)."""
+    if native(G):
+        ext().lstm_fwd_cell(G, ldg, c_prev, c_out, h_out, ldh, B, H)
+        return
+    g = G.as_strided((B, 4 * H), (ldg, 1))
+    gf = g.float()
+    i, f, gg, o = torch.sigmoid(gf[:, :H]), torch.sigmoid(gf[:, H:2 * H]), torch.tanh(gf[:, 2 * H:3 * H]), \
+        torch.sigmoid(gf[:, 3 * H:])
+    c = f * c_prev.view(B, H) + i * gg
+    c_out.view(B, H).copy_(c)
+    h_out.as_strided((B, H), (ldh, 1)).copy_((o * torch.tanh(c)).to(h_out.dtype))
+    g.copy_(torch.cat([i, f, gg, o], 1).to(G.dtype))
+
+
+def lstm_bwd_cell(G, ldg, c, c_prev, dy, lddy, dh_rec, dc, dG, B, H):
+    """Backward of one step: pre-activation gate gradients into dG rows (may alias G), dc
+    (fp32, in: dc_next, out: dc_prev). dy rows (stride lddy) and dh_rec [B, H] are optional."""
+    if native(G):
+        ext().lstm_bwd_cell(G, ldg, c, c_prev, dy, lddy, dh_rec, dc, dG, B, H)
+        return
+    g = G.as_strided((B, 4 * H), (ldg, 1)).float().clone()  # dG may alias G: read everything first
+    i, f, gg, o = g[:, :H], g[:, H:2 * H], g[:, 2 * H:3 * H], g[:, 3 * H:]
+    dh = torch.zeros(B, H)
+    if dy is not None:
+        dh = dh + dy.as_strided((B, H), (lddy, 1)).float()
+    if dh_rec is not None:
+        dh = dh + dh_rec.view(B, H).float()
+    tc = torch.tanh(c.view(B, H))
+    dcv = dc.view(B, H) + dh * o * (1 - tc * tc)
+    out = torch.cat([dcv * gg * i * (1 - i), dcv * c_prev.view(B, H) * f * (1 - f), dcv * i * (1 - gg * gg),
+                     dh * tc * o * (1 - o)], 1)
+    dG.as_strided((B, 4 * H), (ldg, 1)).copy_(out.to(dG.dtype))
+    dc.view(B, H).copy_(dcv * f)
+
+
 # ----------------------------------------------------------------------------- optimizers
 def sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale=1.0):
     if native(master):

@@ -17,6 +17,7 @@ from .cnn import build_alexnet, build_inception_v3, build_resnet50, build_resnex
 from .misc_models import (MoeConfig, TransformerConfig, build_mlp_unify, build_mnist_mlp, build_moe,
                           build_transformer)
 from .recsys import CandleUnoConfig, DLRMConfig, XDLConfig, build_candle_uno, build_dlrm, build_xdl
+from .rnn import NMTConfig, build_nmt
 
 SCCE = LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
 MSE = LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE
@@ -90,6 +91,12 @@ def build(name: str, ff, batch: int, small: bool = False, **kw):
         inputs, loss, mets, ncls = [ids, pos], SCCE, ACC, bc.vocab
         hi[ids.guid] = bc.vocab
         positional.add(pos.guid)
+    elif name == "nmt":
+        nc = NMTConfig.small() if small else NMTConfig()
+        src, dst, out = build_nmt(ff, batch, nc)
+        inputs, loss, mets, ncls = [src, dst], SCCE, ACC, nc.vocab
+        hi[src.guid] = nc.vocab
+        hi[dst.guid] = nc.vocab
     else:
         raise KeyError(f"unknown model {name!r}")
 
@@ -111,9 +118,9 @@ def build(name: str, ff, batch: int, small: bool = False, **kw):
 
 
 MODELS = ["alexnet", "resnet50", "resnext50", "inception_v3", "dlrm", "xdl", "candle_uno", "mlp_unify",
-          "mnist_mlp", "transformer", "moe", "bert"]
+          "mnist_mlp", "transformer", "moe", "bert", "nmt"]
 
 __all__ = ["build", "MODELS", "BertConfig", "build_bert", "build_alexnet", "build_resnet50", "build_resnext50",
            "build_inception_v3", "build_dlrm", "build_xdl", "build_candle_uno", "build_mlp_unify", "build_mnist_mlp",
            "build_transformer", "build_moe", "DLRMConfig", "XDLConfig", "CandleUnoConfig", "TransformerConfig",
-           "MoeConfig"]
+           "MoeConfig", "NMTConfig", "build_nmt"]

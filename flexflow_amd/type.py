@@ -165,6 +165,7 @@ class OperatorType(IntEnum):
     OP_FUSED_PARALLEL = 88
     OP_ALLREDUCE = 89  # extension: explicit all-reduce parallel op (not in the reference snapshot's enum)
     OP_INVALID = 89
+    OP_LSTM = 100  # extension: LSTM layer (the reference's legacy nmt/ app, outside FFModel)
 
 
 class OpType(Enum):

@@ -23,6 +23,7 @@ CASES = [
     ("native/dlrm.py", ["-b", "16", "--iterations", "2", "--small"]),
     ("native/transformer.py", ["-b", "2", "--iterations", "1", "--small"]),
     ("native/mixture_of_experts.py", ["-b", "16", "--iterations", "2", "--small"]),
+    ("native/nmt.py", ["-b", "8", "--iterations", "2", "--small"]),
     ("native/tensor_attach.py", []),
     ("native/print_input.py", ["-b", "4"]),
     ("native/print_weight.py", ["-b", "16"]),
