@@ -156,6 +156,9 @@ class MultiHeadAttention(OpImpl):
                      qs=qs, ks=ks, vs=vs, os=os_, scale=scale, causal=causal)
         return [y.view(B, Sq, E)]
 
+    def overwrites_wgrad(self, i):
+        return not self.layer.weights[i].short_name.endswith("bias")  # projection GEMMs use dw_beta = wb
+
     def _grad_index(self):
         return {w.short_name: i for i, w in enumerate(self.layer.weights)}
 

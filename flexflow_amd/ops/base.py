@@ -135,6 +135,12 @@ class OpImpl:
     def needs_input_grad(self, i: int) -> bool:
         return True
 
+    def overwrites_wgrad(self, i: int) -> bool:
+        """True if, when this layer is its weights' only user (ctx.extra['wgrad_overwrite']), the
+        backward WRITES weight i's whole gradient (beta = 0) instead of adding to it: the executor
+        then skips zeroing that gradient between steps. Conservative default."""
+        return False
+
     # ---------------------------------------------------------------- cost model
     def flops(self, in_shapes, out_shapes, w_shapes) -> float:
         return float(sum(math.prod(s) for s in out_shapes))

@@ -102,6 +102,9 @@ class Linear(OpImpl):
     def accumulates_dx(self):
         return True
 
+    def overwrites_wgrad(self, i):
+        return i == 0  # dW GEMM with dw_beta = 0 under wgrad_overwrite; the bias gradient accumulates
+
     def flops(self, in_shapes, out_shapes, w_shapes):
         return 2.0 * math.prod(out_shapes[0]) * in_shapes[0][-1]
 

@@ -66,6 +66,9 @@ class LSTM(OpImpl):
     def uses_mfma(self):
         return True
 
+    def overwrites_wgrad(self, i):
+        return i in (0, 1)  # W_ih / W_hh GEMMs with beta = 0 under wgrad_overwrite
+
     # ------------------------------------------------------------------ execution
     def forward(self, ctx, xs, ws):
         x, hx, cx = xs

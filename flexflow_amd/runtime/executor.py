@@ -40,6 +40,7 @@ class WeightArena:
         self.lowp_dtype = lowp_dtype
         self.entries = []  # (param, offset, numel, shape)
         self.size = 0
+        self.acc_end = 0   # entries [0, acc_end) accumulate their gradient (+=): zeroed every step
         self.master = self.grad = self.lowp = None
 
     def add(self, param, shape):
@@ -185,8 +186,16 @@ class Executor:
             for w in L.weights:
                 if self.layer_bwd.get(L.name) and self.local.get(L.name):
                     self.weight_users[w.guid] = self.weight_users.get(w.guid, 0) + 1
+        # Gradients an op fully OVERWRITES (a weight GEMM with beta = 0: Linear / attention / LSTM
+        # matrices whose layer is the weights' only user) need no zeroing between steps; every other
+        # gradient is accumulated into (+=: biases, norms, embeddings, shared weights). Each arena
+        # lays out its accumulated entries first, so zero_gradients() clears one prefix instead of
+        # the whole ~1.5 GB fp32 arena of BERT-Large. Within each group the order stays backward-
+        # completion order (reverse layers) for the bucketed all-reduce.
+        placed = []
         for L in reversed(self.layers):  # backward completion order
-            for w, wl in zip(L.weights, self.lay[L.name].weights):
+            single = bool(L.weights) and all(self.weight_users.get(w.guid, 1) == 1 for w in L.weights)
+            for i, (w, wl) in enumerate(zip(L.weights, self.lay[L.name].weights)):
                 if w.guid in self.weight_layout:  # shared weight (shared_op): allocated once
                     assert self.weight_layout[w.guid].key() == wl.key(), "shared weights need equal layouts"
                     continue
@@ -196,9 +205,17 @@ class Executor:
                     continue
                 p = parts[0]
                 grp = tuple(sorted(wl.replica_group(wl.coords(p)[0])))
+                ow = single and self.training and L.impl.overwrites_wgrad(i)
+                placed.append((ow, grp, w, wl.local_shape(p)))
+        for ow_pass in (False, True):
+            for ow, grp, w, shape in placed:
+                if ow != ow_pass:
+                    continue
                 ar = self.arenas.setdefault(grp, WeightArena(grp, self.device, lowp))
-                ar.add(w, wl.local_shape(p))
+                ar.add(w, shape)
                 self.weight_loc[w.guid] = (ar, len(ar.entries) - 1)
+                if not ow:
+                    ar.acc_end = ar.size
         # ZeRO-1 sharded optimizer (opt-in --zero / FF_ZERO=1): replicated (data-parallel) arenas
         # reduce-SCATTER their gradient buckets, each rank runs the optimizer on its 1/R chunk of
         # every bucket, and the updated compute copy is all-gathered back, per bucket, while the
@@ -606,7 +623,10 @@ class Executor:
 
     def zero_gradients(self):
         for ar in self.arenas.values():
-            ar.grad.zero_()
+            if ar.acc_end >= ar.size or os.environ.get("FF_ZERO_ALL_GRADS") == "1":
+                ar.grad.zero_()
+            elif ar.acc_end:
+                ar.grad[:ar.acc_end].zero_()
 
     def _apply_regularizers(self):
         """Keras-style weight regularizers (layer attr 'regularizer' with l1/l2): grad += 2*l2*w +

@@ -83,3 +83,38 @@ def test_bias_grad_fusion_into_layernorm_matches_unfused(monkeypatch):
     assert n0 == 0 and n1 == 2 * BertConfig.tiny(16).layers  # out-proj + FFN2 of every layer
     for k in a:
         np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_partial_gradient_zeroing_matches_full(monkeypatch):
+    """Arenas lay out accumulated gradients first and zero_gradients() clears only that prefix (the
+    overwritten GEMM gradients need no clearing): training matches zeroing the whole arena."""
+    import numpy as np
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(full):
+        if full:
+            monkeypatch.setenv("FF_ZERO_ALL_GRADS", "1")
+        else:
+            monkeypatch.delenv("FF_ZERO_ALL_GRADS", raising=False)
+        cfg = FFConfig(["--device", "cpu"])
+        bc = BertConfig.tiny(16)
+        cfg.batch_size = 2
+        ff = FFModel(cfg)
+        ids, pos, _ = build_bert(ff, 2, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        ars = [a for a in ff.executor.arenas.values() if a.size]
+        rng = np.random.default_rng(0)
+        for _ in range(3):
+            ids.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16), dtype=np.int32))
+            pos.set_tensor(ff, np.tile(np.arange(16, dtype=np.int32), (2, 1)))
+            ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16, 1), dtype=np.int32))
+            ff.train_step()
+        return ars, {f"{L.name}.{i}": np.asarray(w.get_weights(ff)) for L in ff.layers for i, w in enumerate(L.weights)}
+
+    ars, a = run(False)
+    assert all(0 < ar.acc_end < ar.size for ar in ars)  # a real prefix: GEMM weights are not cleared
+    _, b = run(True)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
