@@ -69,6 +69,13 @@ struct TileStage {
   }
 };
 
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
 __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
   bf16x8 o;
 #pragma unroll
@@ -269,10 +276,31 @@ __device__ __forceinline__ int dst_off(int row, int q) {
   return row * 128 + (((q >> 2) ^ f) << 3) + (q & 3) * 2;
 }
 
-// NW waves x 32 keys per workgroup. NW = 8 (256 keys) halves the fp32 dQ partial slabs that
-// attn_dq_finish_kernel has to sum (the dominant HBM traffic of the backward at S = 512).
-template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
+__device__ __forceinline__ unsigned pack_bf2(float x, float y) {
+  return (unsigned)f2bf(x) | ((unsigned)f2bf(y) << 16);
+}
+
+// NW waves x 32 keys per workgroup (NW = 8 at D = 64: 256 keys; 4 at D = 128), loop over 64-query
+// tiles. Shaped by measurements (scripts/lab/attn_bwd_lab.hip, profiles/attn_bwd_lab_r2.txt):
+//  * MASK = false (no ragged blocks, not causal) drops every bounds / mask test; with MASK the
+//    key / causal mask runs only on 32x32 blocks that cross the sequence end or the diagonal (a
+//    per-element select on every block cost the kernel ~30 %).
+//  * Prologue: the K and V blocks go row-coalesced into LDS (K stays there for dQ; V is staged in
+//    the tile buffers) and the per-lane K^T / V^T fragments are read from LDS — not per-lane
+//    gathers at the 6 KB row stride of a fused QKV projection.
+//  * Epilogue: dK / dV are staged through LDS and stored as whole 128/256-B rows, 16 B per lane
+//    (the per-lane 8-B stores scattered over 32 rows were store-issue bound: ~8 % of the kernel).
+//  * dQ tiles are computed transposed (dQ^T = K^T . dS^T: lane = query, 4 consecutive d per
+//    register quad), so partials move as 16-B vectors.
+//  * CHAIN: one launch per key block; launch p adds its dQ contribution to the fp32 running sum
+//    left by launch p - 1 (cache-resident, read back by the same lanes that will rewrite it) and the
+//    last contributing block writes the bf16 dQ — no per-key-block slabs and no finishing pass
+//    (228 -> 163 us at B32 H16 S512 D64). It needs B*H workgroups per launch to fill the chip, so
+//    small batch x heads use one launch with per-key-block slabs + attn_dq_finish_kernel.
+//  * 1-D grid through xcd_remap: the key blocks of one (batch, head) share an XCD (and its L2 copy
+//    of Q / dO).
+template <int D, int NW, bool MASK, bool CHAIN>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, int nkb, int pass) {
   constexpr int NT = 64 * NW;
   constexpr int QT = 64;       // queries per loop step
   constexpr int KB = 32 * NW;  // keys per workgroup
@@ -280,7 +308,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   // LDS: 2 x {Q tile, dO tile, lse, delta} (double-buffered: tile t+1 is fetched into registers
   // while tile t is computed), K block image, dS^T image [KB][QT]
   constexpr int TILE = 2 * QB + 2 * QT * 4;
-  // dQ stage: NTILE (query x d) 32x32 tiles per q-tile; with more waves than tiles, KSPLIT waves
+  static_assert(2 * TILE >= KB * D * 2, "tile buffers stage the V block and the dV image");
+  // dQ stage: NTILE (d x query) 32x32 tiles per q-tile; with more waves than tiles, KSPLIT waves
   // share a tile's key range and the upper parts hand their fp32 partial to part 0 through LDS
   constexpr int NTILE = 2 * (D / 32);
   constexpr int KSPLIT = NW > NTILE ? NW / NTILE : 1;
@@ -291,8 +320,11 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   float* dqx_l = reinterpret_cast<float*>(ds_l + KB * QT * 2);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const int kb0 = blockIdx.x * KB;
+  const int groups = CHAIN ? 1 : nkb;  // workgroups per (batch, head) in this launch
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = lid / groups, b = bh / a.H, hh = bh % a.H;
+  const int kblk = CHAIN ? pass : lid % groups;
+  const int kb0 = kblk * KB;
   const int key = kb0 + wave * 32 + (lane & 31);
   const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
   const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
@@ -301,44 +333,46 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
   const float* LSE = a.lse + (int64_t)bh * a.Sq;
   const float* DL = a.delta + (int64_t)bh * a.Sq;
   const float sl2 = a.scale * LOG2E;
+  // chain: slab 0 carries the running dQ sum; otherwise one fp32 slab per key block
+  const bool chain = CHAIN || nkb == 1;
+  float* dq_part = a.dq_acc + (int64_t)(chain ? 0 : kblk) * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
+  bf16_t* dQb = a.dq + (int64_t)b * a.dq_sb + (int64_t)hh * a.dq_sh;
 
-  // K block -> LDS (needed for dQ), K^T / V^T fragments -> registers (B operands, key on lane)
-  {
-    TileStage<D, KB, NT> st;
-    st.load(K, a.k_ss, kb0, a.Sk, tid);
-    st.store(k_l, tid);
-  }
+  // K block -> LDS (kept for dQ), V block -> tile buffers; K^T / V^T fragments (B operands, key on
+  // the lane) from the LDS images
   bf16x8 kf[D / 16], vf[D / 16];
+  {
+    TileStage<D, KB, NT> sk, sv;
+    sk.load(K, a.k_ss, kb0, MASK ? a.Sk : 1 << 30, tid);
+    sv.load(V, a.v_ss, kb0, MASK ? a.Sk : 1 << 30, tid);
+    sk.store(k_l, tid);
+    sv.store(smem, tid);
+  }
+  __syncthreads();
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    if (key < a.Sk) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * a.k_ss + 16 * s + 8 * h);
-      vf[s] = *reinterpret_cast<const bf16x8*>(V + (int64_t)key * a.v_ss + 16 * s + 8 * h);
-    } else {
-      kf[s] = bf16x8{};
-      vf[s] = bf16x8{};
-    }
+    const int row = wave * 32 + (lane & 31);
+    kf[s] = *reinterpret_cast<const bf16x8*>(k_l + aoff<D>(row, 16 * s + 8 * h));
+    vf[s] = *reinterpret_cast<const bf16x8*>(smem + aoff<D>(row, 16 * s + 8 * h));
   }
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
 
-  int qt_begin = 0;
-  if (a.causal) qt_begin = (kb0 / QT);
+  const int qt_begin = (MASK && a.causal) ? kb0 / QT : 0;
   const int nqt = (a.Sq + QT - 1) / QT;
   const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
-  float* dq_part = a.dq_acc + (int64_t)blockIdx.x * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
 
   TileStage<D, QT, NT> sq, sd;
   float lse_r = INFINITY, dl_r = 0.f;
   auto fetch = [&](int t) {  // global -> registers
     const int qbase = t * QT;
-    sq.load(Q, a.q_ss, qbase, a.Sq, tid);
-    sd.load(dO, a.do_ss, qbase, a.Sq, tid);
+    sq.load(Q, a.q_ss, qbase, MASK ? a.Sq : 1 << 30, tid);
+    sd.load(dO, a.do_ss, qbase, MASK ? a.Sq : 1 << 30, tid);
     if (tid < QT) {
       const int q = qbase + tid;
-      lse_r = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
-      dl_r = q < a.Sq ? DL[q] : 0.f;
+      lse_r = (!MASK || q < a.Sq) ? LSE[q] * LOG2E : INFINITY;
+      dl_r = (!MASK || q < a.Sq) ? DL[q] : 0.f;
     }
   };
   auto stash = [&](int t) {  // registers -> LDS buffer t & 1
@@ -350,10 +384,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
       reinterpret_cast<float*>(tb + 2 * QB)[QT + tid] = dl_r;
     }
   };
-  if (qt_begin < nqt) {
-    fetch(qt_begin);
-    stash(qt_begin);
-  }
+  if (qt_begin < nqt) fetch(qt_begin);
+  __syncthreads();  // every wave has its V fragments: the tile buffers can be overwritten
+  if (qt_begin < nqt) stash(qt_begin);
   __syncthreads();
 
   for (int t = qt_begin; t < nqt; ++t) {
@@ -378,22 +411,30 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
         pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
       }
       // P = exp2(S*sl2 - lse2), dS = P * (dP - delta); accumulator rows 4g..4g+3 are 4 consecutive
-      // queries, so their lse / delta come in as one 16-B LDS read each (not 16 scalar reads)
+      // queries, so their lse / delta come in as one 16-B LDS read each
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int q0l = 32 * qt + 8 * g4 + 4 * h;
-        const float4 L4 = *reinterpret_cast<const float4*>(lse_l + q0l);
-        const float4 D4 = *reinterpret_cast<const float4*>(dl_l + q0l);
-        const float lv[4] = {L4.x, L4.y, L4.z, L4.w}, dv4[4] = {D4.x, D4.y, D4.z, D4.w};
+        const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
+        const float lv[4] = {L4.x, L4.y, L4.z, L4.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g4 + j;
-          const int q = qbase + q0l + j;
-          float p = exp2f(sacc[r] * sl2 - lv[j]);
-          if (key >= a.Sk || (a.causal && key > q)) p = 0.f;
-          sacc[r] = p;
-          pacc[r] = p * (pacc[r] - dv4[j]);
+        for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = exp2f(sacc[4 * g4 + j] * sl2 - lv[j]);
+      }
+      if (MASK) {
+        const bool need = (kb0 + wave * 32 + 31 >= a.Sk) || (a.causal && kb0 + wave * 32 + 31 > qbase + 32 * qt);
+        if (need) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= a.Sk || (a.causal && key > q)) sacc[r] = 0.f;
+          }
         }
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 D4 = *reinterpret_cast<const float4*>(dl_l + 32 * qt + 8 * g4 + 4 * h);
+        const float dv4[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pacc[4 * g4 + j] = sacc[4 * g4 + j] * (pacc[4 * g4 + j] - dv4[j]);
       }
       const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
       const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
@@ -404,37 +445,24 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
-          bf16x8 ao, aq;
-          {
-            const bf16x4 lo = tr_read(do_l, aoff<D>(r0, col));
-            const bf16x4 hi = tr_read(do_l, aoff<D>(r0 + 8, col));
-            ao[0] = lo[0]; ao[1] = lo[1]; ao[2] = lo[2]; ao[3] = lo[3];
-            ao[4] = hi[0]; ao[5] = hi[1]; ao[6] = hi[2]; ao[7] = hi[3];
-          }
-          {
-            const bf16x4 lo = tr_read(q_l, aoff<D>(r0, col));
-            const bf16x4 hi = tr_read(q_l, aoff<D>(r0 + 8, col));
-            aq[0] = lo[0]; aq[1] = lo[1]; aq[2] = lo[2]; aq[3] = lo[3];
-            aq[4] = hi[0]; aq[5] = hi[1]; aq[6] = hi[2]; aq[7] = hi[3];
-          }
+          const bf16x8 ao = cat8(tr_read(do_l, aoff<D>(r0, col)), tr_read(do_l, aoff<D>(r0 + 8, col)));
+          const bf16x8 aq = cat8(tr_read(q_l, aoff<D>(r0, col)), tr_read(q_l, aoff<D>(r0 + 8, col)));
           dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, s2 ? pb1 : pb0, dv[dt], 0, 0, 0);
           dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, s2 ? sb1 : sb0, dk[dt], 0, 0, 0);
         }
       }
-      // dS^T image [key][q] (key = wave*32 + lane&31), 4 consecutive q per 8-B write
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ql = 32 * qt + 8 * g + 4 * h;
+      // dS^T image [key][q] (key = wave*32 + lane&31): the packed dS quads, 4 queries per 8-B write
+      {
         const int krow = wave * 32 + (lane & 31);
-        ushort4 o;
-        o.x = f2bf(pacc[4 * g + 0]); o.y = f2bf(pacc[4 * g + 1]);
-        o.z = f2bf(pacc[4 * g + 2]); o.w = f2bf(pacc[4 * g + 3]);
-        *reinterpret_cast<ushort4*>(ds_l + dst_off(krow, ql)) = o;
+        const bf16x4 parts[4] = {sb0.lo, sb0.hi, sb1.lo, sb1.hi};
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(ds_l + dst_off(krow, 32 * qt + 8 * g + 4 * h)) = parts[g];
       }
     }
     lds_barrier();
-    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's KB keys; wave -> (qt, dt) tiles
-    // (and, with KSPLIT > 1, a 1/KSPLIT slice of the keys)
+    // dQ^T tile (d x query) = K^T . dS^T over this block's keys: wave -> (qt, dt) tiles (and, with
+    // KSPLIT > 1, a 1/KSPLIT slice of the keys); lane = query, rows = d (r&3) + 8(r>>2) + 4h
     for (int tile = wave % NTILE; tile < NTILE; tile += (NW < NTILE ? NW : NTILE)) {
       const int qt = tile / (D / 32), dt = tile % (D / 32);
       const int part = KSPLIT > 1 ? wave / NTILE : 0;
@@ -442,28 +470,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
       f32x16 acc = f32x16{};
 #pragma unroll
       for (int ks = part * KS_PER; ks < (part + 1) * KS_PER; ++ks) {
-        // A = dS[q][key]: lane q = 32qt + lane&31, keys 16ks + 8h + j -> column reads of dS^T image
-        bf16x8 af;
-        {
-          // tr read of dS^T [key][q]: 16-lane group G covers q cols 32qt + 16(G&1) + i, key rows
-          const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
-          const int kr = 16 * ks + 8 * h + qi;
-          const bf16x4 lo = tr_read(ds_l, dst_off(kr, cq));
-          const bf16x4 hi = tr_read(ds_l, dst_off(kr + 4, cq));
-          af[0] = lo[0]; af[1] = lo[1]; af[2] = lo[2]; af[3] = lo[3];
-          af[4] = hi[0]; af[5] = hi[1]; af[6] = hi[2]; af[7] = hi[3];
-        }
-        // B = K[key][d]: lane d = 32dt + lane&31, keys 16ks + 8h + j -> transposed reads of K image
-        bf16x8 bk;
-        {
-          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
-          const int kr = 16 * ks + 8 * h + qi;
-          const bf16x4 lo = tr_read(k_l, aoff<D>(kr, cd));
-          const bf16x4 hi = tr_read(k_l, aoff<D>(kr + 4, cd));
-          bk[0] = lo[0]; bk[1] = lo[1]; bk[2] = lo[2]; bk[3] = lo[3];
-          bk[4] = hi[0]; bk[5] = hi[1]; bk[6] = hi[2]; bk[7] = hi[3];
-        }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
+        const int kr = 16 * ks + 8 * h + qi;
+        const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
+        const bf16x8 af = cat8(tr_read(ds_l, dst_off(kr, cq)), tr_read(ds_l, dst_off(kr + 4, cq)));
+        const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
+        const bf16x8 bk = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bk, af, acc, 0, 0, 0);
       }
       if constexpr (KSPLIT > 1) {
         // parts 1.. park their partial in LDS (lane-major: conflict-free 16-B rows), part 0 adds
@@ -487,39 +499,70 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a) {
           }
         }
       }
-      // acc: col = d (lane&31), row = q
-      if (part == 0) {
+      const int q = qbase + 32 * qt + (lane & 31);
+      if (part == 0 && (!MASK || q < a.Sq)) {
+        float* prow = dq_part + (int64_t)q * D + 32 * dt + 4 * h;
+        if (chain && kblk > 0) {
+          // the previous launch's running sum (written by this lane of the same wave position);
+          // a causal block's query tiles all had key block kblk - 1 contributing too
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int d = 32 * dt + (lane & 31);
-          if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
+          for (int g = 0; g < 4; ++g) {
+            const float4 pv = *reinterpret_cast<const float4*>(prow + 8 * g);
+            acc[4 * g] += pv.x; acc[4 * g + 1] += pv.y; acc[4 * g + 2] += pv.z; acc[4 * g + 3] += pv.w;
+          }
+        }
+        // last key block contributing to this query tile: the last one, or (causal) the diagonal's
+        int last = nkb - 1;
+        if (MASK && a.causal) last = min(last, (qbase + QT - 1) / KB);
+        if (chain && kblk == last) {
+          bf16_t* drow = dQb + (int64_t)q * a.dq_ss + 32 * dt + 4 * h;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2*>(drow + 8 * g) = make_uint2(pack_bf2(acc[4 * g] * a.scale, acc[4 * g + 1] * a.scale),
+                                                                 pack_bf2(acc[4 * g + 2] * a.scale, acc[4 * g + 3] * a.scale));
+        } else {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(prow + 8 * g) = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
         }
       }
     }
     if (more) stash(t + 1);  // other buffer: its last readers finished before this tile's first sync
     lds_barrier();           // tile t+1 visible; dS^T reads of tile t done before it is rewritten
   }
-  // causal: query tiles before qt_begin contribute nothing; zero their partial rows
-  if (a.causal) {
+  // slabs, causal: query tiles before qt_begin get nothing from this key block; zero its rows
+  if (MASK && a.causal && !chain) {
     for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
   }
-  // write dK, dV: lane holds key (lane&31), d = 32dt + (r&3) + 8(r>>2) + 4h
-  if (key < a.Sk) {
-    bf16_t* dK = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh + (int64_t)key * a.dk_ss;
-    bf16_t* dV = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh + (int64_t)key * a.dv_ss;
+  // dK (K block image) and dV (tile buffers) through LDS, 16-B chunks XOR-swizzled by row & 7;
+  // the loop's last barrier retired every read of both regions
+  if (qt_begin >= nqt) __syncthreads();
+  {
+    char* dv_l = smem;
+    const int row = wave * 32 + (lane & 31);
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * h;
-        ushort4 o;
-        o.x = f2bf(dk[dt][4 * g + 0] * a.scale); o.y = f2bf(dk[dt][4 * g + 1] * a.scale);
-        o.z = f2bf(dk[dt][4 * g + 2] * a.scale); o.w = f2bf(dk[dt][4 * g + 3] * a.scale);
-        *reinterpret_cast<ushort4*>(dK + d) = o;
-        o.x = f2bf(dv[dt][4 * g + 0]); o.y = f2bf(dv[dt][4 * g + 1]);
-        o.z = f2bf(dv[dt][4 * g + 2]); o.w = f2bf(dv[dt][4 * g + 3]);
-        *reinterpret_cast<ushort4*>(dV + d) = o;
+        const int c = 4 * dt + g;
+        const int off = row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h;
+        *reinterpret_cast<uint2*>(k_l + off) = make_uint2(pack_bf2(dk[dt][4 * g] * a.scale, dk[dt][4 * g + 1] * a.scale),
+                                                          pack_bf2(dk[dt][4 * g + 2] * a.scale, dk[dt][4 * g + 3] * a.scale));
+        *reinterpret_cast<uint2*>(dv_l + off) = make_uint2(pack_bf2(dv[dt][4 * g], dv[dt][4 * g + 1]),
+                                                           pack_bf2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
+      }
+    }
+    lds_barrier();
+    bf16_t* dKb = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh;
+    bf16_t* dVb = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh;
+    constexpr int CPR = D / 8;  // 16-B chunks per row
+#pragma unroll
+    for (int i = 0; i < KB * CPR / NT; ++i) {
+      const int id = tid + i * NT, r = id / CPR, c = id % CPR;
+      const int off = r * (D * 2) + ((c ^ (r & 7)) << 4);
+      if (!MASK || kb0 + r < a.Sk) {
+        *reinterpret_cast<uint4*>(dKb + (int64_t)(kb0 + r) * a.dk_ss + 8 * c) = *reinterpret_cast<const uint4*>(k_l + off);
+        *reinterpret_cast<uint4*>(dVb + (int64_t)(kb0 + r) * a.dv_ss + 8 * c) = *reinterpret_cast<const uint4*>(dv_l + off);
       }
     }
   }
@@ -783,13 +826,12 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
   }
 }
 
-// Backward variant: 0 = attn_bwd_kernel (4 waves x 32 keys, 2 workgroups per CU), 1 = the
-// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64), 2 = attn_bwd_kernel
-// with 8 waves x 32 keys (256 keys per workgroup, the dQ stage split over wave halves with an LDS
-// hand-off) at D = 64, variant 0 otherwise. Settable for A/B runs in one process
-// (attn_set_bwd_variant); default from FF_ATTN_BWD, else 2: at B32 H16 S512 D64 (pre + main +
-// dQ finish) variant 0 measured 0.308 ms, variant 1 0.316 ms, variant 2 0.271 ms — half the fp32
-// dQ partial slabs, and Q / dO tiles shared by 8 waves (profiles/attn_bwd_variants_r1.txt).
+// Backward variant: 0 = attn_bwd_kernel with 4 waves x 32 keys and per-key-block slabs; 1 = the
+// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64); 2 (default) =
+// attn_bwd_kernel with 8 waves x 32 keys at D = 64 (4 at D = 128), chained launches when B*H
+// workgroups fill the chip (>= 256) or there is one key block, else slabs; 3 = variant 2 always
+// chained; 4 = variant 2 always with slabs. Settable for A/B runs in one process
+// (attn_set_bwd_variant); default from FF_ATTN_BWD.
 static int g_bwd_variant = -1;
 int attn_bwd_variant() {
   if (g_bwd_variant < 0) {
@@ -803,7 +845,8 @@ void attn_set_bwd_variant(int v) { g_bwd_variant = v; }
 // keys per backward workgroup
 static int bwd_keys(int D) {
   const int v = attn_bwd_variant();
-  return ((v == 1 && D == 64) || (v == 2 && D == 64)) ? 256 : 128;
+  if (v == 0) return 128;
+  return D == 64 ? 256 : 128;
 }
 
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
@@ -817,28 +860,43 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   else if (a.D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, st, a);
 }
 
+template <int D, int NW>
+static void launch_bwd_main(AttnArgs a, int nkb, bool chain, hipStream_t st) {
+  const bool mask = a.causal || a.Sk % (32 * NW) != 0 || a.Sq % 64 != 0;
+  const int bh = a.B * a.H;
+  if (chain) {
+    for (int p = 0; p < nkb; ++p) {
+      if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, true>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+      else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, true>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+    }
+  } else {
+    if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, false>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+    else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, false>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+  }
+}
+
 void attn_bwd(AttnArgs a, hipStream_t st) {
-  const int kg = attn_bwd_variant() == 1;
-  const int w8 = attn_bwd_variant() == 2 && a.D == 64;
+  const int v = attn_bwd_variant();
   const int nkb = (a.Sk + bwd_keys(a.D) - 1) / bwd_keys(a.D);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
-  dim3 grid(nkb, a.B * a.H);
-  dim3 grid1((unsigned)(nkb * a.B * a.H));
+  const dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
-  dim3 gfin(ew_grid(per / 4, 256));
-#define FFK_ATTN_BWD(DD)                                                                                 \
-  hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, gpre, dim3(256), 0, st, a);                               \
-  if (kg) hipLaunchKernelGGL((attn_bwd_kg_kernel<DD, DD == 64 ? 2 : 1>), grid1, dim3(256), 0, st, a, nkb); \
-  else if (w8) hipLaunchKernelGGL((attn_bwd_kernel<DD, DD == 64 ? 8 : 4>), grid, dim3(DD == 64 ? 512 : 256), 0, st, a); \
-  else hipLaunchKernelGGL((attn_bwd_kernel<DD, 4>), grid, dim3(256), 0, st, a);                         \
-  hipLaunchKernelGGL(attn_dq_finish_kernel<DD>, gfin, dim3(256), 0, st, a, nkb);
+  const dim3 gfin(ew_grid(per / 4, 256));
+  // (every attn_bwd_kernel launch with a single key block writes the final dQ itself)
+  const bool chain = v == 3 || (v == 2 && a.B * a.H >= 256);
+  const bool finish = v == 1 || (!chain && nkb > 1);
   if (a.D == 64) {
-    FFK_ATTN_BWD(64)
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
+    if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<64, 2>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
+    else if (v == 0) launch_bwd_main<64, 4>(a, nkb, false, st);
+    else launch_bwd_main<64, 8>(a, nkb, chain, st);
+    if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
   } else if (a.D == 128) {
-    FFK_ATTN_BWD(128)
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, gpre, dim3(256), 0, st, a);
+    if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<128, 1>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
+    else launch_bwd_main<128, 4>(a, nkb, v != 0 && chain, st);
+    if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
   }
-#undef FFK_ATTN_BWD
 }
 
 }  // namespace ffk

@@ -143,12 +143,13 @@ def _attn_ref(q, k, v, scale, causal):
     return torch.einsum("bhqk,bhkd->bhqd", p, v), torch.logsumexp(s, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("S,D,causal", [(512, 64, False), (200, 64, False), (256, 128, False), (384, 64, True),
-                                        (640, 64, True), (300, 128, True)])
+                                        (640, 64, True), (300, 128, True), (1024, 64, True), (512, 128, False)])
 def test_flash_attention(ffC, S, D, causal, variant):
-    """Both backward structures (variant 0: 4 waves x 32 keys; 1: one wave per SIMD, 64 keys per
-    wave at D = 64) against an fp32 PyTorch reference, incl. ragged and causal key blocks."""
+    """Every backward structure (0: 4 waves x 32 keys + slabs; 1: one wave per SIMD, 64 keys per
+    wave at D = 64; 2: default; 3: chained per-key-block launches carrying the fp32 dQ sum; 4:
+    8 waves + slabs) against an fp32 PyTorch reference, incl. ragged and causal key blocks."""
     torch.manual_seed(3)
     prev_variant = ffC.attn_bwd_variant()
     ffC.attn_set_bwd_variant(variant)
@@ -174,6 +175,33 @@ def test_flash_attention(ffC, S, D, causal, variant):
     assert _rel(dk, kf.grad) < 3e-2
     assert _rel(dq, qf.grad) < 3e-2
     ffC.attn_set_bwd_variant(prev_variant)
+
+
+def test_flash_attention_bwd_default_chain(ffC):
+    """B*H >= 256 takes the chained backward by default (no dQ slabs, no finishing pass): BERT-Large
+    attention shape with the fused [B,S,3,H,D] projection layout, against fp32 autograd."""
+    torch.manual_seed(6)
+    B, S, H, D = 16, 512, 16, 64
+    assert ffC.attn_bwd_variant() == 2
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
+    o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=DEV)
+    sq = [S * 3 * H * D, D, 3 * H * D]
+    so = [S * H * D, D, H * D]
+    base = qkv.view(-1)
+    scale = 0.125
+    ffC.attn_fwd(base, sq, base[H * D:], sq, base[2 * H * D:], sq, o, so, lse, B, H, S, S, D, scale, False)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(qkv)
+    db = dqkv.view(-1)
+    ws = torch.empty(ffC.attn_bwd_ws(B, H, S, S, D), device=DEV)
+    ffC.attn_bwd(base, sq, base[H * D:], sq, base[2 * H * D:], sq, o, so, do, so, lse, db, sq, db[H * D:], sq,
+                 db[2 * H * D:], sq, ws, B, H, S, S, D, scale, False)
+    q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3).float().requires_grad_() for i in range(3))
+    ref, _ = _attn_ref(q, k, v, scale, False)
+    ref.backward(do.permute(0, 2, 1, 3).float())
+    for i, t in enumerate((q, k, v)):
+        assert _rel(dqkv[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
 
 
 def test_flash_attention_strided_qkv(ffC):
