@@ -369,6 +369,10 @@ __global__ void reduce_mid_kernel(const T* __restrict__ x, T* __restrict__ y, in
 }
 
 static int row_blocks(int rows) { return std::max(1, std::min((rows + 3) / 4, 8192)); }
+// Two-pass row kernels (statistics pass, then a rewrite pass over the same row): at most 3
+// workgroups (12 rows) per CU in flight so a row is still cache-resident for its second pass
+// (see softmax_xent_fwd_bwd)
+static int row_blocks_2pass(int rows) { return std::min(row_blocks(rows), 768); }
 
 #define DT_DISPATCH(dt, ...)                                        \
   do {                                                              \
@@ -378,13 +382,13 @@ static int row_blocks(int rows) { return std::max(1, std::min((rows + 3) / 4, 81
 
 void softmax_fwd(int dt, const void* x, void* y, int rows, int cols, float scale, hipStream_t st) {
   if (rows == 0) return;
-  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_fwd_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st, (const T*)x,
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_fwd_kernel<T>, dim3(row_blocks_2pass(rows)), dim3(256), 0, st, (const T*)x,
                                      (T*)y, rows, cols, scale));
 }
 void softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int cols, float scale, int accumulate,
                  hipStream_t st) {
   if (rows == 0) return;
-  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_bwd_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st, (const T*)y,
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_bwd_kernel<T>, dim3(row_blocks_2pass(rows)), dim3(256), 0, st, (const T*)y,
                                      (const T*)dy, (T*)dx, rows, cols, scale, accumulate));
 }
 void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* loss, void* dlogits, int rows,
@@ -405,7 +409,14 @@ void softmax_xent_fwd_bwd(int dt, const void* logits, const int* labels, float* 
                          (bf16_t*)dlogits, rows, cols, gscale, acc3);
     return;
   }
-  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(row_blocks(rows)), dim3(256), 0, st,
+  // At most 3 workgroups (12 rows) per CU in flight: with every row of a 16384 x 30522 call in
+  // flight at once (4096 workgroups) the ~500 MB between a row's two passes overflowed the 256 MB
+  // Infinity Cache and the gradient pass re-read HBM; capped, the re-read hits the cache:
+  // 795 -> 607 us per call (grid sweep 256..2048: 512..768 best; scripts/xent_probe.py,
+  // profiles/softmax_xent_grid_r2.txt). FF_XENT_GRID overrides the cap.
+  static const int grid_cap = getenv("FF_XENT_GRID") ? atoi(getenv("FF_XENT_GRID")) : 768;
+  const int g = grid_cap > 0 ? std::min(row_blocks(rows), grid_cap) : row_blocks(rows);
+  DT_DISPATCH(dt, hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(g), dim3(256), 0, st,
                                      (const T*)logits, labels, loss, (T*)dlogits, rows, cols, gscale, acc3));
 }
 void xent_grad(int dt, const void* probs, const int* labels, const void* onehot, void* dprobs, float* loss, int rows,
