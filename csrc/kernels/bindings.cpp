@@ -317,6 +317,62 @@ void lstm_bwd_cell(Tensor G, int64_t ldg, Tensor c, Tensor c_prev, optional<Tens
                      ptr(dh_rec), dc.data_ptr<float>(), dG.data_ptr(), B, H, cur_stream());
 }
 
+void batchnorm_fwd(Tensor x, Tensor y, Tensor g, Tensor b, Tensor mean, Tensor rstd, Tensor run_mean,
+                   Tensor run_var, Tensor ws, int64_t N, int64_t C, int64_t HW, double eps, double momentum,
+                   bool training, bool relu) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.numel() == N * C * HW && y.numel() == x.numel(), "batchnorm_fwd: x/y size");
+  TORCH_CHECK(g.numel() >= C && b.numel() >= C && g.scalar_type() == x.scalar_type() &&
+              b.scalar_type() == x.scalar_type(), "batchnorm_fwd: scale/bias");
+  TORCH_CHECK(mean.numel() >= C && rstd.numel() >= C && run_mean.numel() >= C && run_var.numel() >= C,
+              "batchnorm_fwd: statistics");
+  TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "batchnorm_fwd: workspace too small");
+  ffk::batchnorm_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), g.data_ptr(), b.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), run_mean.data_ptr<float>(), run_var.data_ptr<float>(),
+                     ws.data_ptr<float>(), N, C, HW, eps, momentum, training, relu, cur_stream());
+}
+void batchnorm_bwd(Tensor x, Tensor dy, Tensor g, Tensor b, Tensor mean, Tensor rstd, Tensor dx,
+                   optional<Tensor> dg, optional<Tensor> db, Tensor ws, int64_t N, int64_t C, int64_t HW, bool relu) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.numel() == N * C * HW && dy.numel() == x.numel() && dx.numel() == x.numel(), "batchnorm_bwd: size");
+  TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "batchnorm_bwd: workspace too small");
+  TORCH_CHECK(!dg.has_value() || (dg->scalar_type() == at::kFloat && dg->numel() >= C), "batchnorm_bwd: dg fp32");
+  TORCH_CHECK(!db.has_value() || (db->scalar_type() == at::kFloat && db->numel() >= C), "batchnorm_bwd: db fp32");
+  ffk::batchnorm_bwd(dtcode(x), x.data_ptr(), dy.data_ptr(), g.data_ptr(), b.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), dx.data_ptr(), ptr<float>(dg), ptr<float>(db), ws.data_ptr<float>(), N,
+                     C, HW, relu, cur_stream());
+}
+int64_t bn_ws(int64_t N, int64_t C, int64_t HW) { return ffk::bn_partial_floats(N, C, HW); }
+std::vector<int> pool_geom(const std::vector<int64_t>& g) {
+  TORCH_CHECK(g.size() == 14, "pool2d: geometry is N C H W OH OW kh kw sh sw pad_t pad_b pad_l pad_r");
+  TORCH_CHECK(g[6] * g[7] <= 256, "pool2d: window larger than 256 (byte winner index)");
+  TORCH_CHECK(g[8] > 0 && g[9] > 0 && g[10] < g[6] && g[12] < g[7], "pool2d: stride > 0, pad < window");
+  // every output window must start inside the padded input
+  TORCH_CHECK((g[4] - 1) * g[8] - g[10] < g[2] + g[11] && (g[5] - 1) * g[9] - g[12] < g[3] + g[13],
+              "pool2d: output larger than the padded input");
+  return std::vector<int>(g.begin(), g.end());
+}
+void pool2d_fwd(Tensor x, Tensor y, optional<Tensor> idx, std::vector<int64_t> g, bool is_max, bool include_pad,
+                bool relu) {
+  check_dev(x, "x");
+  const auto gi = pool_geom(g);
+  TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && y.numel() == g[0] * g[1] * g[4] * g[5], "pool2d_fwd: size");
+  TORCH_CHECK(!idx.has_value() || idx->numel() >= y.numel(), "pool2d_fwd: idx");
+  ffk::pool2d_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), ptr<uint8_t>(idx), gi.data(), is_max, include_pad, relu,
+                  cur_stream());
+}
+void pool2d_bwd(Tensor x, optional<Tensor> y, Tensor dy, optional<Tensor> idx, Tensor dx, std::vector<int64_t> g,
+                bool is_max, bool include_pad, bool relu) {
+  check_dev(x, "x");
+  const auto gi = pool_geom(g);
+  TORCH_CHECK(dx.numel() == x.numel() && x.numel() == g[0] * g[1] * g[2] * g[3] &&
+              dy.numel() == g[0] * g[1] * g[4] * g[5], "pool2d_bwd: size");
+  TORCH_CHECK(!is_max || (idx.has_value() && idx->numel() >= dy.numel()), "pool2d_bwd: max pooling needs idx");
+  TORCH_CHECK(is_max || !relu || (y.has_value() && y->numel() == dy.numel()), "pool2d_bwd: avg + relu needs y");
+  ffk::pool2d_bwd(dtcode(x), x.data_ptr(), ptr(y), dy.data_ptr(), ptr<uint8_t>(idx), dx.data_ptr(), gi.data(), is_max,
+                  include_pad, relu, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -370,4 +426,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd_ws", &attn_bwd_ws);
   m.def("attn_set_bwd_variant", [](int v) { ffk::attn_set_bwd_variant(v); });
   m.def("attn_bwd_variant", []() { return ffk::attn_bwd_variant(); });
+  m.def("batchnorm_fwd", &batchnorm_fwd);
+  m.def("batchnorm_bwd", &batchnorm_bwd);
+  m.def("bn_ws", &bn_ws);
+  m.def("pool2d_fwd", &pool2d_fwd);
+  m.def("pool2d_bwd", &pool2d_bwd);
 }

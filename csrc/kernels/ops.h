@@ -103,4 +103,18 @@ void lstm_fwd_cell(int dt, void* G, int64_t ldg, const float* c_prev, float* c_o
 void lstm_bwd_cell(int dt, const void* G, int64_t ldg, const float* c, const float* c_prev, const void* dy,
                    int64_t lddy, const void* dh_rec, float* dc, void* dG, int B, int H, hipStream_t st);
 
+// cnn.hip: NCHW batch norm (split Welford statistics, fused ReLU) and 2-D pooling
+int bn_partial_floats(int N, int C, int HW);  // ws floats for batchnorm_fwd / batchnorm_bwd
+void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b, float* mean, float* rstd,
+                   float* run_mean, float* run_var, float* ws, int N, int C, int HW, float eps, float momentum,
+                   int training, int relu, hipStream_t st);
+void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const void* b, const float* mean,
+                   const float* rstd, void* dx, float* dg, float* db, float* ws, int N, int C, int HW, int relu,
+                   hipStream_t st);
+// geom: N C H W OH OW kh kw sh sw pad_top pad_bottom pad_left pad_right
+void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, int is_max, int include_pad, int relu,
+                hipStream_t st);
+void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint8_t* idx, void* dx, const int* geom,
+                int is_max, int include_pad, int relu, hipStream_t st);
+
 }  // namespace ffk

@@ -927,3 +927,110 @@ def metrics_classify(probs2d, labels, acc3):
     acc3[0] += (p.argmax(-1) == lab).float().sum()
     acc3[1] += -torch.log(p.gather(1, lab[:, None]).clamp_min(1e-12)).sum()
     acc3[2] += p.shape[0]
+
+
+# ------------------------------------------------------------------ batch norm / pooling (NCHW)
+def batchnorm_fwd(x, g, b, run_mean, run_var, training, relu, eps=1e-5, momentum=0.1):
+    """Spatial batch norm (+ReLU) of an NCHW tensor (csrc/kernels/cnn.hip). Training normalizes with
+    the batch statistics and updates run_mean / run_var in place (unbiased variance, as torch);
+    inference uses the running statistics. Returns (y, mean, rstd) for the backward."""
+    N, C = x.shape[0], x.shape[1]
+    HW = x.numel() // max(1, N * C)
+    if native(x):
+        y = torch.empty_like(x)
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = torch.empty(ext().bn_ws(N, C, HW), device=x.device, dtype=torch.float32)
+        ext().batchnorm_fwd(x, y, g, b, mean, rstd, run_mean, run_var, ws, N, C, HW, eps, momentum, training, relu)
+        return y, mean, rstd
+    xf = x.float().reshape(N, C, HW)
+    if training:
+        mean = xf.mean((0, 2))
+        var = xf.var((0, 2), unbiased=False)
+        n = N * HW
+        run_mean.mul_(1 - momentum).add_(momentum * mean)
+        run_var.mul_(1 - momentum).add_(momentum * var * (n / max(n - 1, 1)))
+    else:
+        mean, var = run_mean.clone(), run_var
+    rstd = torch.rsqrt(var + eps)
+    y = (xf - mean[None, :, None]) * rstd[None, :, None] * g.float()[None, :, None] + b.float()[None, :, None]
+    if relu:
+        y = y.clamp_min(0)
+    return y.reshape(x.shape).to(x.dtype), mean, rstd
+
+
+def batchnorm_bwd(x, dy, g, b, mean, rstd, dg, db, relu):
+    """dx of batchnorm_fwd (training statistics); dg / db (fp32) += their per-channel sums."""
+    N, C = x.shape[0], x.shape[1]
+    HW = x.numel() // max(1, N * C)
+    if native(x):
+        dx = torch.empty_like(x)
+        ws = torch.empty(ext().bn_ws(N, C, HW), device=x.device, dtype=torch.float32)
+        ext().batchnorm_bwd(x, dy.contiguous(), g, b, mean, rstd, dx, dg, db, ws, N, C, HW, relu)
+        return dx
+    xf = x.float().reshape(N, C, HW)
+    xh = (xf - mean[None, :, None]) * rstd[None, :, None]
+    d = dy.float().reshape(N, C, HW)
+    gf, bf = g.float()[None, :, None], b.float()[None, :, None]
+    if relu:
+        d = d * ((xh * gf + bf) > 0)
+    s1, s2 = d.sum((0, 2)), (d * xh).sum((0, 2))
+    m = N * HW
+    dx = gf * rstd[None, :, None] * (d - s1[None, :, None] / m - xh * s2[None, :, None] / m)
+    if dg is not None:
+        dg.add_(s2)
+    if db is not None:
+        db.add_(s1)
+    return dx.reshape(x.shape).to(x.dtype)
+
+
+def pool_out_size(n, k, s, p0, p1):
+    return (n + p0 + p1 - k) // s + 1
+
+
+def _pool_ref(x, kh, kw, sh, sw, pads, is_max, include_pad, relu):
+    pt, pb, pl, pr = pads
+    if is_max:
+        xp = F.pad(x, (pl, pr, pt, pb), value=float("-inf")) if any(pads) else x
+        y = F.max_pool2d(xp, (kh, kw), (sh, sw))
+    elif pt == pb and pl == pr:
+        y = F.avg_pool2d(x, (kh, kw), (sh, sw), (pt, pl), count_include_pad=include_pad)
+    else:  # asymmetric (spatially split block): window sums over the zero-padded block / divisor
+        s = F.avg_pool2d(F.pad(x, (pl, pr, pt, pb)), (kh, kw), (sh, sw), 0, divisor_override=1)
+        if include_pad:  # floor-sized windows never leave the padded extent: divisor kh * kw
+            y = s / (kh * kw)
+        else:
+            ones = torch.ones_like(x[:1, :1])
+            y = s / F.avg_pool2d(F.pad(ones, (pl, pr, pt, pb)), (kh, kw), (sh, sw), 0, divisor_override=1)
+    return y.clamp_min(0) if relu else y
+
+
+def pool2d_fwd(x, kh, kw, sh, sw, pads, is_max, include_pad, relu, need_idx):
+    """2-D max / average pooling (+ReLU) of an NCHW tensor; pads = (top, bottom, left, right).
+    Returns (y, idx): idx holds the winning window offset per output (max pooling, device)."""
+    N, C, H, W = x.shape
+    OH = pool_out_size(H, kh, sh, pads[0], pads[1])
+    OW = pool_out_size(W, kw, sw, pads[2], pads[3])
+    if native(x):
+        y = torch.empty((N, C, OH, OW), device=x.device, dtype=x.dtype)
+        idx = torch.empty(y.numel(), device=x.device, dtype=torch.uint8) if (is_max and need_idx) else None
+        ext().pool2d_fwd(x.contiguous(), y, idx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads], is_max, include_pad,
+                         relu)
+        return y, idx
+    return _pool_ref(x.float(), kh, kw, sh, sw, pads, is_max, include_pad, relu).to(x.dtype), None
+
+
+def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
+    """dx of pool2d_fwd (gather over the covering outputs; max pooling routes dy to the winners)."""
+    N, C, H, W = x.shape
+    if native(x):
+        dx = torch.empty_like(x)
+        OH, OW = dy.shape[-2:]
+        ext().pool2d_bwd(x.contiguous(), y, dy.contiguous(), idx, dx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads],
+                         is_max, include_pad, relu)
+        return dx
+    xr = x.float().requires_grad_()
+    with torch.enable_grad():
+        yr = _pool_ref(xr, kh, kw, sh, sw, pads, is_max, include_pad, relu)
+    (dx,) = torch.autograd.grad(yr, (xr,), dy.float())
+    return dx.to(x.dtype)

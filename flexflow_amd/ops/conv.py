@@ -71,6 +71,30 @@ class _Spatial(OpImpl):
         xc = F.pad(xc, (lp3, hp3, lp2, hp2))
         return xc, (0, 0)
 
+    def _local_block(self, ctx, x):
+        """Like _local_input, but the block is cropped only and its edge padding returned as
+        (top, bottom, left, right) for kernels that pad implicitly (max pooling pads with -inf,
+        average pooling must not count padding it does not include). Also returns the crop
+        window (a2, b2, a3, b3) in the halo'd block for the backward's scatter."""
+        kh, kw, sh, sw, ph, pw = self._kp()
+        if ctx.degree(2) == 1 and ctx.degree(3) == 1:
+            return x, (ph, ph, pw, pw), None
+        ih, iw = self.layer.inputs[0].dims[2:4]
+        reg = ctx.extra["in_region0"]
+        out_reg = ctx.extra["out_region"]
+        res = []
+        for d, (k, s, p, full) in zip((2, 3), ((kh, sh, ph, ih), (kw, sw, pw, iw))):
+            olo, ohi = out_reg[d]
+            need_lo, need_hi = olo * s - p, (ohi - 1) * s - p + k
+            have_lo, have_hi = reg[d]
+            lo_pad = max(0, have_lo - need_lo) if need_lo < 0 else 0
+            hi_pad = max(0, need_hi - have_hi) if need_hi > full else 0
+            a = max(need_lo, have_lo) - have_lo
+            b = min(need_hi, have_hi) - have_lo
+            res.append((a, b, lo_pad, hi_pad))
+        (a2, b2, lp2, hp2), (a3, b3, lp3, hp3) = res
+        return x[:, :, a2:b2, a3:b3], (lp2, hp2, lp3, hp3), (a2, b2, a3, b3)
+
 
 @register(OperatorType.OP_CONV2D)
 class Conv2D(_Spatial):
@@ -189,8 +213,44 @@ class Pool2D(_Spatial):
     def supports_axis(self, axis):
         return self._spatial_ok(axis)
 
+    def _fused(self):
+        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
+        return act in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU), act == ActiMode.AC_MODE_RELU
+
     def forward(self, ctx, xs, ws):
+        """HIP pooling (csrc/kernels/cnn.hip) with the ReLU the reference allows fused; other
+        activations run through torch (not used by the reference's models)."""
         x = xs[0]
+        kh, kw, sh, sw, ph, pw = self._kp()
+        is_max = self.attrs.get("pool_type", PoolType.POOL_MAX) == PoolType.POOL_MAX
+        include_pad = bool(self.attrs.get("count_include_pad", True))
+        fused, relu = self._fused()
+        if not fused:
+            return self._forward_torch(ctx, x)
+        xc, pads, crop = self._local_block(ctx, x)
+        y, idx = K.pool2d_fwd(xc.contiguous(), kh, kw, sh, sw, pads, is_max, include_pad, relu, ctx.training)
+        if ctx.training:
+            ctx.saved.update(xc=xc.contiguous(), y=y, idx=idx, pads=pads, crop=crop, x_shape=x.shape)
+        return [y]
+
+    def backward(self, ctx, douts):
+        s = ctx.saved
+        if "xr" in s:
+            return self._backward_torch(ctx, douts)
+        kh, kw, sh, sw, ph, pw = self._kp()
+        is_max = self.attrs.get("pool_type", PoolType.POOL_MAX) == PoolType.POOL_MAX
+        _, relu = self._fused()
+        xc, y, idx, pads, crop, x_shape = (s.pop(k) for k in ("xc", "y", "idx", "pads", "crop", "x_shape"))
+        dx = K.pool2d_bwd(xc, y, douts[0].to(xc.dtype), idx, kh, kw, sh, sw, pads, is_max,
+                          bool(self.attrs.get("count_include_pad", True)), relu)
+        if crop is not None:  # attribute-parallel: scatter the block back into the halo'd input
+            a2, b2, a3, b3 = crop
+            full = torch.zeros(x_shape, dtype=dx.dtype, device=dx.device)
+            full[:, :, a2:b2, a3:b3] = dx
+            dx = full
+        return [dx]
+
+    def _forward_torch(self, ctx, x):
         kh, kw, sh, sw, ph, pw = self._kp()
         xc, pad = self._local_input(ctx, x)
         xr = xc.detach().requires_grad_(ctx.training)
@@ -207,7 +267,7 @@ class Pool2D(_Spatial):
             ctx.saved.update(xr=xr, y=y, x_shape=x.shape)
         return [y.detach()]
 
-    def backward(self, ctx, douts):
+    def _backward_torch(self, ctx, douts):
         s = ctx.saved
         xr, y, x_shape = s.pop("xr"), s.pop("y"), s.pop("x_shape")
         (dx,) = torch.autograd.grad(y, (xr,), douts[0].to(y.dtype))

@@ -13,7 +13,6 @@ from __future__ import annotations
 import math
 
 import torch
-import torch.nn.functional as F
 
 from .. import kernels as K
 from ..type import DataType, OperatorType
@@ -110,25 +109,24 @@ class BatchNorm(OpImpl):
         return [(1,), (1,)]
 
     def forward(self, ctx, xs, ws):
-        x = xs[0]
-        xr = x.detach().float().requires_grad_(ctx.training)
-        g = ws[0].detach().float().requires_grad_(ctx.training)
-        b = ws[1].detach().float().requires_grad_(ctx.training)
-        rm = ctx.extra.setdefault("running_mean", torch.zeros(x.shape[1], device=x.device))
-        rv = ctx.extra.setdefault("running_var", torch.ones(x.shape[1], device=x.device))
-        with torch.enable_grad():
-            y = F.batch_norm(xr, rm, rv, g, b, training=ctx.training, momentum=0.1, eps=1e-5)
-            if self.attrs.get("relu", True):
-                y = torch.relu(y)
+        """Batch statistics in training (running statistics updated, momentum 0.1), running
+        statistics in inference; fused ReLU per the reference's batch_norm(relu=True) default.
+        HIP kernels: csrc/kernels/cnn.hip (split Welford statistics + normalize pass)."""
+        x = xs[0].contiguous()
+        c = x.shape[1]
+        rm = ctx.extra.setdefault("running_mean", torch.zeros(c, device=x.device))
+        rv = ctx.extra.setdefault("running_var", torch.ones(c, device=x.device))
+        g, b = ws[0].reshape(-1), ws[1].reshape(-1)
+        relu = bool(self.attrs.get("relu", True))
+        y, mean, rstd = K.batchnorm_fwd(x, g, b, rm, rv, ctx.training, relu)
         if ctx.training:
-            ctx.saved.update(xr=xr, g=g, b=b, y=y)
-        return [y.detach().to(x.dtype)]
+            ctx.saved.update(x=x, g=g, b=b, mean=mean, rstd=rstd)
+        return [y]
 
     def backward(self, ctx, douts):
         s = ctx.saved
-        xr, g, b, y = s.pop("xr"), s.pop("g"), s.pop("b"), s.pop("y")
-        dx, dg, db = torch.autograd.grad(y, (xr, g, b), douts[0].float())
-        if ctx.wgrads:
-            ctx.wgrads[0].add_(dg)
-            ctx.wgrads[1].add_(db)
-        return [dx.to(douts[0].dtype)]
+        dg = ctx.wgrads[0].reshape(-1) if ctx.wgrads else None
+        db = ctx.wgrads[1].reshape(-1) if ctx.wgrads and len(ctx.wgrads) > 1 else None
+        dx = K.batchnorm_bwd(s.pop("x"), douts[0], s.pop("g"), s.pop("b"), s.pop("mean"), s.pop("rstd"), dg, db,
+                             bool(self.attrs.get("relu", True)))
+        return [dx]

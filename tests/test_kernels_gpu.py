@@ -449,3 +449,73 @@ def test_hipblaslt_splitk_and_tuned_choice(ffC):
     C = C0.clone()
     Kn.gemm(A, B, C, M, N, Kd, False, False, M, N, N, beta=1.0)
     assert _rel(C, ref) < 2e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,relu", [((8, 64, 14, 14), True), ((3, 5, 7, 9), False), ((3, 3, 1, 1), True),
+                                        ((64, 16, 32, 32), False)])
+def test_batchnorm(shape, relu, dtype):
+    """HIP batch norm (split Welford statistics, fused ReLU) against torch's fp32 batch_norm:
+    output, running statistics, and dx / dgamma / dbeta."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(21)
+    N, C = shape[:2]
+    x = (torch.randn(shape, device=DEV) * 2 + 3).to(dtype)  # offset mean: Welford, not sum-of-squares
+    g = (torch.rand(C, device=DEV) + 0.5).to(dtype)
+    b = torch.randn(C, device=DEV).to(dtype)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y, mean, rstd = K.batchnorm_fwd(x, g, b, rm, rv, True, relu)
+    xr, gr, br = (t.float().requires_grad_() for t in (x, g, b))
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    ref = torch.nn.functional.batch_norm(xr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5)
+    if relu:
+        ref = torch.relu(ref)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(y, ref) < tol
+    assert _rel(rm, rm2) < 1e-5 and _rel(rv, rv2) < 1e-5
+    dy = torch.randn(shape, device=DEV).to(dtype)
+    ref.backward(dy.float())
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx = K.batchnorm_bwd(x, dy, g, b, mean, rstd, dg, db, relu)
+    assert _rel(dx, xr.grad) < (3e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert _rel(dg, gr.grad) < 1e-3 and _rel(db, br.grad) < 1e-3
+    # inference: running statistics
+    y2, _, _ = K.batchnorm_fwd(x, g, b, rm, rv, False, relu)
+    ref2 = torch.nn.functional.batch_norm(x.float(), rm, rv, g.float(), b.float(), training=False, eps=1e-5)
+    assert _rel(y2, torch.relu(ref2) if relu else ref2) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("k,s,p,is_max,inc,relu", [(3, 2, 1, True, True, False), (2, 2, 0, True, True, True),
+                                                   (3, 1, 1, False, True, False), (3, 2, 1, False, False, True),
+                                                   (5, 3, 2, False, False, False), (3, 2, 0, True, True, True)])
+def test_pool2d(k, s, p, is_max, inc, relu, dtype):
+    """HIP max / average pooling (+ReLU) forward and backward against torch (fp32 reference)."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(22)
+    x = torch.randn(4, 6, 17, 15, device=DEV).to(dtype)
+    y, idx = K.pool2d_fwd(x, k, k, s, s, (p, p, p, p), is_max, inc, relu, True)
+    xr = x.float().requires_grad_()
+    ref = K._pool_ref(xr, k, k, s, s, (p, p, p, p), is_max, inc, relu)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
+    dy = torch.randn_like(ref).to(dtype)
+    ref.backward(dy.float())
+    dx = K.pool2d_bwd(x, y, dy, idx, k, k, s, s, (p, p, p, p), is_max, inc, relu)
+    assert _rel(dx, xr.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
+@pytest.mark.parametrize("is_max,inc", [(True, True), (False, True), (False, False)])
+def test_pool2d_asymmetric_pads(is_max, inc):
+    """A spatially split block pads only its global edges: (top, bottom, left, right) pads."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(23)
+    x = torch.randn(2, 3, 9, 8, device=DEV)
+    pads = (1, 0, 0, 1)
+    y, idx = K.pool2d_fwd(x, 3, 3, 2, 2, pads, is_max, inc, False, True)
+    xr = x.clone().requires_grad_()
+    ref = K._pool_ref(xr, 3, 3, 2, 2, pads, is_max, inc, False)
+    assert _rel(y, ref) < 1e-6
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    assert _rel(K.pool2d_bwd(x, y, dy, idx, 3, 3, 2, 2, pads, is_max, inc, False), xr.grad) < 1e-6
