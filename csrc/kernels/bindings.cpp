@@ -343,6 +343,18 @@ void batchnorm_bwd(Tensor x, Tensor dy, Tensor g, Tensor b, Tensor mean, Tensor 
                      C, HW, relu, cur_stream());
 }
 int64_t bn_ws(int64_t N, int64_t C, int64_t HW) { return ffk::bn_partial_floats(N, C, HW); }
+void channel_sum(Tensor dy, optional<Tensor> y, optional<Tensor> dz, optional<Tensor> db, Tensor ws, int64_t N,
+                 int64_t C, int64_t HW) {
+  check_dev(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && dy.numel() == N * C * HW, "channel_sum: dy");
+  TORCH_CHECK(!y.has_value() || (y->numel() == dy.numel() && y->scalar_type() == dy.scalar_type()), "channel_sum: y");
+  TORCH_CHECK(!dz.has_value() || (dz->numel() == dy.numel() && dz->scalar_type() == dy.scalar_type()),
+              "channel_sum: dz");
+  TORCH_CHECK(!db.has_value() || (db->scalar_type() == at::kFloat && db->numel() >= C), "channel_sum: db fp32");
+  TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "channel_sum: workspace too small");
+  ffk::channel_sum(dtcode(dy), dy.data_ptr(), ptr(y), ptr(dz), ptr<float>(db), ws.data_ptr<float>(), N, C, HW,
+                   cur_stream());
+}
 std::vector<int> pool_geom(const std::vector<int64_t>& g) {
   TORCH_CHECK(g.size() == 14, "pool2d: geometry is N C H W OH OW kh kw sh sw pad_t pad_b pad_l pad_r");
   TORCH_CHECK(g[6] * g[7] <= 256, "pool2d: window larger than 256 (byte winner index)");
@@ -371,6 +383,46 @@ void pool2d_bwd(Tensor x, optional<Tensor> y, Tensor dy, optional<Tensor> idx, T
   TORCH_CHECK(is_max || !relu || (y.has_value() && y->numel() == dy.numel()), "pool2d_bwd: avg + relu needs y");
   ffk::pool2d_bwd(dtcode(x), x.data_ptr(), ptr(y), dy.data_ptr(), ptr<uint8_t>(idx), dx.data_ptr(), gi.data(), is_max,
                   include_pad, relu, cur_stream());
+}
+
+std::vector<int> conv_geom(const std::vector<int64_t>& g) {
+  TORCH_CHECK(g.size() == 14, "conv2d: geometry is N C H W K OH OW KH KW sh sw ph pw G");
+  TORCH_CHECK(g[13] >= 1 && g[1] % g[13] == 0 && g[4] % g[13] == 0, "conv2d: groups must divide C and K");
+  TORCH_CHECK(g[9] > 0 && g[10] > 0 && g[11] >= 0 && g[12] >= 0, "conv2d: stride > 0, pad >= 0");
+  TORCH_CHECK(g[5] == (g[2] + 2 * g[11] - g[7]) / g[9] + 1 && g[6] == (g[3] + 2 * g[12] - g[8]) / g[10] + 1,
+              "conv2d: output size does not match the geometry");
+  return std::vector<int>(g.begin(), g.end());
+}
+int64_t conv_ws(std::vector<int64_t> g) {
+  const auto gi = conv_geom(g);
+  return ffk::conv_ws_elems(gi[0], gi[1], gi[2], gi[3], gi[4], gi[5], gi[6], gi[7], gi[8], gi[13]);
+}
+void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, std::vector<int64_t> g, bool relu) {
+  check_dev(x, "x");
+  const auto gi = conv_geom(g);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+              "conv2d: bf16 tensors");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "conv2d: contiguous tensors");
+  TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && y.numel() == g[0] * g[4] * g[5] * g[6] &&
+              w.numel() == g[4] * (g[1] / g[13]) * g[7] * g[8], "conv2d_fwd: sizes");
+  TORCH_CHECK(!bias.has_value() || (bias->scalar_type() == at::kBFloat16 && bias->numel() >= g[4]), "conv2d: bias");
+  TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_fwd: workspace too small");
+  ffk::conv2d_fwd(x.data_ptr(), w.data_ptr(), ptr(bias), y.data_ptr(), ws.data_ptr(), gi.data(), relu, cur_stream());
+}
+void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Tensor> dw, Tensor ws,
+                std::vector<int64_t> g) {
+  check_dev(x, "x");
+  const auto gi = conv_geom(g);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv2d: bf16 tensors");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && dy.is_contiguous(), "conv2d: contiguous tensors");
+  TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && dy.numel() == g[0] * g[4] * g[5] * g[6], "conv2d_bwd: sizes");
+  TORCH_CHECK(!dx.has_value() || (dx->numel() == x.numel() && dx->scalar_type() == at::kBFloat16 &&
+                                  dx->is_contiguous()), "conv2d_bwd: dx");
+  TORCH_CHECK(!dw.has_value() || (dw->numel() == w.numel() && dw->scalar_type() == at::kFloat && dw->is_contiguous()),
+              "conv2d_bwd: dw must be fp32 like w");
+  TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_bwd: workspace too small");
+  ffk::conv2d_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), ptr(dx), ptr<float>(dw), ws.data_ptr(), gi.data(),
+                  dx.has_value(), cur_stream());
 }
 
 }  // namespace
@@ -429,6 +481,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("batchnorm_fwd", &batchnorm_fwd);
   m.def("batchnorm_bwd", &batchnorm_bwd);
   m.def("bn_ws", &bn_ws);
+  m.def("channel_sum", &channel_sum);
   m.def("pool2d_fwd", &pool2d_fwd);
   m.def("pool2d_bwd", &pool2d_bwd);
+  m.def("conv_ws", &conv_ws);
+  m.def("conv2d_fwd", &conv2d_fwd);
+  m.def("conv2d_bwd", &conv2d_bwd);
 }

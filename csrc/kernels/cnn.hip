@@ -179,6 +179,38 @@ __global__ void __launch_bounds__(256) bn_bwd_dx_kernel(const T* __restrict__ x,
   }
 }
 
+// per-channel sum of dy over (n, h, w) — the bias gradient of a convolution — with the ReLU mask
+// of the forward output applied on the way (dz = dy * (y > 0) written when requested)
+template <typename T>
+__global__ void __launch_bounds__(256) chan_sum_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                       T* __restrict__ dz, float* __restrict__ part, int N, int C,
+                                                       int HW, int S) {
+  __shared__ float sh[1][4];
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int64_t M = (int64_t)N * HW;
+  const int64_t j0 = M * s / S, j1 = M * (s + 1) / S;
+  float acc = 0.f;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+    const int64_t img = j / HW, hw = j - img * HW;
+    const int64_t i = (img * C + c) * HW + hw;
+    float d = Cvt<T>::to_f(dy[i]);
+    if (y && !(Cvt<T>::to_f(y[i]) > 0.f)) d = 0.f;
+    if (dz) dz[i] = Cvt<T>::from_f(d);
+    acc += d;
+  }
+  float v[1] = {acc};
+  block_fold<1>(v, sh, [](float* a, const float* b) { a[0] += b[0]; });
+  if (threadIdx.x == 0) part[(int64_t)c * S + s] = v[0];
+}
+
+__global__ void chan_sum_finalize_kernel(const float* __restrict__ part, int C, int S, float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f;
+  for (int s = 0; s < S; ++s) s1 += part[(int64_t)c * S + s];
+  db[c] += s1;
+}
+
 static int bn_splits(int C, int64_t M) {
   int64_t s = (1024 + C - 1) / C;
   s = std::min<int64_t>(s, std::max<int64_t>(1, M / 2048));
@@ -223,6 +255,15 @@ void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const v
   DT_DISPATCH(dt, hipLaunchKernelGGL(bn_bwd_dx_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
                                      (const T*)dy, mean, rstd, (const T*)g, (const T*)b, sums, (T*)dx, total, C, HW,
                                      1.f / (float)((int64_t)N * HW), relu));
+}
+
+void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, float* ws, int N, int C, int HW,
+                 hipStream_t st) {
+  if ((int64_t)N * C * HW == 0) return;
+  const int S = bn_splits(C, (int64_t)N * HW);
+  DT_DISPATCH(dt, hipLaunchKernelGGL(chan_sum_kernel<T>, dim3(C, S), dim3(256), 0, st, (const T*)dy, (const T*)y,
+                                     (T*)dz, ws, N, C, HW, S));
+  if (db) hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, C, S, db);
 }
 
 // ------------------------------------------------------------------------------- pooling

@@ -111,10 +111,21 @@ void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b,
 void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const void* b, const float* mean,
                    const float* rstd, void* dx, float* dg, float* db, float* ws, int N, int C, int HW, int relu,
                    hipStream_t st);
+// db (fp32) += per-channel sum of dy; with y, dy is ReLU-masked by y > 0 (written to dz if given)
+void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, float* ws, int N, int C, int HW,
+                 hipStream_t st);
 // geom: N C H W OH OW kh kw sh sw pad_top pad_bottom pad_left pad_right
 void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, int is_max, int include_pad, int relu,
                 hipStream_t st);
 void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint8_t* idx, void* dx, const int* geom,
                 int is_max, int include_pad, int relu, hipStream_t st);
+
+// conv.hip: NCHW bf16 convolution as implicit GEMMs on MFMA (channel-last padded staging copies in
+// ws). geom: N C H W K OH OW KH KW sh sw ph pw G
+int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH, int KW, int G);  // bf16 elems
+void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
+                hipStream_t st);
+void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
+                int need_dx, hipStream_t st);
 
 }  // namespace ffk

@@ -930,6 +930,7 @@ def metrics_classify(probs2d, labels, acc3):
 
 
 # ------------------------------------------------------------------ batch norm / pooling (NCHW)
+@torch.no_grad()
 def batchnorm_fwd(x, g, b, run_mean, run_var, training, relu, eps=1e-5, momentum=0.1):
     """Spatial batch norm (+ReLU) of an NCHW tensor (csrc/kernels/cnn.hip). Training normalizes with
     the batch statistics and updates run_mean / run_var in place (unbiased variance, as torch);
@@ -959,6 +960,7 @@ def batchnorm_fwd(x, g, b, run_mean, run_var, training, relu, eps=1e-5, momentum
     return y.reshape(x.shape).to(x.dtype), mean, rstd
 
 
+@torch.no_grad()
 def batchnorm_bwd(x, dy, g, b, mean, rstd, dg, db, relu):
     """dx of batchnorm_fwd (training statistics); dg / db (fp32) += their per-channel sums."""
     N, C = x.shape[0], x.shape[1]
@@ -1005,6 +1007,7 @@ def _pool_ref(x, kh, kw, sh, sw, pads, is_max, include_pad, relu):
     return y.clamp_min(0) if relu else y
 
 
+@torch.no_grad()
 def pool2d_fwd(x, kh, kw, sh, sw, pads, is_max, include_pad, relu, need_idx):
     """2-D max / average pooling (+ReLU) of an NCHW tensor; pads = (top, bottom, left, right).
     Returns (y, idx): idx holds the winning window offset per output (max pooling, device)."""
@@ -1029,8 +1032,128 @@ def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
         ext().pool2d_bwd(x.contiguous(), y, dy.contiguous(), idx, dx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads],
                          is_max, include_pad, relu)
         return dx
-    xr = x.float().requires_grad_()
+    xr = x.detach().float().requires_grad_()
     with torch.enable_grad():
         yr = _pool_ref(xr, kh, kw, sh, sw, pads, is_max, include_pad, relu)
-    (dx,) = torch.autograd.grad(yr, (xr,), dy.float())
+    (dx,) = torch.autograd.grad(yr, (xr,), dy.detach().float())
     return dx.to(x.dtype)
+
+
+# ------------------------------------------------------------------ convolution (NCHW)
+# Our implicit-GEMM MFMA kernels (csrc/kernels/conv.hip) and MIOpen (through torch) are both
+# timed once per call site (geometry) outside graph capture and the faster one is kept, as for
+# GEMMs; FF_CONV_IMPL=ours|lib forces one. The choices land in TUNE_LOG.
+_conv_tuned: dict = {}
+_CONV_IMPL = _os.environ.get("FF_CONV_IMPL", "")
+
+
+def conv_geometry(x, w, stride, pad, groups):
+    N, C, H, W = x.shape
+    K, _, KH, KW = w.shape
+    OH = (H + 2 * pad[0] - KH) // stride[0] + 1
+    OW = (W + 2 * pad[1] - KW) // stride[1] + 1
+    return [N, C, H, W, K, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1], groups]
+
+
+@torch.no_grad()
+def _conv_lib_fwd(x, w, b, g, relu):
+    y = F.conv2d(x, w, b, (g[9], g[10]), (g[11], g[12]), 1, g[13])
+    return torch.relu_(y) if relu else y
+
+
+@torch.no_grad()
+def _conv_lib_bwd(x, w, dy, g, need_dx, need_dw):
+    dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [g[9], g[10]], [g[11], g[12]], [1, 1], False,
+                                                    [0, 0], g[13], [need_dx, need_dw, False])
+    return dx, dw
+
+
+def _conv_ours_fwd(x, w, b, g, relu):
+    y = torch.empty((g[0], g[4], g[5], g[6]), device=x.device, dtype=x.dtype)
+    ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
+    ext().conv2d_fwd(x, w, b, y, ws, g, relu)
+    return y
+
+
+def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out):
+    ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
+    ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g)
+
+
+def _conv_pick(kind, key, cands):
+    if _CONV_IMPL in ("ours", "lib"):
+        return _CONV_IMPL
+    choice = _conv_tuned.get((kind, key))
+    if choice is None:
+        if not _TUNE or torch.cuda.is_current_stream_capturing():
+            return "ours"
+        times = {k: _time(f, reps=3) for k, f in cands.items()}
+        choice = min(times, key=lambda k: times[k])
+        TUNE_LOG.append({"op": f"conv2d_{kind}", "geom": list(key), "times_ms": {k: round(v, 4) for k, v in
+                                                                               times.items()}, "choice": choice})
+        _conv_tuned[(kind, key)] = choice
+    return choice
+
+
+def conv2d_fwd(x, w, b, stride, pad, groups, relu):
+    """y = [relu](conv2d(x, w) + b), NCHW. bf16 on the device: our implicit-GEMM kernel or MIOpen,
+    whichever the per-geometry timing picked; otherwise torch (fp32 / CPU reference)."""
+    g = conv_geometry(x, w, stride, pad, groups)
+    if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        x, w = x.contiguous(), w.contiguous()
+        b = b.contiguous() if b is not None else None
+        choice = _conv_pick("fwd", tuple(g), {"ours": lambda: _conv_ours_fwd(x, w, b, g, relu),
+                                              "lib": lambda: _conv_lib_fwd(x, w, b, g, relu)})
+        if choice == "ours":
+            return _conv_ours_fwd(x, w, b, g, relu)
+    return _conv_lib_fwd(x, w, b, g, relu)
+
+
+def conv2d_bwd(x, w, dy, g, dw, need_dx):
+    """Backward of conv2d_fwd for geometry g (conv_geometry): returns dx (or None) and adds the
+    weight gradient into dw (fp32, shaped like w, may be None)."""
+    if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16:
+        x, w, dy = x.contiguous(), w.contiguous(), dy.contiguous()
+
+        def ours():
+            dxo = torch.empty_like(x) if need_dx else None
+            dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
+            _conv_ours_bwd(x, w, dy, g, dxo, dwo)
+            return dxo, dwo
+
+        choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None),
+                            {"ours": ours, "lib": lambda: _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)})
+        if choice == "ours":
+            dxo = torch.empty_like(x) if need_dx else None
+            if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.shape == w.shape:
+                _conv_ours_bwd(x, w, dy, g, dxo, dw)  # atomics accumulate straight into the gradient
+            else:
+                dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
+                _conv_ours_bwd(x, w, dy, g, dxo, dwo)
+                if dw is not None:
+                    dw.add_(dwo.view_as(dw))
+            return dxo
+    dxo, dwo = _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)
+    if dw is not None:
+        dw.add_(dwo.float().view_as(dw))
+    return dxo
+
+
+@torch.no_grad()
+def conv_bias_relu_bwd(dy, y, db):
+    """NCHW: dz = dy masked by y > 0 when y is given (the fused ReLU), else dy; db (fp32, may be
+    None) += per-channel sums of dz over (n, h, w)."""
+    N, C = dy.shape[0], dy.shape[1]
+    HW = dy.numel() // max(1, N * C)
+    if y is None and db is None:
+        return dy
+    if native(dy):
+        dy = dy.contiguous()
+        dz = torch.empty_like(dy) if y is not None else None
+        ws = torch.empty(ext().bn_ws(N, C, HW), device=dy.device, dtype=torch.float32)
+        ext().channel_sum(dy, y, dz, db, ws, N, C, HW)
+        return dz if dz is not None else dy
+    dz = dy * (y > 0) if y is not None else dy
+    if db is not None:
+        db.add_(dz.float().reshape(N, C, HW).sum((0, 2)))
+    return dz

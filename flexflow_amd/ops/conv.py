@@ -5,7 +5,9 @@ computes an output row/col block and reads its input block plus a halo of the re
 provided by the edge transfer), and for conv a C_in reduction axis with partial-sum outputs.
 Attribute parallelism requires stride-aligned blocks (checked in supports_axis).
 
-Math: MIOpen through torch.nn.functional for now (groups, dilation-free, as the reference).
+Math: Conv2D runs our implicit-GEMM MFMA kernels (csrc/kernels/conv.hip) or MIOpen, timed per
+geometry (kernels.conv2d_fwd / conv2d_bwd); Pool2D runs csrc/kernels/cnn.hip. Groups, no dilation
+(as the reference).
 """
 from __future__ import annotations
 
@@ -135,6 +137,9 @@ class Conv2D(_Spatial):
         return m
 
     def forward(self, ctx, xs, ws):
+        """Implicit-GEMM MFMA convolution (csrc/kernels/conv.hip) with bias and ReLU fused into its
+        store, or MIOpen where the per-geometry timing found it faster (kernels.conv2d_fwd).
+        Activations other than ReLU are applied after the convolution."""
         x = xs[0]
         w = ws[0]
         b = ws[1] if len(ws) > 1 else None
@@ -142,28 +147,29 @@ class Conv2D(_Spatial):
             b = None
         kh, kw, sh, sw, ph, pw = self._kp()
         xc, pad = self._local_input(ctx, x)
-        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE).value
-        xr = xc.detach().requires_grad_(ctx.training)
-        wr = w.detach().requires_grad_(ctx.training)
-        br = b.detach().requires_grad_(ctx.training) if b is not None else None
-        with torch.enable_grad() if ctx.training else torch.no_grad():
-            z = F.conv2d(xr, wr, br, (sh, sw), pad, 1, self.attrs.get("groups", 1))
-            y = K.act_ref(z, act)
+        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
+        relu = act == ActiMode.AC_MODE_RELU
+        z = K.conv2d_fwd(xc, w, b, (sh, sw), pad, self.attrs.get("groups", 1), relu)
+        y = z if act in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU) else K.act_ref(z, act.value)
         if ctx.training:
-            ctx.saved.update(xr=xr, wr=wr, br=br, y=y, x_shape=x.shape)
-        return [y.detach()]
+            ctx.saved.update(xc=xc, w=w, z=z, y=y, pad=pad, x_shape=x.shape, has_b=b is not None)
+        return [y]
 
     def backward(self, ctx, douts):
         s = ctx.saved
-        xr, wr, br, y = s.pop("xr"), s.pop("wr"), s.pop("br"), s.pop("y")
-        x_shape = s.pop("x_shape")
-        need = [xr, wr] + ([br] if br is not None else [])
-        grads = torch.autograd.grad(y, need, douts[0].to(y.dtype))
-        if ctx.wgrads:
-            ctx.wgrads[0].add_(grads[1].float())
-            if br is not None and len(ctx.wgrads) > 1:
-                ctx.wgrads[1].add_(grads[2].float())
-        dx = grads[0]
+        xc, w, z, y, pad, x_shape, has_b = (s.pop(k) for k in ("xc", "w", "z", "y", "pad", "x_shape", "has_b"))
+        act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
+        dy = douts[0].to(y.dtype)
+        if act not in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU):
+            dy = (dy.float() * K.act_grad_ref(z.float(), act.value)).to(y.dtype)
+        db = ctx.wgrads[1] if (has_b and len(ctx.wgrads) > 1) else None
+        dz = K.conv_bias_relu_bwd(dy, y if act == ActiMode.AC_MODE_RELU else None, db)
+        kh, kw, sh, sw, ph, pw = self._kp()
+        g = K.conv_geometry(xc, w, (sh, sw), pad, self.attrs.get("groups", 1))
+        dw = ctx.wgrads[0] if ctx.wgrads else None
+        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True))
+        if dx is None:  # the input needs no gradient (the data, or a frozen producer)
+            return [None]
         if tuple(dx.shape) != tuple(x_shape):  # attribute-parallel: scatter crop back into halo'd block
             full = torch.zeros(x_shape, dtype=dx.dtype, device=dx.device)
             full = self._uncrop(ctx, full, dx)

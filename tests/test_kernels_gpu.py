@@ -519,3 +519,41 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     dy = torch.randn_like(ref)
     ref.backward(dy)
     assert _rel(K.pool2d_bwd(x, y, dy, idx, 3, 3, 2, 2, pads, is_max, inc, False), xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("geo", [
+    # N, C, H, W, K, (kh, kw), (sh, sw), (ph, pw), groups
+    (2, 3, 32, 32, 16, (3, 3), (1, 1), (1, 1), 1),
+    (2, 3, 63, 63, 64, (11, 11), (4, 4), (2, 2), 1),   # AlexNet conv1 shape class
+    (4, 64, 14, 14, 128, (3, 3), (2, 2), (1, 1), 1),
+    (2, 256, 7, 7, 64, (1, 1), (1, 1), (0, 0), 1),
+    (2, 32, 9, 9, 64, (3, 3), (1, 1), (1, 1), 4),
+    (3, 20, 11, 13, 36, (5, 3), (2, 1), (2, 1), 1),
+    (1, 130, 17, 17, 200, (1, 7), (1, 1), (0, 3), 1),   # Inception 1x7, channels past one tile
+])
+def test_conv2d_implicit_gemm(geo):
+    """Our implicit-GEMM MFMA convolution (forward with bias + ReLU, backward data, backward filter
+    through float atomics) against fp32 torch autograd on the same bf16 inputs."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(31)
+    N, C, H, W, Ko, (kh, kw), st, pad, G = geo
+    x = torch.randn(N, C, H, W, device=DEV).bfloat16()
+    w = (torch.randn(Ko, C // G, kh, kw, device=DEV) / math.sqrt(C // G * kh * kw)).bfloat16()
+    b = torch.randn(Ko, device=DEV).bfloat16()
+    g = K.conv_geometry(x, w, st, pad, G)
+    y = K._conv_ours_fwd(x, w, b, g, True)
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    ref = torch.relu(torch.nn.functional.conv2d(xr, wr, br, st, pad, 1, G))
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dz = K.conv_bias_relu_bwd(dy, y, None)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(w.shape, device=DEV)
+    K._conv_ours_bwd(x, w, dz, g, dx, dw)
+    assert _rel(dx, xr.grad) < 1.5e-2
+    assert _rel(dw, wr.grad) < 1e-2
+    db = torch.zeros(Ko, device=DEV)
+    K.conv_bias_relu_bwd(dy, y, db)
+    assert _rel(db, br.grad) < 1e-3
