@@ -104,5 +104,10 @@ def test_bert_two_ranks_match_single(single, search):
             # row is softmax-invariant), so its "gradient" is rounding noise whose sign Adam turns
             # into +-lr steps that differ with any reduction order: compare the q / v biases only
             a, b = a[[0, 2]], b[[0, 2]]
+        # elementwise: Adam turns a near-zero gradient into a +-lr step whose sign follows rounding
+        # noise (any change of reduction order flips some), so one element may drift by up to
+        # 2 * lr per step; the tensor as a whole must still agree closely
         d = np.abs(a - b).max()
-        assert d <= 2e-3 + 2e-2 * np.abs(b).max(), f"{search}: {k} max diff {d}"
+        assert d <= 2 * 3 * 1e-3 + 2e-2 * np.abs(b).max(), f"{search}: {k} max diff {d}"
+        rel = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-12)
+        assert rel < 2e-2, f"{search}: {k} relative difference {rel}"
