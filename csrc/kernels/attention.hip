@@ -84,14 +84,20 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
 }
 
 // ------------------------------------------------------------------------------------ forward
-template <int D>
+// MASK = false (no ragged key tile, not causal) compiles the mask test out. 1-D grid through
+// xcd_remap: the query blocks of one (batch, head) share an XCD and its L2 copy of K / V. The O
+// tile leaves through LDS as whole rows (16 B per lane). Together -5 % at B32 H16 S512 D64
+// (scripts/lab/attn_fwd_lab.hip, profiles/attn_fwd_lab_r2.txt).
+template <int D, bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   constexpr int KV = 64;
   constexpr int TB = KV * D * 2;  // bytes of one K or V tile
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const int qblk0 = blockIdx.x * 128;
+  const int nqb = (a.Sq + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = lid / nqb, b = bh / a.H, hh = bh % a.H;
+  const int qblk0 = (lid % nqb) * 128;
   const int q0 = qblk0 + wave * 32;
   const int qrow = q0 + (lane & 31);
   const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
@@ -145,7 +151,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     // test), online softmax on the raw scores (lane-local + xor-32 partner), scale folded into
     // one FMA per element: p = exp2(s * sl2 - m * sl2)
     const int kbase = t * KV;
-    const bool need_mask = (kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0);
+    const bool need_mask = MASK && ((kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0));
     if (need_mask) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -210,24 +216,34 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     }
     __syncthreads();
   }
-  // epilogue
-  if (qrow < a.Sq) {
+  // epilogue: O^T accumulators (lane = query row, d = 32dt + 8g + 4h + 0..3) -> [128 q][D] LDS
+  // image (16-B chunks XOR-swizzled by row & 7) -> whole-row 16-B stores
+  __syncthreads();  // the last tile's V reads are done: the K/V buffers are free
+  {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    bf16_t* O = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh + (int64_t)qrow * a.o_ss;
+    const int row = wave * 32 + (lane & 31);
 #pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt) {
+    for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * h;
-        ushort4 o;
-        o.x = f2bf(oacc[dt][4 * g + 0] * inv);
-        o.y = f2bf(oacc[dt][4 * g + 1] * inv);
-        o.z = f2bf(oacc[dt][4 * g + 2] * inv);
-        o.w = f2bf(oacc[dt][4 * g + 3] * inv);
-        *reinterpret_cast<ushort4*>(O + d) = o;
+        const int c = 4 * dt + g;
+        *reinterpret_cast<uint2*>(smem + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
+            make_uint2((unsigned)f2bf(oacc[dt][4 * g] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 1] * inv) << 16),
+                       (unsigned)f2bf(oacc[dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 3] * inv) << 16));
       }
+    if (h == 0 && a.lse && qrow < a.Sq) a.lse[(int64_t)bh * a.Sq + qrow] = lsum > 0.f ? (m * LN2 + __logf(lsum)) : INFINITY;
+  }
+  __syncthreads();
+  {
+    constexpr int CPR = D / 8;
+    bf16_t* Ob = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh;
+#pragma unroll
+    for (int i = 0; i < 128 * CPR / 256; ++i) {
+      const int id = tid + i * 256, r = id / CPR, c = id % CPR;
+      if (qblk0 + r < a.Sq)
+        *reinterpret_cast<uint4*>(Ob + (int64_t)(qblk0 + r) * a.o_ss + 8 * c) =
+            *reinterpret_cast<const uint4*>(smem + r * (D * 2) + ((c ^ (r & 7)) << 4));
     }
-    if (h == 0 && a.lse) a.lse[(int64_t)bh * a.Sq + qrow] = lsum > 0.f ? (m * LN2 + __logf(lsum)) : INFINITY;
   }
 }
 
@@ -855,9 +871,15 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
 }
 
 void attn_fwd(AttnArgs a, hipStream_t st) {
-  dim3 grid((a.Sq + 127) / 128, a.B * a.H);
-  if (a.D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, a);
-  else if (a.D == 128) hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, st, a);
+  const dim3 grid((unsigned)((a.Sq + 127) / 128 * a.B * a.H));
+  const bool mask = a.causal || a.Sk % 64 != 0;
+  if (a.D == 64) {
+    if (mask) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, dim3(256), 0, st, a);
+  } else if (a.D == 128) {
+    if (mask) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, dim3(256), 0, st, a);
+  }
 }
 
 template <int D, int NW>
