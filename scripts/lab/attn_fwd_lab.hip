@@ -17,7 +17,33 @@ using namespace ffk;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 enum : int { F_NO_EXP = 1, F_NO_PV = 2, F_NO_RESCALE = 4, F_ONE_TILE = 8, F_NO_EPI = 16, F_LDS_EPI = 32,
-             F_NO_MASKTEST = 64, F_XCD = 256 };
+             F_NO_MASKTEST = 64, F_XCD = 256, F_TREE = 512 };
+// max / sum of the 32 scores of a lane as balanced trees (the serial chains were 32 dependent
+// ops), and the xor-32 partner exchange with v_permlane32_swap instead of ds_bpermute
+__device__ __forceinline__ float tree_max(const f32x16& a, const f32x16& b) {
+  float t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = fmaxf(a[i], b[i]);
+#pragma unroll
+  for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+    for (int i = 0; i < w; ++i) t[i] = fmaxf(t[i], t[i + w]);
+  return t[0];
+}
+__device__ __forceinline__ float tree_sum(const f32x16& a, const f32x16& b) {
+  float t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = a[i] + b[i];
+#pragma unroll
+  for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+    for (int i = 0; i < w; ++i) t[i] = t[i] + t[i + w];
+  return t[0];
+}
+__device__ __forceinline__ float swap32(float x) {  // value of lane l ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
 template <int D>
 __device__ __forceinline__ int aswz(int row) {
   if (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 3) & 1) | (((row >> 4) & 1) << 1);
@@ -138,11 +164,16 @@ __global__ void __launch_bounds__(256, 2) fwd_knob(AttnArgs a) {
       }
     }
     float mx = -INFINITY;
+    if (KN & F_TREE) {
+      mx = tree_max(sacc[0], sacc[1]);
+      mx = fmaxf(mx, swap32(mx)) * sl2;
+    } else {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kt][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+    }
     const float mnew = fmaxf(m, mx);
     const float msafe = mnew == -INFINITY ? 0.f : mnew;
     const float alpha = exp2f(m - msafe);
@@ -153,10 +184,11 @@ __global__ void __launch_bounds__(256, 2) fwd_knob(AttnArgs a) {
       for (int r = 0; r < 16; ++r) {
         const float p = (KN & F_NO_EXP) ? __builtin_fmaf(sacc[kt][r], sl2, -msafe) : exp2f(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
         sacc[kt][r] = p;
-        rs += p;
+        if (!(KN & F_TREE)) rs += p;
       }
     }
-    rs += __shfl_xor(rs, 32, 64);
+    if (KN & F_TREE) rs = tree_sum(sacc[0], sacc[1]) + 0.f, rs += swap32(rs);
+    else rs += __shfl_xor(rs, 32, 64);
     lsum = lsum * alpha + rs;
     m = mnew;
     if (!(KN & F_NO_RESCALE)) {
@@ -297,6 +329,8 @@ int main(int argc, char** argv) {
       {"cand: XCD grouping", launch<F_XCD>, true},
       {"cand: XCD + LDS epilogue", launch<F_XCD | F_LDS_EPI>, true},
       {"cand: XCD + LDS epi + no mask test", launch<F_XCD | F_LDS_EPI | F_NO_MASKTEST>, true},
+      {"cand: tree reductions + permlane32", launch<F_TREE>, true},
+      {"cand: all above + tree", launch<F_XCD | F_LDS_EPI | F_NO_MASKTEST | F_TREE>, true},
   };
   const double flops = 4.0 * B * H * (double)S * S * D;
   std::vector<std::vector<float>> times(vars.size());
