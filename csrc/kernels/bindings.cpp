@@ -343,6 +343,23 @@ void batchnorm_bwd(Tensor x, Tensor dy, Tensor g, Tensor b, Tensor mean, Tensor 
                      C, HW, relu, cur_stream());
 }
 int64_t bn_ws(int64_t N, int64_t C, int64_t HW) { return ffk::bn_partial_floats(N, C, HW); }
+void rmsnorm_fwd(Tensor x, Tensor w, Tensor y, Tensor rstd, int64_t rows, int64_t d, double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(d <= 8192, "rmsnorm: last dimension > 8192");
+  TORCH_CHECK(x.is_contiguous() && x.numel() == rows * d && y.numel() == x.numel() && w.numel() == d &&
+              w.scalar_type() == x.scalar_type() && rstd.numel() >= rows, "rmsnorm_fwd: shapes");
+  ffk::rmsnorm_fwd(dtcode(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), rows, d, eps,
+                   cur_stream());
+}
+void rmsnorm_bwd(Tensor x, Tensor w, Tensor dy, Tensor rstd, Tensor dx, optional<Tensor> dw, int64_t rows, int64_t d) {
+  check_dev(x, "x");
+  TORCH_CHECK(d <= 8192, "rmsnorm: last dimension > 8192");
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous() && x.numel() == rows * d && dy.numel() == x.numel() &&
+              dx.numel() == x.numel() && w.numel() == d && rstd.numel() >= rows, "rmsnorm_bwd: shapes");
+  TORCH_CHECK(!dw.has_value() || (dw->scalar_type() == at::kFloat && dw->numel() >= d), "rmsnorm_bwd: dw fp32");
+  ffk::rmsnorm_bwd(dtcode(x), x.data_ptr(), w.data_ptr(), dy.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
+                   ptr<float>(dw), rows, d, cur_stream());
+}
 void channel_sum(Tensor dy, optional<Tensor> y, optional<Tensor> dz, optional<Tensor> db, Tensor ws, int64_t N,
                  int64_t C, int64_t HW) {
   check_dev(dy, "dy");
@@ -481,6 +498,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("batchnorm_fwd", &batchnorm_fwd);
   m.def("batchnorm_bwd", &batchnorm_bwd);
   m.def("bn_ws", &bn_ws);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("channel_sum", &channel_sum);
   m.def("pool2d_fwd", &pool2d_fwd);
   m.def("pool2d_bwd", &pool2d_bwd);

@@ -303,4 +303,122 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   (void)fused_ok;
 }
 
+// ------------------------------------------------------------------------------- RMS norm
+// y = x * rsqrt(mean(x^2) + eps) * w over the last dimension (T5 / LLaMA "LayerNorm" without
+// centering). One 256-thread workgroup per row at a time, the row held in registers (MAXC
+// columns per thread); the backward keeps each thread's column slice of dw in registers across
+// all of its rows and adds it into the fp32 gradient with one atomic per column per workgroup.
+__device__ __forceinline__ float block_sum256(float v, float* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();  // sh is reused row after row
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+template <typename T, int MAXC>
+__global__ void __launch_bounds__(256) rms_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                      T* __restrict__ y, float* __restrict__ rstd, int rows, int d,
+                                                      float eps) {
+  __shared__ float sh[4];
+  const int tid = threadIdx.x;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const T* xr = x + (int64_t)row * d;
+    float v[MAXC];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + 256 * i;
+      v[i] = c < d ? Cvt<T>::to_f(xr[c]) : 0.f;
+      ss += v[i] * v[i];
+    }
+    const float r = rsqrtf(block_sum256(ss, sh) / (float)d + eps);
+    if (tid == 0 && rstd) rstd[row] = r;
+    T* yr = y + (int64_t)row * d;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + 256 * i;
+      if (c < d) yr[c] = Cvt<T>::from_f(v[i] * r * Cvt<T>::to_f(w[c]));
+    }
+  }
+}
+
+template <typename T, int MAXC>
+__global__ void __launch_bounds__(256) rms_bwd_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                      const T* __restrict__ dy, const float* __restrict__ rstd,
+                                                      T* __restrict__ dx, float* __restrict__ dw, int rows, int d) {
+  __shared__ float sh[4];
+  const int tid = threadIdx.x;
+  float dwp[MAXC];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) dwp[i] = 0.f;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const T* xr = x + (int64_t)row * d;
+    const T* dyr = dy + (int64_t)row * d;
+    const float r = rstd[row];
+    float xv[MAXC], g[MAXC];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + 256 * i;
+      const float dv = c < d ? Cvt<T>::to_f(dyr[c]) : 0.f;
+      xv[i] = c < d ? Cvt<T>::to_f(xr[c]) : 0.f;
+      g[i] = c < d ? dv * Cvt<T>::to_f(w[c]) : 0.f;
+      s += g[i] * xv[i];
+      dwp[i] += dv * xv[i] * r;
+    }
+    const float k = r * r * r * block_sum256(s, sh) / (float)d;
+    T* dxr = dx + (int64_t)row * d;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + 256 * i;
+      if (c < d) dxr[c] = Cvt<T>::from_f(r * g[i] - k * xv[i]);
+    }
+  }
+  if (dw) {
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = tid + 256 * i;
+      if (c < d) atomicAdd(dw + c, dwp[i]);
+    }
+  }
+}
+
+void rmsnorm_fwd(int dt, const void* x, const void* w, void* y, float* rstd, int rows, int d, float eps,
+                 hipStream_t st) {
+  if (rows == 0) return;
+  if (dt == DT_BF16) {
+    const int g = std::max(1, std::min(rows, 1024));
+    if (d <= 256 * 8) hipLaunchKernelGGL((rms_fwd_kernel<bf16_t, 8>), dim3(g), dim3(256), 0, st, (const bf16_t*)x,
+                                         (const bf16_t*)w, (bf16_t*)y, rstd, rows, d, eps);
+    else hipLaunchKernelGGL((rms_fwd_kernel<bf16_t, 32>), dim3(g), dim3(256), 0, st, (const bf16_t*)x,
+                            (const bf16_t*)w, (bf16_t*)y, rstd, rows, d, eps);
+  } else {
+    const int g = std::max(1, std::min(rows, 1024));
+    if (d <= 256 * 8) hipLaunchKernelGGL((rms_fwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)x,
+                                         (const float*)w, (float*)y, rstd, rows, d, eps);
+    else hipLaunchKernelGGL((rms_fwd_kernel<float, 32>), dim3(g), dim3(256), 0, st, (const float*)x,
+                            (const float*)w, (float*)y, rstd, rows, d, eps);
+  }
+}
+
+void rmsnorm_bwd(int dt, const void* x, const void* w, const void* dy, const float* rstd, void* dx, float* dw,
+                 int rows, int d, hipStream_t st) {
+  if (rows == 0) return;
+  const int g = std::max(1, std::min(rows, 1024));
+  if (dt == DT_BF16) {
+    if (d <= 256 * 8) hipLaunchKernelGGL((rms_bwd_kernel<bf16_t, 8>), dim3(g), dim3(256), 0, st, (const bf16_t*)x,
+                                         (const bf16_t*)w, (const bf16_t*)dy, rstd, (bf16_t*)dx, dw, rows, d);
+    else hipLaunchKernelGGL((rms_bwd_kernel<bf16_t, 32>), dim3(g), dim3(256), 0, st, (const bf16_t*)x,
+                            (const bf16_t*)w, (const bf16_t*)dy, rstd, (bf16_t*)dx, dw, rows, d);
+  } else {
+    if (d <= 256 * 8) hipLaunchKernelGGL((rms_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)x,
+                                         (const float*)w, (const float*)dy, rstd, (float*)dx, dw, rows, d);
+    else hipLaunchKernelGGL((rms_bwd_kernel<float, 32>), dim3(g), dim3(256), 0, st, (const float*)x,
+                            (const float*)w, (const float*)dy, rstd, (float*)dx, dw, rows, d);
+  }
+}
+
 }  // namespace ffk

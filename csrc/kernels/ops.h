@@ -103,6 +103,12 @@ void lstm_fwd_cell(int dt, void* G, int64_t ldg, const float* c_prev, float* c_o
 void lstm_bwd_cell(int dt, const void* G, int64_t ldg, const float* c, const float* c_prev, const void* dy,
                    int64_t lddy, const void* dh_rec, float* dc, void* dG, int B, int H, hipStream_t st);
 
+// norm.hip: RMS norm over the last dimension (d <= 8192); rstd [rows] saved for the backward;
+// dw (fp32) += the weight gradient
+void rmsnorm_fwd(int dt, const void* x, const void* w, void* y, float* rstd, int rows, int d, float eps,
+                 hipStream_t st);
+void rmsnorm_bwd(int dt, const void* x, const void* w, const void* dy, const float* rstd, void* dx, float* dw,
+                 int rows, int d, hipStream_t st);
 // cnn.hip: NCHW batch norm (split Welford statistics, fused ReLU) and 2-D pooling
 int bn_partial_floats(int N, int C, int HW);  // ws floats for batchnorm_fwd / batchnorm_bwd
 void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b, float* mean, float* rstd,

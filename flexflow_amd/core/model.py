@@ -90,6 +90,7 @@ class FFModel:
         self._compiled = False
         self._output = None
         self._pending_values = {}
+        self._pending_weights = {}  # weight guid -> array set before compile (applied after init)
         self._tensor_remap = {}  # guid -> replacement tensor (graph substitutions at compile)
         self._names = set()
         self.iter_config_seq_length = None
@@ -267,6 +268,10 @@ class FFModel:
     def layer_norm(self, input, axes, elementwise_affine=True, eps=1e-5, name=None):
         return self._add(OperatorType.OP_LAYERNORM, [input], name, axes=list(axes),
                          elementwise_affine=elementwise_affine, eps=eps).outputs[0]
+
+    def rms_norm(self, input, eps=1e-6, name=None):
+        """y = x * rsqrt(mean(x^2, -1) + eps) * weight (extension; ops/norm.py RMSNorm)."""
+        return self._add(OperatorType.OP_RMS_NORM, [input], name, eps=float(eps)).outputs[0]
 
     def batch_matmul(self, A, B, a_seq_length_dim=None, b_seq_length_dim=None, name=None):
         return self._add(OperatorType.OP_BATCHMATMUL, [A, B], name, a_seq_length_dim=a_seq_length_dim,
@@ -453,6 +458,11 @@ class FFModel:
             t = self._find_tensor(guid)
             if t is not None:
                 self.executor.feed(t, v)
+        if self._pending_weights:
+            by_guid = {w.guid: w for L in self.layers for w in L.weights}
+            for guid, v in self._pending_weights.items():
+                if guid in by_guid:
+                    self.executor.set_weight(by_guid[guid], v)
         for L in self.layers:
             for t in L.outputs:
                 if t._attached is not None:
@@ -674,6 +684,9 @@ class FFModel:
         raise NotImplementedError("activation gradients are not retained")
 
     def _set_weight_value(self, w, arr):
+        if not self._compiled:
+            self._pending_weights[w.guid] = np.asarray(arr)
+            return
         self.executor.set_weight(w, np.asarray(arr))
 
     def _get_weight_value(self, w):

@@ -1157,3 +1157,34 @@ def conv_bias_relu_bwd(dy, y, db):
     if db is not None:
         db.add_(dz.float().reshape(N, C, HW).sum((0, 2)))
     return dz
+
+
+# ------------------------------------------------------------------ RMS norm
+@torch.no_grad()
+def rmsnorm_fwd(x2d, w, eps):
+    """y = x * rsqrt(mean(x^2) + eps) * w per row. Returns (y, rstd)."""
+    rows, d = x2d.shape
+    if native(x2d):
+        y = torch.empty_like(x2d)
+        rstd = torch.empty(rows, device=x2d.device, dtype=torch.float32)
+        ext().rmsnorm_fwd(x2d, w, y, rstd, rows, d, eps)
+        return y, rstd
+    xf = x2d.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1) + eps)
+    return (xf * rstd[:, None] * w.float()).to(x2d.dtype), rstd
+
+
+@torch.no_grad()
+def rmsnorm_bwd(x2d, w, dy2d, rstd, dw):
+    """dx of rmsnorm_fwd; dw (fp32, may be None) += sum over rows of dy * x * rstd."""
+    rows, d = x2d.shape
+    if native(x2d):
+        dx = torch.empty_like(x2d)
+        ext().rmsnorm_bwd(x2d, w, dy2d, rstd, dx, dw, rows, d)
+        return dx
+    xf, dyf, r = x2d.float(), dy2d.float(), rstd[:, None]
+    g = dyf * w.float()
+    dx = r * g - (r ** 3) * xf * (g * xf).sum(-1, keepdim=True) / d
+    if dw is not None:
+        dw.add_((dyf * xf * r).sum(0))
+    return dx.to(x2d.dtype)

@@ -6,7 +6,11 @@ every other dim can. Runs on csrc/kernels/norm.hip (one wave per row, row kept i
 
 BatchNorm (NCHW, reference src/ops/batch_norm.cc) normalises per channel over N,H,W with
 per-shard statistics when the batch is partitioned — the reference's cuDNN per-partition
-semantics. It has no hand kernel yet: MIOpen via torch does the math.
+semantics (csrc/kernels/cnn.hip).
+
+RMSNorm (extension: the T5 / LLaMA "LayerNorm" without centering, which the HuggingFace import
+path of the torch frontend meets) normalises the last dimension: y = x * rsqrt(mean(x^2) + eps) * w
+(csrc/kernels/norm.hip).
 """
 from __future__ import annotations
 
@@ -130,3 +134,44 @@ class BatchNorm(OpImpl):
         dx = K.batchnorm_bwd(s.pop("x"), douts[0], s.pop("g"), s.pop("b"), s.pop("mean"), s.pop("rstd"), dg, db,
                              bool(self.attrs.get("relu", True)))
         return [dx]
+
+
+@register(OperatorType.OP_RMS_NORM)
+class RMSNorm(OpImpl):
+    op_type = OperatorType.OP_RMS_NORM
+
+    @classmethod
+    def infer(cls, attrs, in_dims, in_dtypes):
+        d = in_dims[0]
+        from ..core.initializers import ConstantInitializer
+        return [d], [in_dtypes[0]], [WeightSpec("weight", (d[-1],), in_dtypes[0], ConstantInitializer(1.0))]
+
+    def axis_kinds(self):
+        kinds = super().axis_kinds()
+        kinds[-1] = "none"
+        return kinds
+
+    def supports_axis(self, axis):
+        return axis != len(self.layer.outputs[0].dims) - 1
+
+    def weight_maps(self):
+        return [(None,)]
+
+    def forward(self, ctx, xs, ws):
+        x = xs[0].contiguous()
+        d = x.shape[-1]
+        y, rstd = K.rmsnorm_fwd(x.reshape(-1, d), ws[0].reshape(-1), float(self.attrs.get("eps", 1e-6)))
+        if ctx.training:
+            ctx.saved.update(x=x, w=ws[0].reshape(-1), rstd=rstd)
+        return [y.reshape(x.shape)]
+
+    def backward(self, ctx, douts):
+        s = ctx.saved
+        x, w, rstd = s.pop("x"), s.pop("w"), s.pop("rstd")
+        d = x.shape[-1]
+        dw = ctx.wgrads[0].reshape(-1) if ctx.wgrads else None
+        dx = K.rmsnorm_bwd(x.reshape(-1, d), w, douts[0].reshape(-1, d).contiguous(), rstd, dw)
+        return [dx.reshape(x.shape)]
+
+    def flops(self, in_shapes, out_shapes, w_shapes):
+        return 5.0 * math.prod(out_shapes[0])

@@ -380,7 +380,18 @@ class PyTorchModel:
             for line in self.torch_to_string():
                 f.write(line + "\n")
 
+    def _hf_fx_available(self):
+        try:
+            from transformers.utils.fx import symbolic_trace  # noqa: F401
+            return True
+        except ImportError:  # transformers >= 5 dropped its fx tracer
+            return False
+
     def torch_to_ff(self, ffmodel, input_tensors, verbose=False):
+        if self.is_hf_model and not self._hf_fx_available():
+            from .export import ExportImporter
+            imp = ExportImporter(self.model, self.input_names, self.batch_size, self.seq_length)
+            return imp.to_ff(ffmodel, input_tensors)
         nodes = self._trace()
         outs, built = PyTorchModel._build_nodes(nodes, ffmodel, input_tensors, verbose)
         self._ff_of_module = {self._module_of_node[k]: v for k, v in built.items() if k in self._module_of_node}

@@ -166,6 +166,7 @@ class OperatorType(IntEnum):
     OP_ALLREDUCE = 89  # extension: explicit all-reduce parallel op (not in the reference snapshot's enum)
     OP_INVALID = 89
     OP_LSTM = 100  # extension: LSTM layer (the reference's legacy nmt/ app, outside FFModel)
+    OP_RMS_NORM = 101  # extension: RMS norm (T5 / LLaMA), met by the HuggingFace import path
 
 
 class OpType(Enum):

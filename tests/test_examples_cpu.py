@@ -36,6 +36,7 @@ CASES = [
     ("pytorch/torch_vision.py", ["--small", "-b", "8", "--samples", "16"]),
     ("pytorch/regnet.py", ["--small", "-b", "8", "--samples", "16"]),
     ("pytorch/mnist_mlp_torch2.py", ["-b", "64", "--samples", "2048", "-e", "2", "-a"]),
+    ("pytorch/mt5/mt5_ff.py", ["--tiny", "-b", "4", "-e", "1", "--samples", "16"]),
     ("pytorch/resnet152_training.py", ["--small"]),
     ("keras/seq_mnist_mlp.py", ["--samples", "1024", "-a"]),
     ("keras/func_mnist_mlp_concat.py", ["--samples", "512"]),

@@ -557,3 +557,24 @@ def test_conv2d_implicit_gemm(geo):
     db = torch.zeros(Ko, device=DEV)
     K.conv_bias_relu_bwd(dy, y, db)
     assert _rel(db, br.grad) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,d", [(300, 512), (64, 4096), (33, 100), (8, 8192)])
+def test_rmsnorm(rows, d, dtype):
+    """HIP RMS norm forward / backward (dx, fp32 dw) against fp32 torch autograd."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(41)
+    x = torch.randn(rows, d, device=DEV).to(dtype)
+    w = (torch.rand(d, device=DEV) + 0.5).to(dtype)
+    y, rstd = K.rmsnorm_fwd(x, w, 1e-6)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    ref = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(y, ref) < tol
+    dy = torch.randn(rows, d, device=DEV).to(dtype)
+    ref.backward(dy.float())
+    dw = torch.zeros(d, device=DEV)
+    dx = K.rmsnorm_bwd(x, w, dy, rstd, dw)
+    assert _rel(dx, xr.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-5)
+    assert _rel(dw, wr.grad) < 1e-3
