@@ -14,6 +14,6 @@ Batch_Norm = _op_class(OperatorType.OP_BATCHNORM)
 from .model import FFModel, PerfMetrics  # noqa: F401
 from .netconfig import DLRMConfig, NetConfig  # noqa: F401
 from .optimizers import AdamOptimizer, Optimizer, SGDOptimizer  # noqa: F401
-from .tensor import Parameter, Tensor  # noqa: F401
+from .tensor import Parameter, RegionNdarray, Tensor  # noqa: F401
 
 Op = Layer

@@ -20,6 +20,16 @@ from ..type import DataType
 
 
 class SingleDataLoader:
+    def init_from_tensor(self, ffmodel, input, full_input, num_samples, data_type):
+        """reference SingleDataLoader.init_from_tensor: the full dataset given as an FF tensor
+        (attached array or set value)."""
+        self.__init__(ffmodel, input, np.asarray(full_input.get_array(ffmodel)), num_samples, data_type)
+
+    def init_from_ptr(self, ffmodel, input, full_input, num_samples, data_type):
+        """reference SingleDataLoader.init_from_ptr: the full dataset given as host memory (any
+        object with the buffer / array interface)."""
+        self.__init__(ffmodel, input, np.asarray(full_input), num_samples, data_type)
+
     def __init__(self, ffmodel, input_tensor, full_input, num_samples=None, data_type=None):
         self.model = ffmodel
         self.tensor = input_tensor

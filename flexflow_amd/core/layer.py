@@ -62,6 +62,18 @@ class Layer:
     def get_output_tensor(self):
         return self.outputs[0]
 
+    def init(self, model):
+        """Re-initialise this op's weights with their initializers (reference Op.init)."""
+        model.executor.init_weights(model.config.seed, only=[self])
+
+    def forward(self, model):
+        """Run this op alone on the current values of its inputs (reference Op.forward)."""
+        model.executor.forward_layer(self)
+
+    def _add_to_model(self, model):
+        """Layers join their model when they are built (reference Op._add_to_model)."""
+        assert self in model.layers
+
     def get_input_tensor(self):
         return self.inputs[0]
 

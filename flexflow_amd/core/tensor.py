@@ -118,3 +118,19 @@ class Parameter(Tensor):
 
     def get_weights(self, ffmodel):
         return ffmodel._get_weight_value(self)
+
+
+class RegionNdarray:
+    """A numpy-array view of raw memory (reference flexflow_cffi.py RegionNdarray: a region's
+    base pointer, shape and byte strides exposed through __array_interface__), e.g.
+    np.asarray(RegionNdarray((4, 8), DataType.DT_FLOAT, ptr, (32, 4), False))."""
+    __slots__ = ["__array_interface__"]
+
+    def __init__(self, shape, data_type, base_ptr, strides, read_only):
+        from ..type import DataType
+        typestr = {DataType.DT_FLOAT: "<f4", DataType.DT_INT32: "<i4", DataType.DT_INT64: "<i8",
+                   DataType.DT_DOUBLE: "<f8", DataType.DT_HALF: "<f2"}.get(data_type)
+        assert typestr is not None, f"RegionNdarray: unsupported data type {data_type}"
+        self.__array_interface__ = {"version": 3, "shape": tuple(shape), "typestr": typestr,
+                                    "data": (int(base_ptr), bool(read_only)),
+                                    "strides": tuple(strides) if strides is not None else None}

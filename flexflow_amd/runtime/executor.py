@@ -250,11 +250,14 @@ class Executor:
                 self.ctx[L.name].wgrads = [self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]
                                            if w.guid in self.weight_loc else None for w in L.weights]
 
-    def init_weights(self, seed_base: int):
-        """Deterministic global init, each rank keeping its shard."""
+    def init_weights(self, seed_base: int, only=None):
+        """Deterministic global init, each rank keeping its shard (only: re-initialise just these
+        layers, the reference's Op.init)."""
         from ..core.initializers import default_initializer
         done = set()
         for li, L in enumerate(self.layers):
+            if only is not None and L not in only:
+                continue
             for i, w in enumerate(L.weights):
                 if w.guid not in self.weight_loc or w.guid in done:
                     continue
@@ -348,6 +351,23 @@ class Executor:
     def _like(self, t):
         is_float = t.data_type in (DataType.DT_FLOAT, DataType.DT_HALF, DataType.DT_DOUBLE, DataType.DT_BF16)
         return torch.empty(0, dtype=self.ctorch if is_float else torch_dtype(t.data_type), device=self.device)
+
+    def forward_layer(self, L, training: bool = False):
+        """Run one layer on the current values of its inputs (the reference's Op.forward); its
+        outputs replace the stored values."""
+        vals = self.values
+        if L.op_type == OperatorType.OP_INPUT:
+            return
+        xs = [self.fwd_tx[(L.name, j)].run(self.comm, vals.get(t.guid, self.inputs.get(t.guid)), self._like(t))
+              for j, t in enumerate(L.inputs)]
+        if self.local[L.name]:
+            ctx = self.ctx[L.name]
+            ctx.training = training
+            outs = L.impl.forward(ctx, xs, [self.weight_tensor(w) for w in L.weights])
+            if not training:
+                ctx.saved.clear()
+            for o, v in zip(L.outputs, outs):
+                vals[o.guid] = v
 
     def forward(self, training: Optional[bool] = None):
         tr = self.training if training is None else training

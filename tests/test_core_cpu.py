@@ -177,3 +177,35 @@ def test_config_flag_values():
     with pytest.warns(UserWarning):
         c = FFConfig(["--lr", "--zero", "-b", "16"])
     assert c.batch_size == 16 and c.zero_optimizer
+
+
+def test_op_forward_init_and_dataloader_helpers():
+    """reference Op.forward / Op.init, SingleDataLoader.init_from_ptr / init_from_tensor and
+    RegionNdarray (flexflow_cffi.py)."""
+    import numpy as np
+    from flexflow_amd.core import (DataType, FFConfig, FFModel, LossType, RegionNdarray, SGDOptimizer,
+                                   SingleDataLoader)
+    cfg = FFConfig(["--device", "cpu"])
+    cfg.batch_size = 4
+    ff = FFModel(cfg)
+    x = ff.create_tensor([4, 8], DataType.DT_FLOAT)
+    y = ff.dense(x, 3)
+    ff.optimizer = SGDOptimizer(ff, 0.1)
+    ff.compile(loss_type=LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE)
+    dense = ff.get_layer_by_id(0) if ff.get_layer_by_id(0).weights else ff.layers[-1]
+    xv = np.arange(32, dtype=np.float32).reshape(4, 8) / 32
+    x.set_tensor(ff, xv)
+    dense._add_to_model(ff)
+    dense.forward(ff)
+    w = np.asarray(dense.get_parameter_by_id(0).get_weights(ff))
+    b = np.asarray(dense.get_parameter_by_id(1).get_weights(ff))
+    np.testing.assert_allclose(np.asarray(y.get_tensor(ff)), xv @ w.T + b, rtol=1e-5, atol=1e-6)
+    dense.get_parameter_by_id(0).set_weights(ff, np.zeros_like(w))
+    dense.init(ff)  # back to the deterministic initial values
+    np.testing.assert_allclose(np.asarray(dense.get_parameter_by_id(0).get_weights(ff)), w)
+    buf = np.arange(40, dtype=np.float32).reshape(5, 8)
+    view = np.asarray(RegionNdarray(buf.shape, DataType.DT_FLOAT, buf.ctypes.data, buf.strides, True))
+    np.testing.assert_array_equal(view, buf)
+    dl = SingleDataLoader.__new__(SingleDataLoader)
+    dl.init_from_ptr(ff, x, view, 5, DataType.DT_FLOAT)
+    assert dl.num_samples == 5
