@@ -313,3 +313,9 @@ class Sequential(Model):
 
 
 __all__ = ["Model", "Sequential"]
+
+
+# reference names: keras/models/base_model.py BaseModel (the common base of Model and Sequential)
+# and keras/models/tensor.py Tensor (the symbolic tensor of layer calls)
+BaseModel = Model
+Tensor = KTensor
