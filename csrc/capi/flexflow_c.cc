@@ -413,4 +413,149 @@ flexflow_tensor_t flexflow_model_add_transpose(flexflow_model_t m, flexflow_tens
   return wrap<flexflow_tensor_t>(call("add_transpose", "(OONz)", obj(m.impl), obj(x.impl), int_list(perm, nd), name));
 }
 
+flexflow_tensor_t flexflow_model_add_embedding_typed(flexflow_model_t m, flexflow_tensor_t x, int num, int dim,
+                                                     int aggr, int dtype, const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(
+      call("add_embedding_typed", "(OOiiiiz)", obj(m.impl), obj(x.impl), num, dim, aggr, dtype, name));
+}
+flexflow_tensor_t flexflow_model_add_max(flexflow_model_t m, flexflow_tensor_t a, flexflow_tensor_t b, const char* n) {
+  return binary(m, "max", a, b, n);
+}
+flexflow_tensor_t flexflow_model_add_min(flexflow_model_t m, flexflow_tensor_t a, flexflow_tensor_t b, const char* n) {
+  return binary(m, "min", a, b, n);
+}
+static flexflow_tensor_t reduce(flexflow_model_t m, const char* op, flexflow_tensor_t x, int nd, const int* dims,
+                                bool keep, const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(
+      call("add_reduce", "(OsONiz)", obj(m.impl), op, obj(x.impl), int_list(dims, nd), (int)keep, name));
+}
+flexflow_tensor_t flexflow_model_add_mean(flexflow_model_t m, flexflow_tensor_t x, int nd, const int* dims, bool keep,
+                                          const char* name) {
+  return reduce(m, "mean", x, nd, dims, keep, name);
+}
+flexflow_tensor_t flexflow_model_add_reduce_sum(flexflow_model_t m, flexflow_tensor_t x, int nd, const int* axes,
+                                                bool keep, const char* name) {
+  return reduce(m, "reduce_sum", x, nd, axes, keep, name);
+}
+flexflow_tensor_t flexflow_model_add_gather(flexflow_model_t m, flexflow_tensor_t x, flexflow_tensor_t idx, int dim,
+                                            const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(call("add_gather", "(OOOiz)", obj(m.impl), obj(x.impl), obj(idx.impl), dim, name));
+}
+flexflow_tensor_t flexflow_model_add_cast(flexflow_model_t m, flexflow_tensor_t x, int dtype, const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(call("add_cast", "(OOiz)", obj(m.impl), obj(x.impl), dtype, name));
+}
+flexflow_tensor_t flexflow_model_add_rms_norm(flexflow_model_t m, flexflow_tensor_t x, float eps, const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(call("add_rms_norm", "(OOdz)", obj(m.impl), obj(x.impl), (double)eps, name));
+}
+flexflow_tensor_t flexflow_model_add_reverse(flexflow_model_t m, flexflow_tensor_t x, int axis, const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(call("add_reverse", "(OOiz)", obj(m.impl), obj(x.impl), axis, name));
+}
+
+// a Python list of tensors -> outputs[0..n) (each a new reference); returns n or -1
+static int unpack(PyObject* r, flexflow_tensor_t* outputs) {
+  if (!r) return -1;
+  if (!PyList_Check(r)) {
+    Py_DECREF(r);
+    g_err = "expected a list of tensors";
+    return -1;
+  }
+  const int n = (int)PyList_Size(r);
+  for (int i = 0; i < n; ++i) {
+    PyObject* o = PyList_GetItem(r, i);
+    Py_INCREF(o);
+    outputs[i] = wrap<flexflow_tensor_t>(o);
+  }
+  Py_DECREF(r);
+  return n;
+}
+static PyObject* tensor_list(int n, const flexflow_tensor_t* xs) {
+  PyObject* l = PyList_New(n);
+  for (int i = 0; i < n; ++i) {
+    PyObject* o = obj(xs[i].impl);
+    Py_INCREF(o);
+    PyList_SET_ITEM(l, i, o);
+  }
+  return l;
+}
+int flexflow_model_add_split(flexflow_model_t m, flexflow_tensor_t x, int n, const int* sizes, int axis,
+                             flexflow_tensor_t* outputs, const char* name) {
+  init_once();
+  Gil gil;
+  return unpack(call("add_split", "(OONiz)", obj(m.impl), obj(x.impl), int_list(sizes, n), axis, name), outputs);
+}
+int flexflow_model_add_top_k(flexflow_model_t m, flexflow_tensor_t x, int k, bool sorted, flexflow_tensor_t* outputs,
+                             const char* name) {
+  init_once();
+  Gil gil;
+  return unpack(call("add_top_k", "(OOiiz)", obj(m.impl), obj(x.impl), k, (int)sorted, name), outputs);
+}
+int flexflow_model_add_group_by(flexflow_model_t m, flexflow_tensor_t data, flexflow_tensor_t assign, int n,
+                                float alpha, flexflow_tensor_t* outputs, const char* name) {
+  init_once();
+  Gil gil;
+  return unpack(call("add_group_by", "(OOOidz)", obj(m.impl), obj(data.impl), obj(assign.impl), n, (double)alpha,
+                     name),
+                outputs);
+}
+static flexflow_tensor_t aggregate(flexflow_model_t m, int ni, const flexflow_tensor_t* xs, int n, float lam, int spec,
+                                   const char* name) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(
+      call("add_aggregate", "(ONidiz)", obj(m.impl), tensor_list(ni, xs), n, (double)lam, spec, name));
+}
+flexflow_tensor_t flexflow_model_add_aggregate(flexflow_model_t m, int ni, const flexflow_tensor_t* xs, int n,
+                                               float lam, const char* name) {
+  return aggregate(m, ni, xs, n, lam, 0, name);
+}
+flexflow_tensor_t flexflow_model_add_aggregate_spec(flexflow_model_t m, int ni, const flexflow_tensor_t* xs, int n,
+                                                    float lam, const char* name) {
+  return aggregate(m, ni, xs, n, lam, 1, name);
+}
+flexflow_tensor_t flexflow_model_add_moe(flexflow_model_t m, flexflow_tensor_t x, int num_exp, int num_select,
+                                         int hidden, float alpha, float lam) {
+  init_once();
+  Gil gil;
+  return wrap<flexflow_tensor_t>(call("add_moe", "(OOiiidd)", obj(m.impl), obj(x.impl), num_exp, num_select, hidden,
+                                      (double)alpha, (double)lam));
+}
+bool flexflow_tensor_set_data_int64(flexflow_tensor_t h, flexflow_model_t m, const int64_t* d, int64_t n) {
+  return set_data(h, m, d, n, 42 /* DT_INT64 */);
+}
+void flexflow_model_print_layers(flexflow_model_t m, int id) {
+  init_once();
+  Gil gil;
+  as_bool_ok(call("model_print_layers", "(Oi)", obj(m.impl), id));
+}
+int flexflow_model_get_num_layers(flexflow_model_t m) {
+  init_once();
+  Gil gil;
+  PyObject* r = call("model_num_layers", "(O)", obj(m.impl));
+  if (!r) return -1;
+  const int n = (int)PyLong_AsLong(r);
+  Py_DECREF(r);
+  return n;
+}
+const char* flexflow_model_get_strategy_name(flexflow_model_t m) {
+  static thread_local std::string s;
+  init_once();
+  Gil gil;
+  PyObject* r = call("model_search_algo", "(O)", obj(m.impl));
+  s = r ? PyUnicode_AsUTF8(r) : "";
+  Py_XDECREF(r);
+  return s.c_str();
+}
+
 }  // extern "C"

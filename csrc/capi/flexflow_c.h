@@ -125,6 +125,48 @@ flexflow_tensor_t flexflow_model_add_reshape(flexflow_model_t handle, flexflow_t
 flexflow_tensor_t flexflow_model_add_transpose(flexflow_model_t handle, flexflow_tensor_t input, int num_dims,
                                                const int* perm, const char* name);
 
+flexflow_tensor_t flexflow_model_add_embedding_typed(flexflow_model_t handle, flexflow_tensor_t input, int num_entries,
+                                                     int out_dim, int aggr, int data_type, const char* name);
+flexflow_tensor_t flexflow_model_add_max(flexflow_model_t handle, flexflow_tensor_t x, flexflow_tensor_t y,
+                                         const char* name);
+flexflow_tensor_t flexflow_model_add_min(flexflow_model_t handle, flexflow_tensor_t x, flexflow_tensor_t y,
+                                         const char* name);
+flexflow_tensor_t flexflow_model_add_mean(flexflow_model_t handle, flexflow_tensor_t input, int n_dims,
+                                          const int* dims, bool keepdims, const char* name);
+flexflow_tensor_t flexflow_model_add_reduce_sum(flexflow_model_t handle, flexflow_tensor_t input, int n_axes,
+                                                const int* axes, bool keepdims, const char* name);
+flexflow_tensor_t flexflow_model_add_gather(flexflow_model_t handle, flexflow_tensor_t input, flexflow_tensor_t index,
+                                            int dim, const char* name);
+flexflow_tensor_t flexflow_model_add_cast(flexflow_model_t handle, flexflow_tensor_t input, int data_type,
+                                          const char* name);
+flexflow_tensor_t flexflow_model_add_rms_norm(flexflow_model_t handle, flexflow_tensor_t input, float eps,
+                                              const char* name);
+flexflow_tensor_t flexflow_model_add_reverse(flexflow_model_t handle, flexflow_tensor_t input, int axis,
+                                             const char* name);
+/* multi-output layers write their outputs to outputs[] (split: n, top_k: 2 = values, indices,
+ * group_by: n) and return how many they wrote, or -1 on error */
+int flexflow_model_add_split(flexflow_model_t handle, flexflow_tensor_t input, int n, const int* sizes, int axis,
+                             flexflow_tensor_t* outputs, const char* name);
+int flexflow_model_add_top_k(flexflow_model_t handle, flexflow_tensor_t input, int k, bool sorted,
+                             flexflow_tensor_t* outputs, const char* name);
+int flexflow_model_add_group_by(flexflow_model_t handle, flexflow_tensor_t data, flexflow_tensor_t assign, int n,
+                                float alpha, flexflow_tensor_t* outputs, const char* name);
+/* inputs: gate values, gate assignment, [gate predictions,] then n expert outputs (reference
+ * FFModel::aggregate / aggregate_spec) */
+flexflow_tensor_t flexflow_model_add_aggregate(flexflow_model_t handle, int n_inputs, const flexflow_tensor_t* inputs,
+                                               int n, float lambda_bal, const char* name);
+flexflow_tensor_t flexflow_model_add_aggregate_spec(flexflow_model_t handle, int n_inputs,
+                                                    const flexflow_tensor_t* inputs, int n, float lambda_bal,
+                                                    const char* name);
+/* composite mixture-of-experts layer: gate dense -> top_k -> group_by -> expert denses -> aggregate */
+flexflow_tensor_t flexflow_model_add_moe(flexflow_model_t handle, flexflow_tensor_t input, int num_exp, int num_select,
+                                         int expert_hidden_size, float alpha, float lambda_bal);
+bool flexflow_tensor_set_data_int64(flexflow_tensor_t handle, flexflow_model_t model, const int64_t* data, int64_t n);
+void flexflow_model_print_layers(flexflow_model_t handle, int id /* -1 = all */);
+int flexflow_model_get_num_layers(flexflow_model_t handle);
+/* name of the parallelization strategy chosen at compile ("" before compile); valid until the next call */
+const char* flexflow_model_get_strategy_name(flexflow_model_t handle);
+
 #ifdef __cplusplus
 }
 #endif

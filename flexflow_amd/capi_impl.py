@@ -161,3 +161,60 @@ def add_batch_norm(m, x, relu, name):
 
 def add_mha(m, q, k, v, embed, heads, kdim, vdim, dropout, bias, name):
     return m.multihead_attention(q, k, v, embed, heads, kdim, vdim, dropout, bool(bias), name=_name(name))
+
+
+def add_embedding_typed(m, x, num, dim, aggr, dtype, name):
+    return m.embedding(x, num, dim, AggrMode(aggr), dtype=DataType(dtype), name=_name(name))
+
+
+def add_split(m, x, sizes, axis, name):
+    return m.split(x, list(sizes), axis, name=_name(name))
+
+
+def add_top_k(m, x, k, sorted_, name):
+    return m.top_k(x, k, bool(sorted_), name=_name(name))
+
+
+def add_group_by(m, data, assign, n, alpha, name):
+    return m.group_by(data, assign, n, alpha, name=_name(name))
+
+
+def add_aggregate(m, xs, n, lambda_bal, spec, name):
+    f = m.aggregate_spec if spec else m.aggregate
+    return f(list(xs), n, lambda_bal, name=_name(name))
+
+
+def add_moe(m, x, num_exp, num_select, hidden, alpha, lambda_bal):
+    return m.moe(x, num_exp, num_select, hidden, alpha, lambda_bal)
+
+
+def add_reduce(m, op, x, dims, keepdims, name):
+    return getattr(m, op)(x, list(dims), bool(keepdims), name=_name(name))
+
+
+def add_gather(m, x, index, dim, name):
+    return m.gather(x, index, dim, name=_name(name))
+
+
+def add_cast(m, x, dtype, name):
+    return m.cast(x, DataType(dtype), name=_name(name))
+
+
+def add_rms_norm(m, x, eps, name):
+    return m.rms_norm(x, eps, name=_name(name))
+
+
+def add_reverse(m, x, axis, name):
+    return m.reverse(x, axis, name=_name(name))
+
+
+def model_print_layers(m, idx):
+    m.print_layers(idx)
+
+
+def model_num_layers(m):
+    return len(m._non_input_layers())
+
+
+def model_search_algo(m):
+    return str((m.search_report or {}).get("algo") or "")
