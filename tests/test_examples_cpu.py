@@ -59,6 +59,7 @@ CASES = [
     ("keras/seq_mnist_cnn_nested.py", ["--samples", "128"]),
     ("keras/seq_cifar10_cnn.py", ["--samples", "128"]),
     ("keras/func_cifar10_cnn_nested.py", ["--samples", "128"]),
+    ("keras/func_cifar10_cnn_concat.py", ["--samples", "128"]),
     ("keras/func_cifar10_cnn_concat_model.py", ["--samples", "128"]),
     ("keras/func_cifar10_cnn_concat_seq_model.py", ["--samples", "128"]),
     ("keras/func_cifar10_alexnet.py", ["--small", "--samples", "64"]),
