@@ -86,7 +86,10 @@ class FFConfig:
         self._traces: dict = {}
 
         self._discover_machine()
-        self.parse_args(sys.argv[1:] if argv is None else argv)
+        if argv is None:
+            from .jupyter import jupyter_argv  # notebook flags from a config file (flexflow_amd/jupyter.py)
+            argv = jupyter_argv() + sys.argv[1:]
+        self.parse_args(argv)
 
     # -------------------------------------------------------------------- machine
     def _discover_machine(self):

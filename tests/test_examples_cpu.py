@@ -78,6 +78,8 @@ CASES = [
     ("onnx/resnet.py", ["--small", "--samples", "32", "-b", "16"]),
     ("keras_exp/func_mnist_mlp_concat.py", ["--samples", "256"]),
     ("keras_exp/func_cifar10_cnn.py", ["--samples", "128"]),
+    ("bootcamp_demo/keras_cnn_cifar10.py", ["--samples", "128", "--epochs", "1"]),
+    ("bootcamp_demo/ff_alexnet_cifar10.py", ["--samples", "16", "-b", "8", "-e", "1"]),
     ("keras_exp/func_cifar10_cnn_concat.py", ["--samples", "128"]),
     ("keras_exp/func_cifar10_cnn_nested.py", ["--samples", "128"]),
 ]
