@@ -13,6 +13,9 @@
 //     gather: each input element sums dy over the outputs whose window it won — no atomics, no
 //     read of the whole window again. Average pooling follows torch's divisor rules
 //     (count_include_pad, windows clipped at the padded border).
+#include <algorithm>
+#include <stdexcept>
+
 #include "common.h"
 #include "ops.h"
 
@@ -62,13 +65,19 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   const int64_t M = (int64_t)N * HW;
   const int64_t j0 = M * s / S, j1 = M * (s + 1) / S;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-    const int64_t img = j / HW, hw = j - img * HW;
-    const float v = Cvt<T>::to_f(x[(img * C + c) * HW + hw]);
+  int64_t j = j0 + threadIdx.x;
+  int img = (int)(j / HW), hw = (int)(j - (int64_t)img * HW);
+  for (; j < j1; j += 256) {
+    const float v = Cvt<T>::to_f(x[((int64_t)img * C + c) * HW + hw]);
     n += 1.f;
     const float d = v - mean;
     mean += d / n;
     m2 += d * (v - mean);
+    hw += 256;
+    if (hw >= HW) {
+      img += hw / HW;
+      hw %= HW;
+    }
   }
   float v[3] = {n, mean, m2};
   block_fold<3>(v, sh, [](float* a, const float* b) { wf_merge(a[0], a[1], a[2], b[0], b[1], b[2]); });
@@ -104,14 +113,15 @@ __global__ void bn_running_kernel(const float* __restrict__ run_mean, const floa
   rstd_out[c] = rsqrtf(run_var[c] + eps);
 }
 
-template <typename T>
+// IT: uint32_t below 2^32 elements (32-bit channel index math), else int64_t
+template <typename T, typename IT>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
                                                        const T* __restrict__ g, const T* __restrict__ b, int64_t total,
                                                        int C, int HW, int relu) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c = (int)((i / HW) % C);
+  const IT stride = (IT)gridDim.x * blockDim.x;
+  for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < (IT)total; i += stride) {
+    const int c = (int)((i / (IT)HW) % (IT)C);
     float v = (Cvt<T>::to_f(x[i]) - mean[c]) * rstd[c] * Cvt<T>::to_f(g[c]) + Cvt<T>::to_f(b[c]);
     if (relu) v = fmaxf(v, 0.f);
     y[i] = Cvt<T>::from_f(v);
@@ -130,14 +140,20 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   const int64_t j0 = M * s / S, j1 = M * (s + 1) / S;
   const float mu = mean[c], rs = rstd[c], gc = Cvt<T>::to_f(g[c]), bc = Cvt<T>::to_f(b[c]);
   float s1 = 0.f, s2 = 0.f;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-    const int64_t img = j / HW, hw = j - img * HW;
-    const int64_t i = (img * C + c) * HW + hw;
+  int64_t j = j0 + threadIdx.x;
+  int img = (int)(j / HW), hw = (int)(j - (int64_t)img * HW);
+  for (; j < j1; j += 256) {
+    const int64_t i = ((int64_t)img * C + c) * HW + hw;
     const float xh = (Cvt<T>::to_f(x[i]) - mu) * rs;
     float d = Cvt<T>::to_f(dy[i]);
     if (relu && xh * gc + bc <= 0.f) d = 0.f;
     s1 += d;
     s2 += d * xh;
+    hw += 256;
+    if (hw >= HW) {
+      img += hw / HW;
+      hw %= HW;
+    }
   }
   float v[2] = {s1, s2};
   block_fold<2>(v, sh, [](float* a, const float* bb) { a[0] += bb[0]; a[1] += bb[1]; });
@@ -162,15 +178,15 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int C, in
   if (db) db[c] += s1;
 }
 
-template <typename T>
+template <typename T, typename IT>
 __global__ void __launch_bounds__(256) bn_bwd_dx_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
                                                         const T* __restrict__ g, const T* __restrict__ b,
                                                         const float* __restrict__ sums, T* __restrict__ dx,
                                                         int64_t total, int C, int HW, float inv_m, int relu) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c = (int)((i / HW) % C);
+  const IT stride = (IT)gridDim.x * blockDim.x;
+  for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < (IT)total; i += stride) {
+    const int c = (int)((i / (IT)HW) % (IT)C);
     const float rs = rstd[c], gc = Cvt<T>::to_f(g[c]);
     const float xh = (Cvt<T>::to_f(x[i]) - mean[c]) * rs;
     float d = Cvt<T>::to_f(dy[i]);
@@ -190,13 +206,21 @@ __global__ void __launch_bounds__(256) chan_sum_kernel(const T* __restrict__ dy,
   const int64_t M = (int64_t)N * HW;
   const int64_t j0 = M * s / S, j1 = M * (s + 1) / S;
   float acc = 0.f;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-    const int64_t img = j / HW, hw = j - img * HW;
-    const int64_t i = (img * C + c) * HW + hw;
+  // (image, pixel) of this thread's first element by one division, then advanced incrementally
+  // (a 64-bit division per element was most of this kernel's time)
+  int64_t j = j0 + threadIdx.x;
+  int img = (int)(j / HW), hw = (int)(j - (int64_t)img * HW);
+  for (; j < j1; j += 256) {
+    const int64_t i = ((int64_t)img * C + c) * HW + hw;
     float d = Cvt<T>::to_f(dy[i]);
     if (y && !(Cvt<T>::to_f(y[i]) > 0.f)) d = 0.f;
     if (dz) dz[i] = Cvt<T>::from_f(d);
     acc += d;
+    hw += 256;
+    if (hw >= HW) {
+      img += hw / HW;
+      hw %= HW;
+    }
   }
   float v[1] = {acc};
   block_fold<1>(v, sh, [](float* a, const float* b) { a[0] += b[0]; });
@@ -238,8 +262,12 @@ void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b,
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps, mean,
                        rstd);
   }
-  DT_DISPATCH(dt, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
-                                     (T*)y, mean, rstd, (const T*)g, (const T*)b, total, C, HW, relu));
+  if (total < (1ll << 31))
+    DT_DISPATCH(dt, hipLaunchKernelGGL((bn_apply_kernel<T, uint32_t>), dim3(ew_grid(total, 256)), dim3(256), 0, st,
+                                       (const T*)x, (T*)y, mean, rstd, (const T*)g, (const T*)b, total, C, HW, relu));
+  else
+    DT_DISPATCH(dt, hipLaunchKernelGGL((bn_apply_kernel<T, int64_t>), dim3(ew_grid(total, 256)), dim3(256), 0, st,
+                                       (const T*)x, (T*)y, mean, rstd, (const T*)g, (const T*)b, total, C, HW, relu));
 }
 
 void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const void* b, const float* mean,
@@ -252,9 +280,15 @@ void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const v
   DT_DISPATCH(dt, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(C, S), dim3(256), 0, st, (const T*)x, (const T*)dy,
                                      mean, rstd, (const T*)g, (const T*)b, ws, N, C, HW, S, relu));
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, C, S, sums, dg, db);
-  DT_DISPATCH(dt, hipLaunchKernelGGL(bn_bwd_dx_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
-                                     (const T*)dy, mean, rstd, (const T*)g, (const T*)b, sums, (T*)dx, total, C, HW,
-                                     1.f / (float)((int64_t)N * HW), relu));
+  const float inv_m = 1.f / (float)((int64_t)N * HW);
+  if (total < (1ll << 31))
+    DT_DISPATCH(dt, hipLaunchKernelGGL((bn_bwd_dx_kernel<T, uint32_t>), dim3(ew_grid(total, 256)), dim3(256), 0, st,
+                                       (const T*)x, (const T*)dy, mean, rstd, (const T*)g, (const T*)b, sums, (T*)dx,
+                                       total, C, HW, inv_m, relu));
+  else
+    DT_DISPATCH(dt, hipLaunchKernelGGL((bn_bwd_dx_kernel<T, int64_t>), dim3(ew_grid(total, 256)), dim3(256), 0, st,
+                                       (const T*)x, (const T*)dy, mean, rstd, (const T*)g, (const T*)b, sums, (T*)dx,
+                                       total, C, HW, inv_m, relu));
 }
 
 void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, float* ws, int N, int C, int HW,
@@ -282,52 +316,97 @@ __device__ __forceinline__ float pool_divisor(const PoolGeom& p, int oh, int ow,
   return (float)(include_pad ? full : (h1 - h0) * (w1 - w0));
 }
 
+// output-centric forward: one thread per output, 32-bit index math (64-bit division per element
+// was the kernel's cost), the divisor once per output
 template <typename T>
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        uint8_t* __restrict__ idx, PoolGeom p, int is_max,
                                                        int include_pad, int relu) {
-  const int64_t total = (int64_t)p.N * p.C * p.OH * p.OW;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
-    const int ow = (int)(o % p.OW), oh = (int)((o / p.OW) % p.OH);
-    const int64_t nc = o / ((int64_t)p.OW * p.OH);
-    const T* xp = x + nc * p.H * p.W;
+  const unsigned total = (unsigned)p.N * p.C * p.OH * p.OW;
+  const unsigned ohw = (unsigned)p.OH * p.OW;
+  for (unsigned o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const unsigned nc = o / ohw, r = o - nc * ohw;
+    const int oh = (int)(r / (unsigned)p.OW), ow = (int)(r - (unsigned)oh * p.OW);
+    const T* xp = x + (size_t)nc * p.H * p.W;
     const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
-    float r;
+    const int i0 = max(0, -h0), i1 = min(p.kh, p.H - h0), j0 = max(0, -w0), j1 = min(p.kw, p.W - w0);
+    float res;
     if (is_max) {
       float best = -INFINITY;
       int bi = 0;
-      for (int i = 0; i < p.kh; ++i) {
-        const int ih = h0 + i;
-        if (ih < 0 || ih >= p.H) continue;
-        for (int j = 0; j < p.kw; ++j) {
-          const int iw = w0 + j;
-          if (iw < 0 || iw >= p.W) continue;
-          const float v = Cvt<T>::to_f(xp[ih * p.W + iw]);
+      for (int i = i0; i < i1; ++i)
+        for (int j = j0; j < j1; ++j) {
+          const float v = Cvt<T>::to_f(xp[(h0 + i) * p.W + w0 + j]);
           if (v > best || v != v) { best = v; bi = i * p.kw + j; }
         }
-      }
-      r = best;
+      res = best;
       if (idx) idx[o] = (uint8_t)bi;
     } else {
-      float s = 0.f;
-      for (int i = 0; i < p.kh; ++i) {
-        const int ih = h0 + i;
-        if (ih < 0 || ih >= p.H) continue;
-        for (int j = 0; j < p.kw; ++j) {
-          const int iw = w0 + j;
-          if (iw >= 0 && iw < p.W) s += Cvt<T>::to_f(xp[ih * p.W + iw]);
-        }
-      }
-      r = s / pool_divisor(p, oh, ow, include_pad);
+      float sum = 0.f;
+      for (int i = i0; i < i1; ++i)
+        for (int j = j0; j < j1; ++j) sum += Cvt<T>::to_f(xp[(h0 + i) * p.W + w0 + j]);
+      res = sum / pool_divisor(p, oh, ow, include_pad);
     }
-    if (relu) r = fmaxf(r, 0.f);
-    y[o] = Cvt<T>::from_f(r);
+    if (relu) res = fmaxf(res, 0.f);
+    y[o] = Cvt<T>::from_f(res);
   }
 }
 
-// one thread per input element: sum dy over the outputs whose window covers it (max: whose
-// recorded winner it is); relu after the pool masks by the output (avg) or the winner itself (max)
+// input-centric backward over whole planes: a workgroup stages P planes of dy (avg: pre-divided
+// and ReLU-masked by y; max: dy and the winner bytes) in LDS, then every input element sums the
+// outputs whose window covers it (max: whose recorded winner it is) from LDS
+template <typename T, bool MAX>
+__global__ void __launch_bounds__(256) pool_bwd_plane_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                                                             const T* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                                                             PoolGeom p, int include_pad, int relu, int P) {
+  extern __shared__ float sdy[];
+  const int nplanes = p.N * p.C;
+  const int pl0 = blockIdx.x * P, np = min(P, nplanes - pl0);
+  const int nout = p.OH * p.OW, HW = p.H * p.W;
+  uint8_t* sidx = reinterpret_cast<uint8_t*>(sdy + P * nout);
+  const size_t obase = (size_t)pl0 * nout;
+  for (int k = threadIdx.x; k < np * nout; k += 256) {
+    float v = Cvt<T>::to_f(dy[obase + k]);
+    if (MAX) {
+      sidx[k] = idx[obase + k];
+    } else {
+      const int r = k % nout, oh = r / p.OW, ow = r - oh * p.OW;
+      if (relu && !(Cvt<T>::to_f(y[obase + k]) > 0.f)) v = 0.f;
+      v /= pool_divisor(p, oh, ow, include_pad);
+    }
+    sdy[k] = v;
+  }
+  __syncthreads();
+  const size_t ibase = (size_t)pl0 * HW;
+  for (int k = threadIdx.x; k < np * HW; k += 256) {
+    const int pl = k / HW, r = k - pl * HW;
+    const int ih = r / p.W, iw = r - ih * p.W;
+    // outputs oh with oh*sh - ph <= ih < oh*sh - ph + kh
+    const int oh0 = ih + p.ph - p.kh < 0 ? 0 : (ih + p.ph - p.kh) / p.sh + 1;
+    const int oh1 = min((ih + p.ph) / p.sh, p.OH - 1);
+    const int ow0 = iw + p.pw - p.kw < 0 ? 0 : (iw + p.pw - p.kw) / p.sw + 1;
+    const int ow1 = min((iw + p.pw) / p.sw, p.OW - 1);
+    const float* sp = sdy + pl * nout;
+    float g = 0.f;
+    if (MAX) {
+      if (!(relu && !(Cvt<T>::to_f(x[ibase + k]) > 0.f))) {  // a window it won has output relu(x) = 0
+        const uint8_t* ip = sidx + pl * nout;
+        for (int oh = oh0; oh <= oh1; ++oh) {
+          const int wi = (ih - (oh * p.sh - p.ph)) * p.kw + iw + p.pw;
+          for (int ow = ow0; ow <= ow1; ++ow)
+            if (ip[oh * p.OW + ow] == wi - ow * p.sw) g += sp[oh * p.OW + ow];
+        }
+      }
+    } else {
+      for (int oh = oh0; oh <= oh1; ++oh)
+        for (int ow = ow0; ow <= ow1; ++ow) g += sp[oh * p.OW + ow];
+    }
+    dx[ibase + k] = Cvt<T>::from_f(g);
+  }
+}
+
+// fallback for planes too large for LDS: one thread per input element, reading dy from memory
 template <typename T>
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
                                                        const T* __restrict__ dy, const uint8_t* __restrict__ idx,
@@ -339,15 +418,12 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ x, 
     const int iw = (int)(i % p.W), ih = (int)((i / p.W) % p.H);
     const int64_t nc = i / ((int64_t)p.W * p.H);
     const int64_t ob = nc * p.OH * p.OW;
-    // outputs oh with oh*sh - ph <= ih < oh*sh - ph + kh
     const int oh0 = ih + p.ph - p.kh < 0 ? 0 : (ih + p.ph - p.kh) / p.sh + 1;
     const int oh1 = min((ih + p.ph) / p.sh, p.OH - 1);
     const int ow0 = iw + p.pw - p.kw < 0 ? 0 : (iw + p.pw - p.kw) / p.sw + 1;
     const int ow1 = min((iw + p.pw) / p.sw, p.OW - 1);
     float g = 0.f;
-    if (is_max && relu && !(Cvt<T>::to_f(x[i]) > 0.f)) {
-      g = 0.f;  // a window this element won has output relu(x) = 0
-    } else {
+    if (!(is_max && relu && !(Cvt<T>::to_f(x[i]) > 0.f))) {
       for (int oh = oh0; oh <= oh1; ++oh) {
         for (int ow = ow0; ow <= ow1; ++ow) {
           const int64_t o = ob + (int64_t)oh * p.OW + ow;
@@ -369,20 +445,35 @@ void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, i
                 hipStream_t st) {
   const PoolGeom p{geom[0], geom[1], geom[2], geom[3], geom[4],  geom[5],  geom[6],
                    geom[7], geom[8], geom[9], geom[10], geom[11], geom[12], geom[13]};
-  const int N = p.N, C = p.C, OH = p.OH, OW = p.OW;
-  const int64_t total = (int64_t)N * C * OH * OW;
+  const int64_t total = (int64_t)p.N * p.C * p.OH * p.OW;
   if (total == 0) return;
-  DT_DISPATCH(dt, hipLaunchKernelGGL(pool_fwd_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
-                                     (T*)y, idx, p, is_max, include_pad, relu));
+  if (total >= (1ll << 31) || (int64_t)p.N * p.C * p.H * p.W >= (1ll << 31))
+    throw std::runtime_error("pool2d: tensors of 2^31 or more elements are not supported");
+  DT_DISPATCH(dt, hipLaunchKernelGGL(pool_fwd_kernel<T>, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)),
+                                     dim3(256), 0, st, (const T*)x, (T*)y, idx, p, is_max, include_pad, relu));
 }
 
 void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint8_t* idx, void* dx, const int* geom,
                 int is_max, int include_pad, int relu, hipStream_t st) {
   const PoolGeom p{geom[0], geom[1], geom[2], geom[3], geom[4],  geom[5],  geom[6],
                    geom[7], geom[8], geom[9], geom[10], geom[11], geom[12], geom[13]};
-  const int N = p.N, C = p.C, H = p.H, W = p.W;
-  const int64_t total = (int64_t)N * C * H * W;
+  const int64_t total = (int64_t)p.N * p.C * p.H * p.W;
   if (total == 0) return;
+  const int nout = p.OH * p.OW, HW = p.H * p.W, nplanes = p.N * p.C;
+  constexpr int LDS_BYTES = 64 * 1024;
+  if (total < (1ll << 31) && nout * 5 <= LDS_BYTES) {
+    // planes per workgroup: ~2K input elements of work, within the LDS budget
+    const int P = std::max(1, std::min({2048 / std::max(HW, 1), LDS_BYTES / (nout * 5), 64}));
+    const unsigned grid = (unsigned)((nplanes + P - 1) / P);
+    const size_t lds = (size_t)P * nout * (is_max ? 5 : 4);
+    if (is_max)
+      DT_DISPATCH(dt, hipLaunchKernelGGL((pool_bwd_plane_kernel<T, true>), dim3(grid), dim3(256), lds, st,
+                                         (const T*)x, (const T*)y, (const T*)dy, idx, (T*)dx, p, include_pad, relu, P));
+    else
+      DT_DISPATCH(dt, hipLaunchKernelGGL((pool_bwd_plane_kernel<T, false>), dim3(grid), dim3(256), lds, st,
+                                         (const T*)x, (const T*)y, (const T*)dy, idx, (T*)dx, p, include_pad, relu, P));
+    return;
+  }
   DT_DISPATCH(dt, hipLaunchKernelGGL(pool_bwd_kernel<T>, dim3(ew_grid(total, 256)), dim3(256), 0, st, (const T*)x,
                                      (const T*)y, (const T*)dy, idx, (T*)dx, p, is_max, include_pad, relu));
 }

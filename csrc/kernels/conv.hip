@@ -43,28 +43,37 @@ __device__ __forceinline__ int off32(int r, int c) { return r * 64 + ((c ^ ((r >
 
 // ------------------------------------------------------------------------------- re-layouts
 // x [N][G*Cg][HW] -> xt [N][HW][G][Cp] (channels zero-padded to Cp per group)
+// A workgroup transposes a 64-pixel x 64-channel tile of one (image, group) through LDS: loads are
+// one channel row of 64 consecutive pixels per wave instruction, stores are whole 16-B
+// 8-channel chunks, consecutive lanes on consecutive chunks / pixels (the pixel-per-thread
+// version with 64-bit index math and pixel-strided 16-B stores ran at ~1 TB/s)
+constexpr int NHWC_ROW = 72;  // LDS row (one pixel): 64 channels + 8 pad, 144 B (16-B aligned)
 __global__ void __launch_bounds__(256) conv_nhwc_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xt, int N,
                                                         int G, int Cg, int HW, int Cp) {
-  const int C8 = Cp / 8;
-  const int64_t total = (int64_t)N * G * C8 * HW;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int hw = (int)(i % HW);
-    int64_t r = i / HW;
-    const int c8 = (int)(r % C8); r /= C8;
-    const int g = (int)(r % G);
-    const int64_t n = r / G;
-    uint16_t v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c8 * 8 + j;
-      v[j] = c < Cg ? x[((n * G + g) * Cg + c) * HW + hw] : (uint16_t)0;
-    }
-    uint4 o;
-    o.x = v[0] | ((uint32_t)v[1] << 16); o.y = v[2] | ((uint32_t)v[3] << 16);
-    o.z = v[4] | ((uint32_t)v[5] << 16); o.w = v[6] | ((uint32_t)v[7] << 16);
-    *reinterpret_cast<uint4*>(xt + ((n * HW + hw) * G + g) * Cp + c8 * 8) = o;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64 * NHWC_ROW];
+  const int hw0 = blockIdx.x * 64, ct = blockIdx.y;
+  const int ng = blockIdx.z, n = ng / G, g = ng - n * G;
+  const int c0 = ct * 64;
+  const int t = threadIdx.x, px = t & 63;
+  const bf16_t* src = x + ((int64_t)n * G + g) * Cg * HW;
+#pragma unroll 4
+  for (int r = t >> 6; r < 64; r += 4) {
+    const int c = c0 + r, hw = hw0 + px;
+    tile[px * NHWC_ROW + r] = (c < Cg && hw < HW) ? src[(int64_t)c * HW + hw] : (uint16_t)0;
   }
+  __syncthreads();
+  const int nch = min(8, (Cp - c0) / 8);  // 8-channel chunks of this tile inside Cp
+  for (int k = t; k < 64 * 8; k += 256) {
+    const int pi = k >> 3, ch = k & 7, hw = hw0 + pi;
+    if (ch < nch && hw < HW)
+      *reinterpret_cast<uint4*>(xt + (((int64_t)n * HW + hw) * G + g) * Cp + c0 + ch * 8) =
+          *reinterpret_cast<const uint4*>(tile + pi * NHWC_ROW + ch * 8);
+  }
+}
+
+static void launch_nhwc(const bf16_t* x, bf16_t* xt, int N, int G, int Cg, int HW, int Cp, hipStream_t st) {
+  const dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((Cp + 63) / 64), (unsigned)(N * G));
+  hipLaunchKernelGGL(conv_nhwc_kernel, grid, dim3(256), 0, st, x, xt, N, G, Cg, HW, Cp);
 }
 
 // w [G*Kg][Cg][KH][KW] -> wp [G][Kg][KH][KW][Cp] + zero tail to Kp per row (forward operand), or
@@ -405,8 +414,7 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   bf16_t* xt = (bf16_t*)ws;
   bf16_t* wp = xt + (int64_t)N * H * W * G * Cp + (int64_t)N * OH * OW * G * round8(Kg);
   const int Kp = kpad(KH, KW, Cp);
-  hipLaunchKernelGGL(conv_nhwc_kernel, dim3(ew_grid((int64_t)N * G * (Cp / 8) * H * W, 256)), dim3(256), 0, st,
-                     (const bf16_t*)x, xt, N, G, Cg, H * W, Cp);
+  launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Kg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                      wp, G, Kg, Cg, KH, KW, Kp, 0);
   IGemmArgs a{wp, xt, (bf16_t*)y, (const bf16_t*)bias, N, G, Kg, Kp, H, W, Cp, OH, OW, KH, KW, sh, sw, ph, pw, relu};
@@ -421,8 +429,7 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
   bf16_t* xt = (bf16_t*)ws;
   bf16_t* yt = xt + (int64_t)N * H * W * G * Cp;
   bf16_t* wp = yt + (int64_t)N * OH * OW * G * Kgp;
-  hipLaunchKernelGGL(conv_nhwc_kernel, dim3(ew_grid((int64_t)N * G * (Kgp / 8) * OH * OW, 256)), dim3(256), 0, st,
-                     (const bf16_t*)dy, yt, N, G, Kg, OH * OW, Kgp);
+  launch_nhwc((const bf16_t*)dy, yt, N, G, Kg, OH * OW, Kgp, st);
   if (need_dx) {
     const int Kp = kpad(KH, KW, Kgp);
     hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
@@ -432,8 +439,7 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
   }
   if (dw) {
     // the forward's channel-last input copy is rebuilt here (the workspace is per call)
-    hipLaunchKernelGGL(conv_nhwc_kernel, dim3(ew_grid((int64_t)N * G * (Cp / 8) * H * W, 256)), dim3(256), 0, st,
-                       (const bf16_t*)x, xt, N, G, Cg, H * W, Cp);
+    launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
     // 64-channel tiles (the 128-channel variant measured no faster); split the pixels so that
     // about 1k workgroups run, each over at least 16 steps of 64 pixels (2k workgroups of 8+
     // steps measured slower: more atomics, more prologues; scripts/conv_probe.py)

@@ -505,6 +505,27 @@ def test_pool2d(k, s, p, is_max, inc, relu, dtype):
     assert _rel(dx, xr.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
 
 
+@pytest.mark.parametrize("shape,k,s,p,is_max", [((8, 32, 35, 35), 3, 1, 1, False),   # Inception A/C/E pools
+                                                 ((4, 16, 147, 147), 3, 2, 0, True),  # Inception stem
+                                                 ((2, 3, 64, 48), 3, 3, 1, True),
+                                                 ((1, 2, 260, 260), 2, 1, 0, False),  # plane past LDS: fallback
+                                                 ((1, 2, 260, 260), 2, 1, 0, True)])
+def test_pool2d_planes(shape, k, s, p, is_max):
+    """Large-plane pooling: the LDS plane-staged backward (several planes per workgroup) and the
+    memory-gather fallback for planes too large for LDS, against torch fp32."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(24)
+    x = torch.randn(*shape, device=DEV).bfloat16()
+    y, idx = K.pool2d_fwd(x, k, k, s, s, (p, p, p, p), is_max, True, False, True)
+    xr = x.float().requires_grad_()
+    ref = K._pool_ref(xr, k, k, s, s, (p, p, p, p), is_max, True, False)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dx = K.pool2d_bwd(x, y, dy, idx, k, k, s, s, (p, p, p, p), is_max, True, False)
+    assert _rel(dx, xr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("is_max,inc", [(True, True), (False, True), (False, False)])
 def test_pool2d_asymmetric_pads(is_max, inc):
     """A spatially split block pads only its global edges: (top, bottom, left, right) pads."""
@@ -530,6 +551,8 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     (2, 32, 9, 9, 64, (3, 3), (1, 1), (1, 1), 4),
     (3, 20, 11, 13, 36, (5, 3), (2, 1), (2, 1), 1),
     (1, 130, 17, 17, 200, (1, 7), (1, 1), (0, 3), 1),   # Inception 1x7, channels past one tile
+    (2, 192, 35, 35, 64, (1, 1), (1, 1), (0, 0), 1),   # Inception A 1x1: 3 channel tiles, odd HW
+    (2, 64, 16, 16, 64, (3, 3), (1, 1), (1, 1), 32),   # ResNeXt grouped 3x3: Cp = 8 per group
 ])
 def test_conv2d_implicit_gemm(geo):
     """Our implicit-GEMM MFMA convolution (forward with bias + ReLU, backward data, backward filter
