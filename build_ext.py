@@ -84,7 +84,8 @@ def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-L", tlib, f"-Wl,-rpath,{tlib}",
               "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
               "-lhipblaslt",  # torch/lib copy (same soname as the one libtorch_hip loads)
-              "-o", out])
+              "-o", out + ".tmp"])
+        os.replace(out + ".tmp", out)  # atomic: a concurrent tree snapshot never sees a partial .so
     if verbose:
         print(f"[build_ext] {len(jobs_list)} kernel objects rebuilt -> {out}")
     return out

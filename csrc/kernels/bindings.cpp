@@ -73,6 +73,38 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
   ffk::gemm_bf16(p, cur_stream());
 }
 
+// C = (A.B) * act'(zin) [+ dbias += colsum] in one 256-row MFMA GEMM; false if the shape does not fit
+bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias, int64_t M, int64_t N, int64_t K,
+               int64_t lda, int64_t ldb, int64_t ldc, bool a_k, bool b_k, int64_t act) {
+  check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C"); check_dev(zin, "zin");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+              C.scalar_type() == at::kBFloat16 && zin.scalar_type() == at::kBFloat16, "gemm_dact: bf16 operands");
+  TORCH_CHECK((a_k ? (M - 1) * lda + K : (K - 1) * lda + M) <= A.numel(), "gemm_dact: A too small");
+  TORCH_CHECK((b_k ? (N - 1) * ldb + K : (K - 1) * ldb + N) <= B.numel(), "gemm_dact: B too small");
+  TORCH_CHECK((M - 1) * ldc + N <= C.numel() && (M - 1) * ldc + N <= zin.numel(), "gemm_dact: C / zin too small");
+  const bool has_db = dbias.has_value() && dbias->defined();
+  if (has_db) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->numel() >= N, "gemm_dact: dbias");
+  ffk::GemmArgs p;
+  p.A = reinterpret_cast<const uint16_t*>(A.data_ptr());
+  p.B = reinterpret_cast<const uint16_t*>(B.data_ptr());
+  p.C = C.data_ptr();
+  p.zin = zin.data_ptr();
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.act = act;
+  p.a_kcontig = a_k; p.b_kcontig = b_k;
+  p.a_bytes = A.numel() * 2;
+  p.b_bytes = B.numel() * 2;
+  const int64_t rows = 2 * ((M + 255) / 256);
+  Tensor part;
+  if (has_db) {
+    part = at::empty({rows * N}, C.options().dtype(at::kFloat));
+    p.colpart = part.data_ptr<float>();
+  }
+  if (!ffk::gemm_dact_bf16(p, cur_stream())) return false;
+  if (has_db) ffk::col_reduce_add(p.colpart, dbias->data_ptr<float>(), (int)rows, (int)N, cur_stream());
+  return true;
+}
+
 int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t impl) {
   return ffk::gemm_pick_splitk(M, N, K, batch, (int)impl);
 }
@@ -450,6 +482,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
         py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2);
+  m.def("gemm_dact", &gemm_dact);
   m.def("lstm_fwd_cell", &lstm_fwd_cell);
   m.def("lstm_bwd_cell", &lstm_bwd_cell);
   m.def("lt_plan", &lt_plan);

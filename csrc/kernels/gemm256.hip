@@ -259,6 +259,27 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
     OutT2* C = OUT_MODE == 2 ? nullptr : reinterpret_cast<OutT2*>(p.C) + (int64_t)b * p.sC;
     bf16_t* Zp = p.Z ? reinterpret_cast<bf16_t*>(p.Z) + (int64_t)b * p.sC : nullptr;
     float* W = OUT_MODE == 2 ? p.ws + (int64_t)z * p.M * p.N : nullptr;
+    constexpr int CPR = WN / 8;  // 8-column chunks per row; a lane's chunk (lane % CPR) is fixed
+    const bf16_t* Zin = reinterpret_cast<const bf16_t*>(p.zin);
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of this lane's chunk
+    // dact: every pre-activation chunk this lane will need is requested up front (16 x 16 B in
+    // flight per lane; the fragment registers of the main loop are dead by now), so the tile pays
+    // one HBM latency instead of one per row group
+    constexpr int ITS = 32 * CPR / 64;
+    uint4 zpre[OUT_MODE == 0 ? 4 * ITS : 1];
+    if (OUT_MODE == 0 && p.dact) {
+#pragma unroll
+      for (int qtr = 0; qtr < 4; ++qtr)
+#pragma unroll
+        for (int it = 0; it < ITS; ++it) {
+          const int idx = it * 64 + lane;
+          const int m = m0 + wr * 128 + qtr * 32 + idx / CPR;
+          const int n = n0 + wc * WN + (idx % CPR) * 8;
+          zpre[qtr * ITS + it] = (m < p.M && n < p.N)
+                                     ? *reinterpret_cast<const uint4*>(Zin + (int64_t)m * p.ldc + n)
+                                     : make_uint4(0, 0, 0, 0);
+        }
+    }
 #pragma unroll
     for (int qtr = 0; qtr < 4; ++qtr) {
 #pragma unroll
@@ -269,7 +290,6 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
           *reinterpret_cast<float4*>(st + (i * 16 + (lane & 15)) * LDW + j * 16 + (lane >> 4) * 4) =
               make_float4(v[0] * p.alpha, v[1] * p.alpha, v[2] * p.alpha, v[3] * p.alpha);
         }
-      constexpr int CPR = WN / 8;  // 8-column chunks per row
 #pragma unroll
       for (int it = 0; it < 32 * CPR / 64; ++it) {
         const int idx = it * 64 + lane;
@@ -287,6 +307,20 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
           continue;
         }
         OutT2* dst = C + (int64_t)m * p.ldc + n;
+        if (OUT_MODE == 0 && p.dact) {
+          // consumer dgrad * producer act'(pre-activation); the column sums feed the producer's
+          // bias gradient (the separate bias_act_bwd pass re-read and re-wrote this whole tile)
+          float zz[8];
+          const uint4 zv = zpre[OUT_MODE == 0 ? qtr * ITS + it : 0];
+          load16(reinterpret_cast<const bf16_t*>(&zv), zz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            x[e] *= act_grad(p.act, zz[e]);
+            cs[e] += x[e];
+          }
+          store16(reinterpret_cast<bf16_t*>(dst), x);
+          continue;
+        }
         if (p.beta != 0.f) {
           float c[8];
           if (OUT_MODE == 0) load16(reinterpret_cast<const bf16_t*>(dst), c);
@@ -318,6 +352,20 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
           reinterpret_cast<float4*>(dst)[0] = make_float4(x[0], x[1], x[2], x[3]);
           reinterpret_cast<float4*>(dst)[1] = make_float4(x[4], x[5], x[6], x[7]);
         }
+      }
+    }
+    if (OUT_MODE == 0 && p.dact && p.colpart) {
+      // fold the 64 / CPR lanes that share a column chunk, then one lane per chunk stores the
+      // wave's 128-row partial (row tile_m * 2 + wr of the [2 tm][N] slab; summed by col_reduce_add)
+#pragma unroll
+      for (int sh = CPR; sh < 64; sh <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], sh);
+      const int n = n0 + wc * WN + lane * 8;
+      if (lane < CPR && n < p.N) {
+        float4* d = reinterpret_cast<float4*>(p.colpart + (int64_t)(tile_m * 2 + wr) * p.N + n);
+        d[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        d[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
     }
     return;
@@ -440,6 +488,19 @@ bool gemm256_bf16(const GemmArgs& p0, int64_t a_bytes, int64_t b_bytes, hipStrea
   if (bn == 256) launch_mode<256>(p, grid, stream, a_bytes, b_bytes, mode);
   else launch_mode<128>(p, grid, stream, a_bytes, b_bytes, mode);
   return true;
+}
+
+bool gemm_dact_bf16(GemmArgs p, hipStream_t stream) {
+  if (p.M <= 0 || p.N <= 0) return true;
+  if (!p.zin || p.out_f32 || p.batch != 1 || p.beta != 0.f || p.bias || p.Z || p.act == ACT_NONE) return false;
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (p.N % 8 || p.ldc % 8 || !al16(p.C) || !al16(p.zin) || (p.colpart && !al16(p.colpart))) return false;
+  p.vec8_ok = true;
+  p.vec_ok = true;
+  p.dact = true;
+  p.splitk = 1;
+  p.ws = nullptr;
+  return gemm256_bf16(p, p.a_bytes, p.b_bytes, stream);
 }
 
 }  // namespace ffk

@@ -452,6 +452,7 @@ class FFModel:
         if os.environ.get("FF_NO_INPLACE") != "1":
             self.executor._plan_inplace()
         self.executor._plan_bias_grad_fusion()
+        self.executor._plan_dact_fusion()
         if self.optimizer is not None and training:
             self.executor.init_optimizer(self.optimizer)
         for guid, v in self._pending_values.items():

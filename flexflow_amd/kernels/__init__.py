@@ -409,6 +409,51 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
     return C
 
 
+def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
+    """C = (op(A).op(B)) * act'(Zp); db (fp32, optional) += colsum(C): the dgrad GEMM of a Linear
+    fused with the activation backward of the Linear that produced its input (BERT: FFN2's dgrad
+    and FFN1's GELU'). Autotuned per call site between the fused 256-row MFMA kernel
+    (csrc/kernels/gemm256.hip dact epilogue) and the plain GEMM followed by an in-place
+    bias_act_bwd pass (what the two ops run unfused)."""
+    if not native(C) or C.dtype != torch.bfloat16:
+        r = A.float() @ B.float().t() if b_k else A.float() @ B.float()
+        r = r * act_grad_ref(Zp.float(), act)
+        C.copy_(r)
+        if db is not None:
+            db.add_(r.sum(0))
+        return C
+    X = ext()
+
+    def fused(out=C, dbo=db):
+        return X.gemm_dact(A, B, out, Zp, dbo, M, N, K, lda, ldb, ldc, a_k, b_k, act)
+
+    def unfused(out=C, dbo=db):
+        gemm(A, B, out, M, N, K, a_k, b_k, lda, ldb, ldc)
+        X.bias_act_bwd(out, Zp, out, dbo, M, N, act)
+
+    key = ("dact", M, N, K, a_k, b_k, lda, ldb, ldc, act, db is not None)
+    choice = _tuned.get(key)
+    if choice is None:
+        if not _TUNE or torch.cuda.is_current_stream_capturing():
+            choice = "fused"
+        else:
+            scratch = torch.empty_like(C)
+            dbs = torch.zeros_like(db) if db is not None else None
+            if not fused(scratch, dbs):
+                choice = "unfused"
+            else:
+                unfused(scratch, dbs)  # tune the plain GEMM's call site outside the timing
+                times = {"fused": _time(lambda: fused(scratch, dbs)), "unfused": _time(lambda: unfused(scratch, dbs))}
+                choice = min(times, key=lambda k: times[k])
+                TUNE_LOG.append({"op": "gemm_dact", "M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "act": act,
+                                 "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
+        _tuned[key] = choice
+    if choice == "fused" and fused():
+        return C
+    unfused()
+    return C
+
+
 def linear_fwd(x2d, w, bias, act, save_z):
     """y = act(x.w^T + b) for x2d [M,K], w [N,K]. Returns (y, z_or_None)."""
     M, K = x2d.shape
@@ -427,10 +472,12 @@ def linear_fwd(x2d, w, bias, act, save_z):
     return y, z
 
 
-def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None):
+def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None):
     """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+= ; dw_beta=0 overwrites dw
     when the executor knows this op is the weight's only user). dx_out: an existing input gradient
-    [M, K] to accumulate into (dgrad GEMM with beta = 1, no separate add). Returns dx (or None)."""
+    [M, K] to accumulate into (dgrad GEMM with beta = 1, no separate add). dact = (z, act, db) of
+    the Linear that produced x: the returned dx is then already that producer's pre-activation
+    gradient (and its bias gradient is summed), see gemm_dact. Returns dx (or None)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     if act != ACT_NONE:
@@ -440,6 +487,11 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
         if db is not None:
             bias_grad(dz, db)
     dx = None
+    if dact is not None:
+        assert need_dx and dx_out is None
+        dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
+        gemm_dact(dz, w, dx, dact[0], dact[2], M, K, N, True, False, N, K, K, dact[1])
+        need_dx = False
     if native(dy2d) and dy2d.dtype == torch.bfloat16:
         if need_dx:
             if dx_out is not None:

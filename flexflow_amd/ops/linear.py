@@ -88,12 +88,26 @@ class Linear(OpImpl):
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         dw = ctx.wgrads[0] if ctx.wgrads else None
         db = ctx.wgrads[1] if (len(ctx.wgrads) > 1 and ctx.saved["has_b"]) else None
+        act = self.act
         if ctx.extra.get("bias_grad_fused"):  # the consuming LayerNorm's backward already summed it
             db = None
+        if ctx.extra.get("dact_fused"):
+            # the consuming Linear's dgrad GEMM already applied act' and summed the bias gradient
+            act, z, db = K.ACT_NONE, None, None
         acc = (ctx.extra.get("dx_accum") or {}).get(0)
-        dx = K.linear_bwd(dy2, x2, w, z, self.act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
+        dact = None
+        src = ctx.extra.get("dact_src")  # (producer's ctx, its act) when this op's dgrad is fused
+        if src is not None:
+            # planned by Executor._plan_dact_fusion: sole consumer, so no accumulated dx exists
+            assert ctx.extra.get("need_dx0", True) and acc is None, "dact fusion needs a fresh dx"
+            pctx, pact = src
+            pdb = None
+            if len(pctx.wgrads) > 1 and pctx.saved.get("has_b") and not pctx.extra.get("bias_grad_fused"):
+                pdb = pctx.wgrads[1]
+            dact = (pctx.saved["z"].reshape(-1, x2.shape[1]), pact, pdb)
+        dx = K.linear_bwd(dy2, x2, w, z, act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
                           dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0,
-                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None)
+                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None, dact=dact)
         ctx.saved.clear()
         if dx is None:
             return [None]

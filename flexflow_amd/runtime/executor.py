@@ -610,6 +610,43 @@ class Executor:
                 break
         return n
 
+    def _plan_dact_fusion(self):
+        """Cross-op fusion for the backward: a Linear whose input comes straight (identity transfer,
+        sole consumer) from a Linear with an activation computes the producer's pre-activation
+        gradient in its own dgrad GEMM epilogue, dx * act'(z), together with the producer's bias
+        gradient (kernels.gemm_dact). The producer's backward then skips its bias_act_bwd pass,
+        which re-read and re-wrote the whole [tokens, ffn] gradient (BERT: FFN2's dgrad carries
+        FFN1's GELU')."""
+        if not self.training or os.environ.get("FF_NO_DACT_FUSION") == "1":
+            return 0
+        consumers = {}
+        for L in self.layers:
+            for t in L.inputs:
+                consumers[t.guid] = consumers.get(t.guid, 0) + 1
+        prod = {o.guid: L for L in self.layers for o in L.outputs}
+        out_guid = self.output_tensor.guid if self.output_tensor is not None else None
+        n = 0
+        for L in self.layers:
+            if L.op_type != OperatorType.OP_LINEAR or L.name not in self.ctx or not self.layer_bwd.get(L.name):
+                continue
+            t = L.inputs[0]
+            P = prod.get(t.guid)
+            if P is None or P.op_type != OperatorType.OP_LINEAR or P.name not in self.ctx or P.impl.act == K.ACT_NONE:
+                continue
+            if consumers.get(t.guid, 0) != 1 or t.guid == out_guid or not self.layer_bwd.get(P.name):
+                continue
+            if not self.in_grad.get((L.name, 0)) or self.fwd_tx[(L.name, 0)].kind != "identity":
+                continue
+            if self.bwd_tx[(L.name, 0)].kind != "identity":
+                continue
+            pctx = self.ctx[P.name]
+            if pctx.wgrads and len(pctx.wgrads) > 1 and pctx.wgrads[1].dtype != torch.float32:
+                continue
+            self.ctx[L.name].extra["dact_src"] = (pctx, P.impl.act)
+            pctx.extra["dact_fused"] = True
+            n += 1
+        return n
+
     def _hooked(self, L, phase):
         """Nest every attached hook's op(L, phase) context (profiler, non-finite guard)."""
         from contextlib import ExitStack

@@ -321,6 +321,49 @@ def test_bias_act_bwd(ffC, rows, cols, act):
     assert _rel(db, 1.0 + dz_ref.sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("a_k,b_k", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (300, 136, 72), (1000, 4096, 1024), (256, 200, 64)])
+@pytest.mark.parametrize("act", [14, 11])  # GELU, RELU
+def test_gemm_dact(ffC, a_k, b_k, M, N, K, act):
+    """Consumer dgrad GEMM with the producer's act' and bias-gradient column sums in the epilogue
+    (gemm256.hip dact mode) against fp32 torch."""
+    from flexflow_amd.kernels import act_grad_ref
+    torch.manual_seed(3)
+    Am = torch.randn(M, K, device=DEV).bfloat16()
+    Bn = torch.randn(N, K, device=DEV).bfloat16()
+    A = Am if a_k else Am.t().contiguous()
+    B = Bn if b_k else Bn.t().contiguous()
+    z = torch.randn(M, N, device=DEV).bfloat16()
+    C = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    db = torch.ones(N, device=DEV)
+    ok = ffC.gemm_dact(A, B, C, z, db, M, N, K, A.shape[-1], B.shape[-1], N, a_k, b_k, act)
+    assert ok == (N % 8 == 0 and K % 64 == 0 and (a_k or M % 8 == 0))
+    if not ok:
+        return
+    ref = (Am.float() @ Bn.float().t()) * act_grad_ref(z.float(), act)
+    assert _rel(C, ref) < 1e-2
+    assert _rel(db, 1.0 + ref.sum(0)) < 1e-2
+
+
+def test_gemm_dact_dispatch_matches_unfused():
+    """kernels.gemm_dact's autotuned choice and its GEMM + in-place bias_act_bwd alternative agree."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(4)
+    M, N, Kd = 768, 512, 256
+    dy = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = torch.randn(Kd, N, device=DEV).bfloat16()
+    z = torch.randn(M, N, device=DEV).bfloat16()
+    outs = []
+    for fused in (True, False):
+        K._tuned[("dact", M, N, Kd, True, False, Kd, N, N, 14, True)] = "fused" if fused else "unfused"
+        C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        db = torch.zeros(N, device=DEV)
+        K.gemm_dact(dy, w, C, z, db, M, N, Kd, True, False, Kd, N, N, 14)
+        outs.append((C.float(), db))
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2
+    assert _rel(outs[0][1], outs[1][1]) < 1e-2
+
+
 def test_adam_sgd_embedding_dropout(ffC):
     torch.manual_seed(7)
     n = 10001

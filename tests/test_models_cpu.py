@@ -85,6 +85,42 @@ def test_bias_grad_fusion_into_layernorm_matches_unfused(monkeypatch):
         np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6, err_msg=k)
 
 
+def test_dact_fusion_into_consumer_dgrad_matches_unfused(monkeypatch):
+    """FFN2's dgrad GEMM applying FFN1's GELU' and summing FFN1's bias gradient
+    (executor._plan_dact_fusion -> kernels.gemm_dact) trains like the separate bias_act_bwd pass."""
+    import numpy as np
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(fused):
+        if fused:
+            monkeypatch.delenv("FF_NO_DACT_FUSION", raising=False)
+        else:
+            monkeypatch.setenv("FF_NO_DACT_FUSION", "1")
+        cfg = FFConfig(["--device", "cpu"])
+        bc = BertConfig.tiny(16)
+        cfg.batch_size = 2
+        ff = FFModel(cfg)
+        ids, pos, _ = build_bert(ff, 2, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        n = sum(1 for c in ff.executor.ctx.values() if c.extra.get("dact_fused"))
+        rng = np.random.default_rng(0)
+        ids.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(16, dtype=np.int32), (2, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (2, 16, 1), dtype=np.int32))
+        for _ in range(2):
+            ff.train_step()
+        ws = {f"{L.name}.{i}": np.asarray(w.get_weights(ff)) for L in ff.layers for i, w in enumerate(L.weights)}
+        return n, ws
+
+    n1, a = run(True)
+    n0, b = run(False)
+    assert n0 == 0 and n1 == BertConfig.tiny(16).layers  # FFN1 of every layer (the MLM transform feeds a LayerNorm)
+    for k in a:
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
 def test_partial_gradient_zeroing_matches_full(monkeypatch):
     """Arenas lay out accumulated gradients first and zero_gradients() clears only that prefix (the
     overwritten GEMM gradients need no clearing): training matches zeroing the whole arena."""
