@@ -28,5 +28,7 @@ void attn_bwd(AttnArgs a, hipStream_t st);
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D);
 int attn_bwd_variant();
 void attn_set_bwd_variant(int v);
+int attn_fwd_variant();
+void attn_set_fwd_variant(int v);
 
 }  // namespace ffk

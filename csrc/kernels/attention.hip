@@ -69,6 +69,28 @@ struct TileStage {
   }
 };
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Same [64][D] tile image as TileStage::store, written by the LDS-DMA path (buffer_load ... lds):
+// no staging registers, so the forward needs 32 fewer VGPRs (4 workgroups per CU instead of 3 at
+// D = 64). Each wave instruction fills one 1-KiB piece, lane l landing at piece + 16 l; the XOR
+// swizzle is applied on the global side (lane l of slot s fetches chunk (s % CPR) ^ aswz(row)).
+// Rows past the sequence end read as zero (buffer range check), like TileStage's clamp.
+template <int D, int NWAVES>
+__device__ __forceinline__ void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int64_t ss, int r0, int wave,
+                                         int lane) {
+  constexpr int PIECES = 64 * D * 2 / 1024, CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < PIECES / NWAVES; ++i) {
+    const int piece = i * NWAVES + wave;
+    const int slot = piece * 64 + lane;
+    const int row = slot / CPR;
+    const int ch = (slot % CPR) ^ aswz<D>(row);
+    const int off = (int)(((int64_t)(r0 + row) * ss + ch * 8) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(lds_tile + piece * 1024), 16, off, 0, 0, 0);
+  }
+}
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
@@ -88,8 +110,8 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
 // xcd_remap: the query blocks of one (batch, head) share an XCD and its L2 copy of K / V. The O
 // tile leaves through LDS as whole rows (16 B per lane). Together -5 % at B32 H16 S512 D64
 // (scripts/lab/attn_fwd_lab.hip, profiles/attn_fwd_lab_r2.txt).
-template <int D, bool MASK>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+template <int D, bool MASK, bool DMA>
+__global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) {
   constexpr int KV = 64;
   constexpr int TB = KV * D * 2;  // bytes of one K or V tile
   __shared__ __attribute__((aligned(16))) char smem[4 * TB];
@@ -120,11 +142,21 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   if (a.causal) nkv = min(nkv, (min(qblk0 + 128, a.Sq) + KV - 1) / KV);
 
   TileStage<D, KV, 256> sk, sv;
+  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
+  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, kb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, vb, 0x00020000);
   if (nkv > 0) {
-    sk.load(K, a.k_ss, 0, a.Sk, tid);
-    sv.load(V, a.v_ss, 0, a.Sk, tid);
-    sk.store(smem, tid);
-    sv.store(smem + TB, tid);
+    if (DMA) {
+      dma_tile<D, 4>(rk, smem, a.k_ss, 0, wave, lane);
+      dma_tile<D, 4>(rv, smem + TB, a.v_ss, 0, wave, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      sk.load(K, a.k_ss, 0, a.Sk, tid);
+      sv.load(V, a.v_ss, 0, a.Sk, tid);
+      sk.store(smem, tid);
+      sv.store(smem + TB, tid);
+    }
     __syncthreads();
   }
   for (int t = 0; t < nkv; ++t) {
@@ -133,8 +165,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     char* nk = smem + ((t + 1) & 1) * 2 * TB;
     const bool more = t + 1 < nkv;
     if (more) {
-      sk.load(K, a.k_ss, (t + 1) * KV, a.Sk, tid);
-      sv.load(V, a.v_ss, (t + 1) * KV, a.Sk, tid);
+      if (DMA) {
+        dma_tile<D, 4>(rk, nk, a.k_ss, (t + 1) * KV, wave, lane);
+        dma_tile<D, 4>(rv, nk + TB, a.v_ss, (t + 1) * KV, wave, lane);
+      } else {
+        sk.load(K, a.k_ss, (t + 1) * KV, a.Sk, tid);
+        sv.load(V, a.v_ss, (t + 1) * KV, a.Sk, tid);
+      }
     }
     // S^T[key][q] for keys 32kt..32kt+31 of this tile
     f32x16 sacc[2] = {f32x16{}, f32x16{}};
@@ -211,8 +248,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       }
     }
     if (more) {
-      sk.store(nk, tid);
-      sv.store(nk + TB, tid);
+      if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else {
+        sk.store(nk, tid);
+        sv.store(nk + TB, tid);
+      }
     }
     __syncthreads();
   }
@@ -870,15 +910,36 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
+// Forward K/V staging at D = 64: 1 = LDS-DMA (default), 0 = through registers (attn_set_fwd_variant;
+// default from FF_ATTN_FWD).
+static int g_fwd_variant = -1;
+int attn_fwd_variant() {
+  if (g_fwd_variant < 0) {
+    const char* e = getenv("FF_ATTN_FWD");
+    g_fwd_variant = e ? atoi(e) : 1;
+  }
+  return g_fwd_variant;
+}
+void attn_set_fwd_variant(int v) { g_fwd_variant = v; }
+
 void attn_fwd(AttnArgs a, hipStream_t st) {
   const dim3 grid((unsigned)((a.Sq + 127) / 128 * a.B * a.H));
   const bool mask = a.causal || a.Sk % 64 != 0;
+  // the DMA path needs 16-B aligned K / V rows and buffer offsets below 2 GiB
+  const bool dma = attn_fwd_variant() == 1 && ((uintptr_t)a.k & 15) == 0 && ((uintptr_t)a.v & 15) == 0 &&
+                   a.k_ss % 8 == 0 && a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
+                   (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
   if (a.D == 64) {
-    if (mask) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, dim3(256), 0, st, a);
+    if (dma) {
+      if (mask) hipLaunchKernelGGL((attn_fwd_kernel<64, true, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_kernel<64, false, true>), grid, dim3(256), 0, st, a);
+    } else {
+      if (mask) hipLaunchKernelGGL((attn_fwd_kernel<64, true, false>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_kernel<64, false, false>), grid, dim3(256), 0, st, a);
+    }
   } else if (a.D == 128) {
-    if (mask) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, dim3(256), 0, st, a);
+    if (mask) hipLaunchKernelGGL((attn_fwd_kernel<128, true, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, false, false>), grid, dim3(256), 0, st, a);
   }
 }
 

@@ -527,6 +527,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_ws", &attn_bwd_ws);
   m.def("attn_set_bwd_variant", [](int v) { ffk::attn_set_bwd_variant(v); });
+  m.def("attn_fwd_variant", []() { return ffk::attn_fwd_variant(); });
+  m.def("attn_set_fwd_variant", [](int v) { ffk::attn_set_fwd_variant(v); });
   m.def("attn_bwd_variant", []() { return ffk::attn_bwd_variant(); });
   m.def("batchnorm_fwd", &batchnorm_fwd);
   m.def("batchnorm_bwd", &batchnorm_bwd);

@@ -36,10 +36,23 @@ def timed(fn):
     return s.elapsed_time(e) / reps
 
 
-lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
-fwd_ms = timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False))
 fl_f = 4.0 * B * H * S * S * D
-print(f"attn fwd B={B} H={H} S={S} D={D}: {fwd_ms:.3f} ms {fl_f / fwd_ms / 1e9:.1f} TFLOPS")
+# forward K/V staging variants (0: through registers, 1: LDS-DMA), interleaved rounds
+default_fwd = X.attn_fwd_variant()
+fres, fouts = {0: [], 1: []}, {}
+for rnd in range(3):
+    for var in (0, 1):
+        X.attn_set_fwd_variant(var)
+        lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
+        fouts[var] = (o.clone(), lse.clone())
+        fres[var].append(timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)))
+for var in (0, 1):
+    ms = min(fres[var])
+    print(f"attn fwd variant {var} B={B} H={H} S={S} D={D}: {ms:.4f} ms {fl_f / ms / 1e9:.1f} TFLOPS "
+          f"(rounds {[round(t, 4) for t in fres[var]]})")
+print(f"fwd variants identical: {torch.equal(fouts[0][0], fouts[1][0]) and torch.equal(fouts[0][1], fouts[1][1])}")
+X.attn_set_fwd_variant(default_fwd)
+lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
 # backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
 default_variant = X.attn_bwd_variant()
 res = {0: [], 1: [], 2: []}
