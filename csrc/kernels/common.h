@@ -112,21 +112,28 @@ enum Act : int { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13, 
 
 // erf with |error| < 1.5e-7 (Abramowitz & Stegun 7.1.26): one v_rcp, one v_exp and five FMAs
 // instead of libm erff's branchy polynomial — the GELU epilogues evaluate it per output element.
-__device__ __forceinline__ float fast_erf(float x) {
-  const float ax = fabsf(x);
-  const float t = __frcp_rn(1.f + 0.3275911f * ax);
+// The reciprocal is the bare v_rcp_f32 (1 ulp): __frcp_rn / '1.f / x' lower to the IEEE division
+// sequence (div_scale x2, rcp, div_fmas, div_fixup + refinement FMAs), which doubled the VALU cost
+// of the GELU passes.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float erf_poly_t(float t) {  // A&S 7.1.26 polynomial times t
   float y = __builtin_fmaf(1.061405429f, t, -1.453152027f);
   y = __builtin_fmaf(y, t, 1.421413741f);
   y = __builtin_fmaf(y, t, -0.284496736f);
   y = __builtin_fmaf(y, t, 0.254829592f);
-  y = 1.f - y * t * __expf(-ax * ax);
+  return y * t;
+}
+__device__ __forceinline__ float fast_erf(float x) {
+  const float ax = fabsf(x);
+  const float t = fast_rcp(__builtin_fmaf(0.3275911f, ax, 1.f));
+  const float y = 1.f - erf_poly_t(t) * __expf(-ax * ax);
   return copysignf(y, x);
 }
 
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ACT_RELU: return fmaxf(x, 0.f);
-    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case ACT_SIGMOID: return fast_rcp(1.f + __expf(-x));
     case ACT_TANH: return tanhf(x);
     case ACT_GELU: return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f));
     default: return x;
@@ -136,12 +143,16 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
-    case ACT_SIGMOID: { float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
+    case ACT_SIGMOID: { float s = fast_rcp(1.f + __expf(-x)); return s * (1.f - s); }
     case ACT_TANH: { float t = tanhf(x); return 1.f - t * t; }
     case ACT_GELU: {
-      float cdf = 0.5f * (1.f + fast_erf(x * 0.70710678118654752f));
-      float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-      return cdf + x * pdf;
+      // Phi(x) + x phi(x); erf(x / sqrt 2) and phi share one exp(-x^2 / 2)
+      const float au = fabsf(x) * 0.70710678118654752f;
+      const float t = fast_rcp(__builtin_fmaf(0.3275911f, au, 1.f));
+      const float e = __expf(-au * au);
+      const float erf_abs = 1.f - erf_poly_t(t) * e;
+      const float cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
+      return __builtin_fmaf(x * 0.3989422804014327f, e, cdf);
     }
     default: return 1.f;
   }
