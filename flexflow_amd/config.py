@@ -76,6 +76,10 @@ class FFConfig:
         self.mcmc_iterations = 2000
         self.grad_bucket_mb = 64.0
         self.zero_optimizer = False   # --zero: ZeRO-1 sharded optimizer state / update on DP arenas
+        # train_step runs each gradient bucket's optimizer update on a side stream as soon as the
+        # bucket is final (all-reduced), overlapping the rest of the backward (runtime/executor.py
+        # 'overlapped update'); --overlap-update / --no-overlap-update, FF_OVERLAP_UPDATE=0|1
+        self.overlap_update = os.environ.get("FF_OVERLAP_UPDATE", "0") == "1"
         self.seed = 1234
         self.cpu_only = False  # -ll:gpu 0 / --device cpu: run on the host even with a GPU present
         self.trace_dir = ""
@@ -212,6 +216,10 @@ class FFConfig:
                     self.mcmc_iterations = int(nxt())
                 elif a == "--zero":
                     self.zero_optimizer = True
+                elif a == "--overlap-update":
+                    self.overlap_update = True
+                elif a == "--no-overlap-update":
+                    self.overlap_update = False
                 elif a == "--grad-bucket-mb":
                     self.grad_bucket_mb = float(nxt())
                 elif a == "--seed":

@@ -326,6 +326,7 @@ class GradBucketer:
         self.param_bucket = {}
         self.param_buckets = {}  # sharded arenas: a parameter may straddle bucket boundaries
         self.handles = []
+        self.on_ready = None  # callback(bucket, async handle or None) once a bucket's grads are final
 
     def add_sharded_arena(self, group_ranks, flat, segments, rank):
         """ZeRO-1 arena (flexflow_amd/runtime/executor.py 'sharded optimizer'): buckets are fixed
@@ -384,11 +385,13 @@ class GradBucketer:
         for b in bs:
             b["ready"].add(key)
             if len(b["ready"]) == len(b["params"]):
-                self._launch(b)
+                h = self._launch(b)
+                if self.on_ready is not None:
+                    self.on_ready(b, h)
 
     def _launch(self, b):
         if len(b["group"]) <= 1 or not self.comm.distributed:
-            return
+            return None
         view = b["flat"][b["lo"]:b["hi"]]
         g = self.comm.group(b["group"])
         if b.get("sharded"):  # in-place reduce-scatter: this rank's chunk of the bucket gets the sum
@@ -397,6 +400,7 @@ class GradBucketer:
         else:
             h = dist.all_reduce(view, group=g, async_op=True)
         self.handles.append(h)
+        return h
 
     def flush(self):
         for _, _, buckets in self.arenas:

@@ -51,10 +51,11 @@ class StepGraph:
     def step(self):
         m = self.model
         ex = m.executor
+        ov = bool(getattr(m.config, "overlap_update", False))
         if not self.enabled():
             ex.zero_gradients()
             ex.forward()
-            ex.backward()
+            ex.backward(overlap_update=ov)
             ex.update(m.optimizer)
             return
         if self.warm < 3:
@@ -69,7 +70,7 @@ class StepGraph:
                 st.record()
             ex.zero_gradients()
             ex.forward()
-            ex.backward()
+            ex.backward(overlap_update=ov)
             ex.update(m.optimizer)
             if auto and self.warm >= 2:
                 en.record()
