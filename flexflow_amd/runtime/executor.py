@@ -511,6 +511,8 @@ class Executor:
         pass of BERT-Large mostly disappears from the step."""
         if not self._overlap_active or b.get("sharded"):
             return
+        if handle is not None and dist.get_backend(self.comm.group(b["group"])) != "nccl":
+            return  # gloo's wait() blocks the host: leave this bucket to update()
         ar = self._bucket_arena.get(id(b))
         if ar is None or b["hi"] <= b["lo"]:
             return
