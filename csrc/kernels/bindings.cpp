@@ -216,6 +216,19 @@ void metrics_classify(Tensor probs, Tensor labels, int64_t rows, int64_t cols, T
 void reduce_rows(Tensor x, Tensor y, int64_t outer, int64_t red, int64_t inner, bool mean) {
   ffk::reduce_rows(dtcode(x), x.data_ptr(), y.data_ptr(), outer, red, inner, mean, cur_stream());
 }
+void sgd_sparse_rows(Tensor idx, Tensor mark, Tensor master, Tensor grad, optional<Tensor> lowp, double lr) {
+  check_dev(idx, "idx"); check_dev(master, "master");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous(), "sgd_sparse_rows: int64 contiguous ids");
+  TORCH_CHECK(master.dim() == 2 && grad.sizes() == master.sizes() && master.is_contiguous() && grad.is_contiguous() &&
+              master.scalar_type() == at::kFloat && grad.scalar_type() == at::kFloat, "sgd_sparse_rows: fp32 [rows, dim]");
+  TORCH_CHECK(mark.scalar_type() == at::kInt && mark.numel() >= master.size(0), "sgd_sparse_rows: mark");
+  if (lowp.has_value() && lowp->defined())
+    TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel() && lowp->is_contiguous());
+  TORCH_CHECK(idx.numel() < (1LL << 31));
+  ffk::sgd_sparse_rows(idx.data_ptr<int64_t>(), (int)idx.numel(), master.size(0), (int)master.size(1),
+                       mark.data_ptr<int>(), master.data_ptr<float>(), grad.data_ptr<float>(), ptr(lowp), lr,
+                       cur_stream());
+}
 void sgd_update(Tensor master, Tensor grad, optional<Tensor> mom, optional<Tensor> lowp, double lr,
                 double momentum, bool nesterov, double wd, double gscale) {
   TORCH_CHECK(master.scalar_type() == at::kFloat && grad.scalar_type() == at::kFloat);
@@ -516,6 +529,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("metrics_classify", &metrics_classify);
   m.def("reduce_rows", &reduce_rows);
   m.def("sgd_update", &sgd_update);
+  m.def("sgd_sparse_rows", &sgd_sparse_rows);
   m.def("adam_update", &adam_update);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

@@ -67,6 +67,10 @@ void mse_grad(int dt, const void* pred, const void* label, void* dpred, float* l
               hipStream_t st);
 
 // optimizer.hip (flat multi-tensor buffers)
+// row-sparse SGD (momentum 0, no weight decay) over the rows named in idx, clearing their gradient;
+// mark: int32 [rows] scratch
+void sgd_sparse_rows(const int64_t* idx, int n, int64_t rows, int dim, int* mark, float* master, float* grad,
+                     void* lowp, float lr, hipStream_t st);
 void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
                 int nesterov, float wd, float gscale, hipStream_t st);
 void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,

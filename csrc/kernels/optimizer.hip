@@ -86,6 +86,45 @@ __global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, 
   }
 }
 
+// Row-sparse SGD for embedding tables (momentum 0, no weight decay: a row no id touched has a zero
+// gradient, so skipping it is exact). Two passes, no sort: every occurrence i of row r stores i
+// into mark[r] (one store wins), then only the occurrence that won applies w -= lr * g to the row
+// (and refreshes its bf16 copy) — each touched row is updated exactly once whatever the
+// duplicates, and clears the row's gradient (so zero_gradients can skip the table: only touched
+// rows were ever non-zero). mark needs no clearing: pass 1 rewrites every row this step touches.
+__global__ void sparse_rows_mark_kernel(const int64_t* __restrict__ idx, int n, int64_t rows, int* __restrict__ mark) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int64_t r = idx[i];
+    if (r >= 0 && r < rows) mark[r] = i;
+  }
+}
+__global__ void sparse_rows_sgd_kernel(const int64_t* __restrict__ idx, int n, int64_t rows, int dim,
+                                       const int* __restrict__ mark, float* __restrict__ w,
+                                       float* __restrict__ g, bf16_t* __restrict__ wl, float lr) {
+  // one wave per occurrence, lanes over the row's columns
+  const int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const int64_t r = idx[i];
+  if (r < 0 || r >= rows || mark[r] != i) return;
+  float* wr = w + r * dim;
+  float* gr = g + r * dim;
+  for (int d = lane; d < dim; d += 64) {
+    const float v = wr[d] - lr * gr[d];
+    wr[d] = v;
+    gr[d] = 0.f;
+    if (wl) wl[r * dim + d] = f2bf(v);
+  }
+}
+void sgd_sparse_rows(const int64_t* idx, int n, int64_t rows, int dim, int* mark, float* master, float* grad,
+                     void* lowp, float lr, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sparse_rows_mark_kernel, dim3((n + 255) / 256), dim3(256), 0, st, idx, n, rows, mark);
+  hipLaunchKernelGGL(sparse_rows_sgd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, idx, n, rows, dim, mark, master,
+                     grad, (bf16_t*)lowp, lr);
+}
+
 void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
                 int nesterov, float wd, float gscale, hipStream_t st) {
   if (n == 0) return;

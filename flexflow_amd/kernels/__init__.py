@@ -903,6 +903,23 @@ def sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale=1.0):
         lowp.copy_(master)
 
 
+def sgd_sparse_rows(idx, mark, master, grad, lowp, lr):
+    """master[r] -= lr * grad[r] (and the bf16 copy), then grad[r] = 0, for each distinct row r named
+    in idx — plain SGD restricted to the rows a step touched (exact when momentum = weight decay =
+    0: no other row has a non-zero gradient). Ids outside
+    [0, rows) are ignored (other vocab-parallel parts' rows). mark: int32 [rows] scratch."""
+    idx = idx.reshape(-1)
+    if native(master):
+        ext().sgd_sparse_rows(idx.to(torch.int64).contiguous(), mark, master, grad, lowp, lr)
+        return
+    rows = torch.unique(idx.to(torch.int64))
+    rows = rows[(rows >= 0) & (rows < master.shape[0])]
+    master[rows] -= lr * grad[rows]
+    grad[rows] = 0
+    if lowp is not None:
+        lowp[rows] = master[rows].to(lowp.dtype)
+
+
 def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0):
     if native(master):
         ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale)

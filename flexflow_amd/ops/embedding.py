@@ -84,6 +84,7 @@ class Embedding(OpImpl):
 
     def backward(self, ctx, douts):
         idx = ctx.saved.pop("idx")
+        ctx.extra["touched_idx"] = idx  # rows this step touched (Executor row-sparse SGD update)
         if ctx.wgrads and ctx.wgrads[0] is not None:
             dim = ctx.wgrads[0].shape[1]
             K.embedding_bwd(idx, douts[0].reshape(-1, dim), ctx.wgrads[0], self.bag,

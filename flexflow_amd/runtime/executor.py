@@ -250,6 +250,9 @@ class Executor:
         self._overlap_active = False
         self._opt_next_done = False
         self.bucketer.on_ready = self._on_bucket_ready
+        self._sparse, self._sparse_key = {}, None  # row-sparse SGD plan (_sparse_plan)
+        self._sparse_cleared = {}  # arena group -> [(lo, hi)] whose gradient the sparse update cleared
+        self._marks = {}           # weight guid -> int32 [rows] scratch of the sparse update
         for L in self.layers:
             if L.name in self.ctx:
                 self.ctx[L.name].extra["wgrad_overwrite"] = bool(L.weights) and all(
@@ -498,6 +501,7 @@ class Executor:
     def _overlap_possible(self):
         opt = self.model.optimizer
         return (self.training and opt is not None and hasattr(opt, "step_range") and not self.zero
+                and not self._sparse_plan(opt)
                 and not self.hooks and self.device.type == "cuda"
                 and not torch.cuda.is_current_stream_capturing()
                 and not any(L.attrs.get("regularizer") is not None for L in self.layers))
@@ -727,11 +731,57 @@ class Executor:
         return out or None
 
     def zero_gradients(self):
-        for ar in self.arenas.values():
+        # tables updated by the row-sparse SGD had their touched gradient rows cleared by it
+        skip = self._sparse_cleared if os.environ.get("FF_ZERO_ALL_GRADS") != "1" else {}
+        self._sparse_cleared = {}
+        for grp, ar in self.arenas.items():
             if ar.acc_end >= ar.size or os.environ.get("FF_ZERO_ALL_GRADS") == "1":
-                ar.grad.zero_()
-            elif ar.acc_end:
-                ar.grad[:ar.acc_end].zero_()
+                end = ar.size
+            else:
+                end = ar.acc_end
+            if not end:
+                continue
+            holes = sorted(skip.get(grp, ()))
+            if not holes:
+                if end >= ar.size:
+                    ar.grad.zero_()
+                else:
+                    ar.grad[:end].zero_()
+                continue
+            lo = 0
+            for a, b in holes:
+                if a > lo:
+                    ar.grad[lo:min(a, end)].zero_()
+                lo = max(lo, b)
+            if lo < end:
+                ar.grad[lo:end].zero_()
+
+    def _sparse_plan(self, optimizer):
+        """Embedding tables the optimizer may update row-sparsely: plain SGD (momentum 0, no weight
+        decay), so a row no id touched keeps a zero gradient and would not move; the table is
+        this rank's alone (no gradient all-reduce), its layer is its only user and carries no
+        regularizer. {arena group: [(entry index, layer name)]}. FF_SPARSE_EMB=0 disables."""
+        key = id(optimizer)
+        if self._sparse_key == key:
+            return self._sparse
+        plan = {}
+        from ..core.optimizers import SGDOptimizer
+        if (isinstance(optimizer, SGDOptimizer) and not optimizer.momentum and not optimizer.weight_decay
+                and os.environ.get("FF_SPARSE_EMB", "1") != "0" and not self.zero):
+            for L in self.layers:
+                if L.op_type != OperatorType.OP_EMBEDDING or L.name not in self.ctx or not self.layer_bwd.get(L.name):
+                    continue
+                if L.attrs.get("regularizer") is not None or not L.weights:
+                    continue
+                w = L.weights[0]
+                if w.guid not in self.weight_loc or self.weight_users.get(w.guid, 1) != 1:
+                    continue
+                ar, i = self.weight_loc[w.guid]
+                if len(ar.group) > 1 or len(ar.entries[i][3]) != 2:
+                    continue
+                plan.setdefault(ar.group, []).append((i, L.name))
+        self._sparse, self._sparse_key = plan, key
+        return plan
 
     def _apply_regularizers(self):
         """Keras-style weight regularizers (layer attr 'regularizer' with l1/l2): grad += 2*l2*w +
@@ -764,6 +814,10 @@ class Executor:
             if not ar.size:
                 continue
             bs = self.zero_buckets.get(grp)
+            sparse = self._sparse_plan(optimizer).get(grp) if bs is None else None
+            if sparse:
+                self._sparse_update(optimizer, grp, ar, sparse)
+                continue
             if bs is None:
                 if overlapped:  # the buckets the backward did not complete (e.g. frozen weights)
                     for _, flat, buckets in self.bucketer.arenas:
@@ -789,6 +843,31 @@ class Executor:
         self._overlap_active = False
         self._opt_next_done = False
         self.step_idx += 1
+
+    def _sparse_update(self, optimizer, grp, ar, sparse):
+        """Dense SGD over the arena minus the sparse tables, then each table's touched rows only
+        (kernels.sgd_sparse_rows, which also clears those gradient rows)."""
+        holes = sorted((ar.entries[i][1], ar.entries[i][1] + ar.entries[i][2], i, name) for i, name in sparse)
+        lo = 0
+        for a, b, _, _ in holes:
+            if a > lo:
+                optimizer.step_range(ar, lo, a)
+            lo = max(lo, b)
+        if lo < ar.size:
+            optimizer.step_range(ar, lo, ar.size)
+        cleared = []
+        for a, b, i, name in holes:
+            idx = self.ctx[name].extra.get("touched_idx")
+            m, g, c = ar.views(i)
+            if idx is None:  # the table's layer did not run backward: its gradient is whatever it was
+                continue
+            w = ar.entries[i][0]
+            mark = self._marks.get(w.guid)
+            if mark is None:
+                mark = self._marks[w.guid] = torch.empty(m.shape[0], dtype=torch.int32, device=m.device)
+            K.sgd_sparse_rows(idx, mark, m, g, c if ar.lowp is not None else None, optimizer.lr)
+            cleared.append((a, b))
+        self._sparse_cleared[grp] = cleared
 
     def _wait_weights(self, L):
         """Sharded optimizer: the all-gathers of the buckets holding L's weights must land first."""

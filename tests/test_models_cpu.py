@@ -154,3 +154,36 @@ def test_partial_gradient_zeroing_matches_full(monkeypatch):
     _, b = run(True)
     for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_sparse_embedding_sgd_matches_dense(monkeypatch):
+    """Plain SGD updates DLRM's embedding tables only on the rows the step's ids touched (and
+    clears just those gradient rows; executor._sparse_update -> kernels.sgd_sparse_rows), exactly
+    like the dense update over the whole table."""
+    def run(sparse):
+        if sparse:
+            monkeypatch.delenv("FF_SPARSE_EMB", raising=False)
+        else:
+            monkeypatch.setenv("FF_SPARSE_EMB", "0")
+        cfg = FFConfig(["--no-hip-graphs"])
+        cfg.batch_size = 4
+        ff = FFModel(cfg)
+        inputs, out, loss, mets, make_batch = build("dlrm", ff, 4, small=True)
+        ff.optimizer = SGDOptimizer(ff, 0.05)
+        ff.compile(loss_type=loss, metrics=mets)
+        n = sum(len(v) for v in ff.executor._sparse_plan(ff.optimizer).values())
+        rng = np.random.default_rng(0)
+        for _ in range(3):  # a new batch (new rows, repeated ids) every step
+            arrs, lab = make_batch(rng)
+            for t, a in zip(inputs, arrs):
+                t.set_tensor(ff, a)
+            ff.label_tensor.set_tensor(ff, lab)
+            ff.train_step()
+        ws = [np.asarray(w.get_weights(ff)) for L in ff.layers for w in L.weights]  # names carry guids
+        return n, ws
+
+    n1, a = run(True)
+    n0, b = run(False)
+    assert n1 > 0 and n0 == 0 and len(a) == len(b)
+    for k, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-7, err_msg=str(k))
