@@ -38,6 +38,11 @@ __device__ __forceinline__ int aoff(int row, int col) {
   return row * (D * 2) + ((ch ^ aswz<D>(row)) << 4) + ((col & 7) << 1);
 }
 
+// 2^x as the bare v_exp_f32. exp2f() lowers to v_exp_f32 wrapped in a denormal range fix-up
+// (v_cmp + 2 v_cndmask + v_add + v_ldexp: six VALU ops per score element instead of one); softmax
+// probabilities below 2^-126 are irrelevant (they flush to 0, exp2(-inf) stays 0).
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 typedef short v4s __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bf16x4 tr_read(const char* lds, int off) {
@@ -207,13 +212,13 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
     const float mnew = fmaxf(m, mx);
     const float msafe = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m - msafe);
+    const float alpha = fast_exp2(m - msafe);
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
+        const float p = fast_exp2(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
         sacc[kt][r] = p;
         rs += p;
       }
@@ -473,7 +478,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
         const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
         const float lv[4] = {L4.x, L4.y, L4.z, L4.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = exp2f(sacc[4 * g4 + j] * sl2 - lv[j]);
+        for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = fast_exp2(sacc[4 * g4 + j] * sl2 - lv[j]);
       }
       if (MASK) {
         const bool need = (kb0 + wave * 32 + 31 >= a.Sk) || (a.causal && kb0 + wave * 32 + 31 > qbase + 32 * qt);
@@ -746,7 +751,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kg_kernel(AttnArgs a, int nkb
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ql = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float p = exp2f(__builtin_fmaf(sacc[g][r], sl2, -lse_l[ql]));
+          float p = fast_exp2(__builtin_fmaf(sacc[g][r], sl2, -lse_l[ql]));
           if (need_mask && (key >= a.Sk || (a.causal && key > qbase + ql))) p = 0.f;
           sacc[g][r] = p;
           pacc[g][r] = p * (pacc[g][r] - dl_l[ql]);

@@ -3,7 +3,9 @@
 
 Steps are delimited by the optimizer kernel (one fused adam/sgd launch per weight arena per step);
 the first `--skip` steps (autotuning, graph capture warm-up) are dropped so the numbers reflect
-the steady state only.  Prints ms/step per kernel (grouped by demangled-name prefix), the busy
+the steady state only. With the overlapped update (one optimizer launch per gradient bucket, on a
+side stream) delimit steps by a once-per-step kernel instead, e.g. `--delim softmax_xent_kernel`;
+busy then exceeds span by the overlapped time.  Prints ms/step per kernel (grouped by demangled-name prefix), the busy
 time and the wall span per step (span - busy = launch gaps / host stalls).
 
 usage: prof_steps.py run_kernel_trace.csv [--skip 2] [--top 40] [--delim adam_kernel]
