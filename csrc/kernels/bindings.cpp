@@ -230,22 +230,22 @@ void sgd_sparse_rows(Tensor idx, Tensor mark, Tensor master, Tensor grad, option
                        cur_stream());
 }
 void sgd_update(Tensor master, Tensor grad, optional<Tensor> mom, optional<Tensor> lowp, double lr,
-                double momentum, bool nesterov, double wd, double gscale) {
+                double momentum, bool nesterov, double wd, double gscale, int64_t max_blocks) {
   TORCH_CHECK(master.scalar_type() == at::kFloat && grad.scalar_type() == at::kFloat);
   TORCH_CHECK(master.numel() == grad.numel());
   if (momentum > 0) TORCH_CHECK(mom.has_value() && mom->numel() == master.numel());
   if (lowp.has_value() && lowp->defined())
     TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel());
   ffk::sgd_update(master.data_ptr<float>(), grad.data_ptr<float>(), ptr<float>(mom), ptr(lowp), master.numel(), lr,
-                  momentum, nesterov, wd, gscale, cur_stream());
+                  momentum, nesterov, wd, gscale, cur_stream(), (int)max_blocks);
 }
 void adam_update(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> lowp, double alpha_t, double b1,
-                 double b2, double wd, double eps, double gscale) {
+                 double b2, double wd, double eps, double gscale, int64_t max_blocks) {
   TORCH_CHECK(master.numel() == grad.numel() && m.numel() == master.numel() && v.numel() == master.numel());
   if (lowp.has_value() && lowp->defined())
     TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel());
   ffk::adam_update(master.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                   ptr(lowp), master.numel(), alpha_t, b1, b2, wd, eps, gscale, cur_stream());
+                   ptr(lowp), master.numel(), alpha_t, b1, b2, wd, eps, gscale, cur_stream(), (int)max_blocks);
 }
 void embedding_fwd(Tensor idx, Tensor table, Tensor out, int64_t n_rows, int64_t bag, int64_t dim, bool avg) {
   TORCH_CHECK(idx.numel() == n_rows * bag && out.numel() == n_rows * dim && table.size(-1) == dim);
@@ -528,9 +528,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("mse_grad", &mse_grad);
   m.def("metrics_classify", &metrics_classify);
   m.def("reduce_rows", &reduce_rows);
-  m.def("sgd_update", &sgd_update);
+  m.def("sgd_update", &sgd_update, py::arg("master"), py::arg("grad"), py::arg("mom"), py::arg("lowp"), py::arg("lr"),
+        py::arg("momentum"), py::arg("nesterov"), py::arg("wd"), py::arg("gscale"), py::arg("max_blocks") = 0);
   m.def("sgd_sparse_rows", &sgd_sparse_rows);
-  m.def("adam_update", &adam_update);
+  m.def("adam_update", &adam_update, py::arg("master"), py::arg("grad"), py::arg("m"), py::arg("v"), py::arg("lowp"),
+        py::arg("alpha_t"), py::arg("b1"), py::arg("b2"), py::arg("wd"), py::arg("eps"), py::arg("gscale"),
+        py::arg("max_blocks") = 0);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("init_uniform", &init_uniform);

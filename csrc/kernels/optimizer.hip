@@ -125,16 +125,22 @@ void sgd_sparse_rows(const int64_t* idx, int n, int64_t rows, int dim, int* mark
                      grad, (bf16_t*)lowp, lr);
 }
 
+// max_blocks > 0 caps the grid (an update overlapped with the backward on a side stream leaves CU
+// slots to the compute stream's kernels; the grid-stride loops keep enough bytes in flight).
+static int opt_grid(int64_t n, int max_blocks) {
+  const int g = ew_grid(n / 4 + 1, 256);
+  return max_blocks > 0 ? std::min(g, max_blocks) : g;
+}
 void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
-                int nesterov, float wd, float gscale, hipStream_t st) {
+                int nesterov, float wd, float gscale, hipStream_t st, int max_blocks) {
   if (n == 0) return;
-  hipLaunchKernelGGL(sgd_kernel, dim3(ew_grid(n / 4 + 1, 256)), dim3(256), 0, st, master, grad, mom,
+  hipLaunchKernelGGL(sgd_kernel, dim3(opt_grid(n, max_blocks)), dim3(256), 0, st, master, grad, mom,
                      (bf16_t*)param_lowp, n, lr, momentum, nesterov, wd, gscale);
 }
 void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,
-                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st) {
+                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st, int max_blocks) {
   if (n == 0) return;
-  hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(n / 4 + 1, 256)), dim3(256), 0, st, master, grad, m, v,
+  hipLaunchKernelGGL(adam_kernel, dim3(opt_grid(n, max_blocks)), dim3(256), 0, st, master, grad, m, v,
                      (bf16_t*)param_lowp, n, alpha_t, beta1, beta2, wd, eps, gscale);
 }
 

@@ -32,8 +32,9 @@ class Optimizer:
     def step(self, arena):
         raise NotImplementedError
 
-    def step_range(self, arena, lo, hi):
-        """Update elements [lo, hi) of the arena only (sharded optimizer: this rank's chunk)."""
+    def step_range(self, arena, lo, hi, max_blocks=0):
+        """Update elements [lo, hi) of the arena only (sharded optimizer: this rank's chunk; the
+        overlapped update: one gradient bucket, launched with at most max_blocks workgroups)."""
         raise NotImplementedError
 
 
@@ -52,11 +53,11 @@ class SGDOptimizer(Optimizer):
         K.sgd_update(arena.master, arena.grad, self.state.get(id(arena)), arena.lowp, self.lr, self.momentum,
                      self.nesterov, self.weight_decay)
 
-    def step_range(self, arena, lo, hi):
+    def step_range(self, arena, lo, hi, max_blocks=0):
         mom = self.state.get(id(arena))
         K.sgd_update(arena.master[lo:hi], arena.grad[lo:hi], mom[lo:hi] if mom is not None else None,
                      arena.lowp[lo:hi] if arena.lowp is not None else None, self.lr, self.momentum, self.nesterov,
-                     self.weight_decay)
+                     self.weight_decay, max_blocks=max_blocks)
 
 
 class AdamOptimizer(Optimizer):
@@ -88,8 +89,8 @@ class AdamOptimizer(Optimizer):
         K.adam_update(arena.master, arena.grad, m, v, arena.lowp, self.alpha_t, self.beta1, self.beta2,
                       self.weight_decay, self.epsilon)
 
-    def step_range(self, arena, lo, hi):
+    def step_range(self, arena, lo, hi, max_blocks=0):
         m, v = self.state[id(arena)]
         K.adam_update(arena.master[lo:hi], arena.grad[lo:hi], m[lo:hi], v[lo:hi],
                       arena.lowp[lo:hi] if arena.lowp is not None else None, self.alpha_t, self.beta1, self.beta2,
-                      self.weight_decay, self.epsilon)
+                      self.weight_decay, self.epsilon, max_blocks=max_blocks)

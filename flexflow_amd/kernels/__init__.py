@@ -890,9 +890,10 @@ def lstm_bwd_cell(G, ldg, c, c_prev, dy, lddy, dh_rec, dc, dG, B, H):
 
 
 # ----------------------------------------------------------------------------- optimizers
-def sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale=1.0):
+def sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale=1.0, max_blocks=0):
+    """max_blocks > 0 caps the launch grid (overlapped side-stream updates, Executor._on_bucket_ready)."""
     if native(master):
-        ext().sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale)
+        ext().sgd_update(master, grad, mom, lowp, lr, momentum, nesterov, wd, gscale, max_blocks)
         return
     g = grad * gscale + wd * master
     if momentum > 0:
@@ -920,9 +921,9 @@ def sgd_sparse_rows(idx, mark, master, grad, lowp, lr):
         lowp[rows] = master[rows].to(lowp.dtype)
 
 
-def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0):
+def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0, max_blocks=0):
     if native(master):
-        ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale)
+        ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale, max_blocks)
         return
     g = grad * gscale + wd * master
     m.mul_(b1).add_((1 - b1) * g)

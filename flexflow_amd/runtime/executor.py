@@ -250,6 +250,8 @@ class Executor:
         self._overlap_active = False
         self._opt_next_done = False
         self.bucketer.on_ready = self._on_bucket_ready
+        # workgroup cap of the overlapped update launches (FF_UPD_BLOCKS; 0 = the full 2048 grid)
+        self._upd_blocks = int(os.environ.get("FF_UPD_BLOCKS", "0"))
         self._sparse, self._sparse_key = {}, None  # row-sparse SGD plan (_sparse_plan)
         self._sparse_cleared = {}  # arena group -> [(lo, hi)] whose gradient the sparse update cleared
         self._marks = {}           # weight guid -> int32 [rows] scratch of the sparse update
@@ -528,7 +530,7 @@ class Executor:
             self._upd_stream.wait_event(ev)
             if handle is not None:
                 handle.wait()  # the side stream waits for the bucket's all-reduce
-            self.model.optimizer.step_range(ar, b["lo"], b["hi"])
+            self.model.optimizer.step_range(ar, b["lo"], b["hi"], max_blocks=self._upd_blocks)
         self._upd_done.add(id(b))
 
     def backward(self, overlap_update: bool = False):
