@@ -313,9 +313,11 @@ __global__ void __launch_bounds__(NT, 1) gemm256_kernel(GemmArgs p, int64_t a_by
           float zz[8];
           const uint4 zv = zpre[OUT_MODE == 0 ? qtr * ITS + it : 0];
           load16(reinterpret_cast<const bf16_t*>(&zv), zz);
+          // round the GEMM result to bf16 first, as the unfused GEMM + bias_act_bwd pair does, so
+          // the autotuner's choice between the two never changes the numerics beyond summation order
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            x[e] *= act_grad(p.act, zz[e]);
+            x[e] = bf2f(f2bf(x[e])) * act_grad(p.act, zz[e]);
             cs[e] += x[e];
           }
           store16(reinterpret_cast<bf16_t*>(dst), x);

@@ -58,8 +58,11 @@ def _train(search, steps=3):
 
 
 def _worker(rank, world, port, search, out_file):
+    # FF_GEMM_TUNE=0: every process takes the same kernel per call site (the autotuner's timing-
+    # dependent picks between forms that round differently would otherwise leak into the comparison)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), FF_DIST_BACKEND="gloo")
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), FF_DIST_BACKEND="gloo",
+                      FF_GEMM_TUNE="0")
     sys.path.insert(0, ROOT)
     res = _train(search)
     import torch.distributed as dist
@@ -79,10 +82,14 @@ def _run_world(search, world=2):
 
 @pytest.fixture(scope="module")
 def single():
+    from flexflow_amd import kernels as K
     old = {k: os.environ.pop(k, None) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    tune, tuned = K._TUNE, K._tuned
+    K._TUNE, K._tuned = False, {}  # the ranks' FF_GEMM_TUNE=0 choices, not this process's warm cache
     try:
         return _train("dp")
     finally:
+        K._TUNE, K._tuned = tune, tuned
         for k, v in old.items():
             if v is not None:
                 os.environ[k] = v
@@ -110,7 +117,4 @@ def test_bert_two_ranks_match_single(single, search):
         d = np.abs(a - b).max()
         assert d <= 2 * 3 * 1e-3 + 2e-2 * np.abs(b).max(), f"{search}: {k} max diff {d}"
         rel = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-12)
-        # the zero-initialised q / v biases are themselves only ~3 Adam steps (3 lr) large, so a
-        # few sign-noise flips weigh more in their norm: measured 0.2-4.5 % across boxes
-        tol = 6e-2 if k.endswith("attn.1") else 2e-2
-        assert rel < tol, f"{search}: {k} relative difference {rel}"
+        assert rel < 2e-2, f"{search}: {k} relative difference {rel}"
