@@ -147,3 +147,34 @@ def test_zero_never_captured_in_hip_graph(monkeypatch):
                          device=SimpleNamespace(type="cuda"))
     m = SimpleNamespace(executor=ex, config=SimpleNamespace(hip_graphs=True))
     assert StepGraph(m).enabled() is False
+
+
+def test_bucket_ready_callback_once_per_bucket_in_completion_order():
+    """GradBucketer.on_ready (the overlapped optimizer update's trigger, Executor._on_bucket_ready)
+    fires exactly once per bucket, when its last parameter is marked ready, in completion order;
+    reset() re-arms every bucket for the next step; flush() never fires it."""
+    import torch
+    from flexflow_amd.parallel.comm import GradBucketer
+
+    class _Comm:
+        distributed = False
+    flat = torch.zeros(64)
+    segs = [("w3", 0, 8), ("w2", 8, 24), ("w1", 24, 40), ("w0", 40, 64)]  # backward-completion order
+    bk = GradBucketer(_Comm(), bucket_bytes=4 * 20)  # a bucket closes once it holds >= 20 floats
+    bk.add_arena((0,), flat, segs)
+    assert [(b["lo"], b["hi"]) for b in bk.arenas[0][2]] == [(0, 24), (24, 64)]  # {w3, w2} {w1, w0}
+    fired = []
+    bk.on_ready = lambda b, h: fired.append((b["lo"], b["hi"], h))
+    for step in range(2):
+        bk.reset()
+        fired.clear()
+        bk.mark_ready("w3")
+        assert fired == []  # w2 still pending in the first bucket
+        bk.mark_ready("w2")
+        bk.mark_ready("w1")
+        assert fired == [(0, 24, None)]
+        if step == 0:
+            bk.mark_ready("w0")
+            assert fired == [(0, 24, None), (24, 64, None)]
+        bk.flush()  # step 1: w0 never marked (a frozen layer) -> update() updates that bucket itself
+        assert len(fired) == (2 if step == 0 else 1)
