@@ -19,11 +19,17 @@ ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--skip", type=int, default=2)
 ap.add_argument("--top", type=int, default=40)
-ap.add_argument("--delim", default="adam_kernel|sgd_kernel")
+ap.add_argument("--delim", default=None,
+                help="regex of a once-per-step kernel (default: the optimizer kernel, or softmax_xent_kernel "
+                     "when the optimizer runs once per gradient bucket)")
 a = ap.parse_args()
 
 rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+if a.delim is None:
+    n_opt = sum(1 for r in rows if re.search("adam_kernel|sgd_kernel", r["Kernel_Name"]))
+    n_xent = sum(1 for r in rows if "softmax_xent_kernel" in r["Kernel_Name"])
+    a.delim = "softmax_xent_kernel" if n_xent and n_opt > n_xent else "adam_kernel|sgd_kernel"
 delim = re.compile(a.delim)
 ends = [i for i, r in enumerate(rows) if delim.search(r["Kernel_Name"])]
 # several arenas -> several optimizer launches back to back; keep the last of each run
