@@ -530,7 +530,10 @@ class Executor:
             self._upd_stream.wait_event(ev)
             if handle is not None:
                 handle.wait()  # the side stream waits for the bucket's all-reduce
-            self.model.optimizer.step_range(ar, b["lo"], b["hi"], max_blocks=self._upd_blocks)
+            if self._upd_blocks:
+                self.model.optimizer.step_range(ar, b["lo"], b["hi"], max_blocks=self._upd_blocks)
+            else:  # plain call: user optimizers may implement step_range(arena, lo, hi) only
+                self.model.optimizer.step_range(ar, b["lo"], b["hi"])
         self._upd_done.add(id(b))
 
     def backward(self, overlap_update: bool = False):
