@@ -502,7 +502,9 @@ class Executor:
 
     def _overlap_possible(self):
         opt = self.model.optimizer
-        return (self.training and opt is not None and hasattr(opt, "step_range") and not self.zero
+        from ..core.optimizers import Optimizer
+        ranged = opt is not None and getattr(type(opt), "step_range", None) not in (None, Optimizer.step_range)
+        return (self.training and ranged and not self.zero
                 and not self._sparse_plan(opt)
                 and not self.hooks and self.device.type == "cuda"
                 and not torch.cuda.is_current_stream_capturing()
