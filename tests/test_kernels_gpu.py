@@ -651,3 +651,18 @@ def test_rmsnorm(rows, d, dtype):
     dx = K.rmsnorm_bwd(x, w, dy, rstd, dw)
     assert _rel(dx, xr.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-5)
     assert _rel(dw, wr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(3, 5, 7, 9), (64, 32, 35, 35), (2, 3, 1, 1), (16, 48, 17, 17), (1, 7, 64, 64)])
+def test_chan_sum_relu_mask(shape):
+    """Per-channel bias gradient with the ReLU mask (chan_sum_kernel: 4 loads in flight per lane,
+    incremental (image, pixel) indexing across odd planes and the tail) against torch."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(43)
+    dy = torch.randn(*shape, device=DEV).bfloat16()
+    y = torch.randn(*shape, device=DEV).bfloat16()
+    db = torch.full((shape[1],), 0.5, device=DEV)
+    dz = K.conv_bias_relu_bwd(dy, y, db)
+    ref = dy.float() * (y.float() > 0)
+    assert torch.equal(dz.float(), ref.bfloat16().float())
+    assert _rel(db, 0.5 + ref.sum((0, 2, 3))) < 1e-4
