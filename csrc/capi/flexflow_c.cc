@@ -33,8 +33,12 @@ void record_error() {
   if (v) {
     PyObject* s = PyObject_Str(v);
     if (s) {
-      g_err = PyUnicode_AsUTF8(s);
+      const char* u = PyUnicode_AsUTF8(s);  // NULL when the message cannot be encoded
+      if (u) g_err = u;
+      else PyErr_Clear();
       Py_DECREF(s);
+    } else {
+      PyErr_Clear();
     }
   }
   std::fprintf(stderr, "[flexflow_c] %s\n", g_err.c_str());
@@ -463,8 +467,9 @@ flexflow_tensor_t flexflow_model_add_reverse(flexflow_model_t m, flexflow_tensor
   return wrap<flexflow_tensor_t>(call("add_reverse", "(OOiz)", obj(m.impl), obj(x.impl), axis, name));
 }
 
-// a Python list of tensors -> outputs[0..n) (each a new reference); returns n or -1
-static int unpack(PyObject* r, flexflow_tensor_t* outputs) {
+// a Python list of tensors -> outputs[0..n) (each a new reference); returns n, or -1 on error
+// or when the list holds more than `cap` tensors (the caller's array size)
+static int unpack(PyObject* r, flexflow_tensor_t* outputs, int cap) {
   if (!r) return -1;
   if (!PyList_Check(r)) {
     Py_DECREF(r);
@@ -472,6 +477,11 @@ static int unpack(PyObject* r, flexflow_tensor_t* outputs) {
     return -1;
   }
   const int n = (int)PyList_Size(r);
+  if (n > cap || !outputs) {
+    Py_DECREF(r);
+    g_err = "output array too small for the op's outputs";
+    return -1;
+  }
   for (int i = 0; i < n; ++i) {
     PyObject* o = PyList_GetItem(r, i);
     Py_INCREF(o);
@@ -493,13 +503,13 @@ int flexflow_model_add_split(flexflow_model_t m, flexflow_tensor_t x, int n, con
                              flexflow_tensor_t* outputs, const char* name) {
   init_once();
   Gil gil;
-  return unpack(call("add_split", "(OONiz)", obj(m.impl), obj(x.impl), int_list(sizes, n), axis, name), outputs);
+  return unpack(call("add_split", "(OONiz)", obj(m.impl), obj(x.impl), int_list(sizes, n), axis, name), outputs, n);
 }
 int flexflow_model_add_top_k(flexflow_model_t m, flexflow_tensor_t x, int k, bool sorted, flexflow_tensor_t* outputs,
                              const char* name) {
   init_once();
   Gil gil;
-  return unpack(call("add_top_k", "(OOiiz)", obj(m.impl), obj(x.impl), k, (int)sorted, name), outputs);
+  return unpack(call("add_top_k", "(OOiiz)", obj(m.impl), obj(x.impl), k, (int)sorted, name), outputs, 2);
 }
 int flexflow_model_add_group_by(flexflow_model_t m, flexflow_tensor_t data, flexflow_tensor_t assign, int n,
                                 float alpha, flexflow_tensor_t* outputs, const char* name) {
@@ -507,7 +517,7 @@ int flexflow_model_add_group_by(flexflow_model_t m, flexflow_tensor_t data, flex
   Gil gil;
   return unpack(call("add_group_by", "(OOOidz)", obj(m.impl), obj(data.impl), obj(assign.impl), n, (double)alpha,
                      name),
-                outputs);
+                outputs, n);
 }
 static flexflow_tensor_t aggregate(flexflow_model_t m, int ni, const flexflow_tensor_t* xs, int n, float lam, int spec,
                                    const char* name) {

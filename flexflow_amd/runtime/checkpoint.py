@@ -16,7 +16,17 @@ import json
 import os
 
 import torch
+from safetensors import safe_open
 from safetensors.torch import load_file, save_file
+
+
+def _weight_keys(model):
+    """Sharding- and arena-order-independent identity of every weight: (layer position, slot)."""
+    keys = {}
+    for li, L in enumerate(model.layers):
+        for i, w in enumerate(L.weights):
+            keys.setdefault(w.guid, f"{li}:{i}")
+    return keys
 
 
 def _arenas(ex):
@@ -40,6 +50,7 @@ def save_checkpoint(model, path: str):
     os.makedirs(path, exist_ok=True)
     tensors = {}
     layout = []
+    wkeys = _weight_keys(model)
     for i, ar in _arenas(ex):
         tensors[f"arena{i}.master"] = ar.master.detach().contiguous().cpu()
         st = getattr(opt, "state", {}).get(id(ar))
@@ -47,8 +58,12 @@ def save_checkpoint(model, path: str):
             for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
                 tensors[f"arena{i}.opt{j}"] = t.detach().contiguous().cpu()
         layout.append({"arena": i, "size": int(ar.size), "used": _used(ar),
-                       "entries": [[getattr(e[0], "name", str(e[0])), int(e[1]), int(e[2])] for e in ar.entries]})
-    save_file(tensors, os.path.join(path, f"rank{cfg.rank}.safetensors"))
+                       "entries": [[wkeys.get(e[0].guid, getattr(e[0], "name", str(e[0]))), int(e[1]), int(e[2]),
+                                    list(e[3])] for e in ar.entries]})
+    # every rank's own arena layout travels inside its shard: arena order and offsets depend on
+    # the rank's placement, self.training and weight sharing, so the loader maps entry by entry
+    save_file(tensors, os.path.join(path, f"rank{cfg.rank}.safetensors"),
+              metadata={"arenas": json.dumps(layout)})
     if cfg.rank == 0:
         meta = {
             "step": int(ex.step_idx),
@@ -81,25 +96,40 @@ def load_checkpoint(model, path: str, strict: bool = True):
         if cur != [[op, c] for _, op, c in meta["strategy"]]:
             raise ValueError("checkpoint strategy differs from the compiled strategy (import it with "
                              "--import-strategy to resume)")
-    tensors = load_file(os.path.join(path, f"rank{cfg.rank}.safetensors"))
-    saved = {a["arena"]: a for a in meta.get("arenas", [])}
+    fn = os.path.join(path, f"rank{cfg.rank}.safetensors")
+    tensors = load_file(fn)
+    with safe_open(fn, framework="pt") as f:
+        md = f.metadata() or {}
+    if "arenas" not in md:
+        raise ValueError(f"{fn} has no per-entry arena layout (written by an older version); "
+                         "it cannot be mapped onto this job's arenas safely")
+    # saved weight key -> (arena index, offset, numel, shape)
+    saved = {}
+    for a in json.loads(md["arenas"]):
+        for key, off, n, shape in a["entries"]:
+            saved[key] = (a["arena"], int(off), int(n), tuple(shape))
+    wkeys = _weight_keys(model)
     for i, ar in _arenas(ex):
-        m = tensors[f"arena{i}.master"]
-        used = _used(ar)
-        # arenas are padded to a multiple of 16*R under --zero; only the used prefix must agree
-        if used != saved.get(i, {}).get("used", m.numel()) or m.numel() < used:
-            raise ValueError(f"arena {i} size mismatch ({m.numel()} saved, {used} used by this job)")
         ar.master.zero_()
-        ar.master[:used].copy_(m[:used].to(ar.master.device))
+        st = getattr(opt, "state", {}).get(id(ar))
+        st = list(st) if isinstance(st, (tuple, list)) else ([st] if st is not None else [])
+        for t in st:
+            t.zero_()
+        for w, off, n, shape in ar.entries:
+            key = wkeys.get(w.guid)
+            if key not in saved:
+                raise ValueError(f"weight {getattr(w, 'name', key)} ({key}) is not in checkpoint {fn}")
+            si, soff, sn, sshape = saved[key]
+            if sn != n or tuple(sshape) != tuple(shape):
+                raise ValueError(f"weight {getattr(w, 'name', key)}: checkpoint shard {sshape} != job shard {tuple(shape)}")
+            src = tensors[f"arena{si}.master"]
+            ar.master[off:off + n].copy_(src[soff:soff + n].to(ar.master.device))
+            for j, t in enumerate(st):
+                sk = f"arena{si}.opt{j}"
+                if sk in tensors:
+                    t[off:off + n].copy_(tensors[sk][soff:soff + n].to(t.device))
         if ar.lowp is not None:
             ar.lowp.copy_(ar.master.to(ar.lowp.dtype))
-        st = getattr(opt, "state", {}).get(id(ar))
-        if st is not None:
-            for j, t in enumerate(st if isinstance(st, (tuple, list)) else (st,)):
-                key = f"arena{i}.opt{j}"
-                if key in tensors:
-                    t.zero_()
-                    t[:used].copy_(tensors[key][:used].to(t.device))
     for k, v in meta.get("optimizer", {}).items():
         if hasattr(opt, k) and not callable(getattr(opt, k)):
             setattr(opt, k, v)

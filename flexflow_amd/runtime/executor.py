@@ -248,7 +248,8 @@ class Executor:
         self._upd_stream = None
         self._upd_done = set()
         self._overlap_active = False
-        self._opt_next_done = False
+        self._opt_next_done = None  # the optimizer whose next() the overlapped backward already ran
+        self._bwd_since_update = 0   # backward passes since the last update (row-sparse SGD guard)
         self.bucketer.on_ready = self._on_bucket_ready
         # workgroup cap of the overlapped update launches (FF_UPD_BLOCKS; 0 = the full 2048 grid)
         self._upd_blocks = int(os.environ.get("FF_UPD_BLOCKS", "0"))
@@ -547,10 +548,11 @@ class Executor:
         self.bucketer.reset()
         self._upd_done = set()
         self._overlap_active = bool(overlap_update) and self._overlap_possible()
-        self._opt_next_done = False
+        self._opt_next_done = None
+        self._bwd_since_update += 1
         if self._overlap_active:
             self.model.optimizer.next()  # this step's bias-corrected scalars, before any bucket update
-            self._opt_next_done = True
+            self._opt_next_done = self.model.optimizer
         self._wdone = {}
         grads: Dict[int, torch.Tensor] = {}
         if self.output_tensor is not None and self.loss_type is not None:
@@ -768,7 +770,10 @@ class Executor:
         decay), so a row no id touched keeps a zero gradient and would not move; the table is
         this rank's alone (no gradient all-reduce), its layer is its only user and carries no
         regularizer. {arena group: [(entry index, layer name)]}. FF_SPARSE_EMB=0 disables."""
-        key = id(optimizer)
+        # hyper-parameters are part of the key: setting momentum / weight decay on the same
+        # optimizer object after the first update must switch the tables back to the dense step
+        key = (id(optimizer), getattr(optimizer, "momentum", None), getattr(optimizer, "weight_decay", None),
+               getattr(optimizer, "nesterov", None))
         if self._sparse_key == key:
             return self._sparse
         plan = {}
@@ -813,15 +818,20 @@ class Executor:
             self.wait_all_gathers()
         self.bucketer.flush()
         self._apply_regularizers()
-        if not self._opt_next_done:
+        if self._opt_next_done is not optimizer:
             optimizer.next()
         self._master_stale = False
         overlapped = self._overlap_active and optimizer is self.model.optimizer
+        # the row-sparse update only knows the rows of the LAST backward's ids: after several
+        # backward passes without an update the accumulated table gradient can hold other rows too,
+        # so this update runs dense (and zero_gradients then clears the whole table)
+        multi_bwd = self._bwd_since_update > 1
+        self._bwd_since_update = 0
         for grp, ar in self.arenas.items():
             if not ar.size:
                 continue
             bs = self.zero_buckets.get(grp)
-            sparse = self._sparse_plan(optimizer).get(grp) if bs is None else None
+            sparse = self._sparse_plan(optimizer).get(grp) if bs is None and not multi_bwd else None
             if sparse:
                 self._sparse_update(optimizer, grp, ar, sparse)
                 continue
@@ -848,7 +858,7 @@ class Executor:
             torch.cuda.current_stream(self.device).wait_stream(self._upd_stream)
         self._upd_done = set()
         self._overlap_active = False
-        self._opt_next_done = False
+        self._opt_next_done = None
         self.step_idx += 1
 
     def _sparse_update(self, optimizer, grp, ar, sparse):

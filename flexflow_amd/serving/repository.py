@@ -31,6 +31,10 @@ class ModelRepository:
         return sorted((v for v in os.listdir(d) if v.isdigit() and os.path.isdir(os.path.join(d, v))), key=int)
 
     def load(self, name: str) -> ServedModel:
+        # only names the repository lists (a plain directory under root): '..', absolute paths
+        # and separators in a request path must never reach os.path.join
+        if name not in self.names() or os.path.dirname(os.path.normpath(os.path.join(self.root, name))) != self.root:
+            raise KeyError(f"no model {name!r} in {self.root}")
         cfg_path = os.path.join(self.root, name, "config.pbtxt")
         if not os.path.isfile(cfg_path):
             raise KeyError(f"no model {name!r} in {self.root}")

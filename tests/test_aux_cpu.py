@@ -114,3 +114,59 @@ def test_launcher_argv():
     assert a[:2] == ["--nproc-per-node", "4"] and "127.0.0.1" in a and a[-3:] == ["train.py", "--epochs", "2"]
     b = build_argv(["--nproc=2", "--master-addr", "10.0.0.1", "x.py"])
     assert "127.0.0.1" not in b and b[-1] == "x.py"
+
+
+def test_checkpoint_from_training_loads_into_inference_model(tmp_path):
+    """Arena order differs between a training and an inference compile (accumulated gradients
+    first); the loader maps every weight by (layer position, slot), not by flat arena offset."""
+    ff, _ = _model(opt="adam")
+    ff.train_step()
+    ff.save_checkpoint(str(tmp_path / "ck"))
+    w_ref = [np.asarray(w.get_weights(ff)).copy() for L in ff.layers for w in L.weights]
+    cfg = FFConfig(["--no-hip-graphs"])
+    cfg.batch_size = 8
+    ff2 = FFModel(cfg)
+    build("mnist_mlp", ff2, 8, small=True)
+    ff2.optimizer = AdamOptimizer(ff2, 1e-3)
+    from flexflow_amd.type import CompMode
+    ff2.compile(comp_mode=CompMode.INFERENCE)
+    assert not ff2.executor.training
+    ff2.load_checkpoint(str(tmp_path / "ck"), strict=False)
+    w2 = [np.asarray(w.get_weights(ff2)).copy() for L in ff2.layers for w in L.weights]
+    assert len(w_ref) == len(w2)
+    for a, b in zip(w_ref, w2):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_checkpoint_rejects_mismatched_shapes(tmp_path):
+    ff, _ = _model(opt="adam")
+    ff.save_checkpoint(str(tmp_path / "ck"))
+    ff2, _ = _model(name="mlp_unify", opt="adam")
+    with pytest.raises(ValueError):
+        ff2.load_checkpoint(str(tmp_path / "ck"), strict=False)
+
+
+def test_update_with_other_optimizer_runs_its_next():
+    """backward(overlap_update) ran next() for the model's optimizer; an update() with another
+    optimizer object must still advance that optimizer's own Adam step."""
+    ff, _ = _model(opt="adam")
+    other = AdamOptimizer(ff, 1e-3)
+    ff.executor.init_optimizer(other)
+    ff.executor.zero_gradients()
+    ff.executor.forward()
+    ff.executor.backward(overlap_update=True)
+    t0 = other.beta1_t
+    ff.executor.update(other)
+    assert other.beta1_t != t0
+
+
+def test_model_repository_rejects_path_escape(tmp_path):
+    from flexflow_amd.serving.repository import ModelRepository
+    root = tmp_path / "repo"
+    root.mkdir()
+    (tmp_path / "evil").mkdir()
+    (tmp_path / "evil" / "config.pbtxt").write_text('name: "evil"')
+    repo = ModelRepository(str(root))
+    for name in ("../evil", "..", str(tmp_path / "evil")):
+        with pytest.raises(KeyError):
+            repo.load(name)

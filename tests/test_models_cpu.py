@@ -187,3 +187,48 @@ def test_sparse_embedding_sgd_matches_dense(monkeypatch):
     assert n1 > 0 and n0 == 0 and len(a) == len(b)
     for k, (x, y) in enumerate(zip(a, b)):
         np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-7, err_msg=str(k))
+
+
+def test_sparse_embedding_sgd_two_backwards_then_update(monkeypatch):
+    """forward/backward twice (different ids), then one update: rows touched only by the first
+    backward must move exactly as with the dense update (the row-sparse plan falls back to dense
+    when more than one backward ran since the last update)."""
+    def run(sparse):
+        if sparse:
+            monkeypatch.delenv("FF_SPARSE_EMB", raising=False)
+        else:
+            monkeypatch.setenv("FF_SPARSE_EMB", "0")
+        cfg = FFConfig(["--no-hip-graphs"])
+        cfg.batch_size = 4
+        ff = FFModel(cfg)
+        inputs, out, loss, mets, make_batch = build("dlrm", ff, 4, small=True)
+        ff.optimizer = SGDOptimizer(ff, 0.05)
+        ff.compile(loss_type=loss, metrics=mets)
+        rng = np.random.default_rng(1)
+        for step in range(2):
+            ff.zero_gradients()
+            for _ in range(2):
+                arrs, lab = make_batch(rng)
+                for t, a in zip(inputs, arrs):
+                    t.set_tensor(ff, a)
+                ff.label_tensor.set_tensor(ff, lab)
+                ff.forward()
+                ff.backward()
+            ff.update()
+        return [np.asarray(w.get_weights(ff)) for L in ff.layers for w in L.weights]
+
+    a, b = run(True), run(False)
+    for k, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-7, err_msg=str(k))
+
+
+def test_sparse_plan_follows_momentum_change():
+    cfg = FFConfig(["--no-hip-graphs"])
+    cfg.batch_size = 4
+    ff = FFModel(cfg)
+    _, _, loss, mets, _ = build("dlrm", ff, 4, small=True)
+    ff.optimizer = SGDOptimizer(ff, 0.05)
+    ff.compile(loss_type=loss, metrics=mets)
+    assert ff.executor._sparse_plan(ff.optimizer)
+    ff.optimizer.momentum = 0.9
+    assert not ff.executor._sparse_plan(ff.optimizer)
