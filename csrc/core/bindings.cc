@@ -133,7 +133,20 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("max_mem", &SimResult::max_mem)
       .def_readonly("oom", &SimResult::oom);
 
+  py::class_<SplitInfo>(m, "SplitInfo")
+      .def_readonly("start", &SplitInfo::start)
+      .def_readonly("end", &SplitInfo::end)
+      .def_readonly("components", &SplitInfo::components)
+      .def_readonly("groups", &SplitInfo::groups)
+      .def_readonly("group_of", &SplitInfo::group_of)
+      .def_readonly("whole_ms", &SplitInfo::whole_ms)
+      .def_readonly("split_ms", &SplitInfo::split_ms)
+      .def_readonly("sim_before_ms", &SplitInfo::sim_before_ms)
+      .def_readonly("sim_after_ms", &SplitInfo::sim_after_ms)
+      .def_readonly("accepted", &SplitInfo::accepted);
+
   py::class_<SearchResult>(m, "SearchResult")
+      .def_readonly("splits", &SearchResult::splits)
       .def_readonly("choice", &SearchResult::choice)
       .def_readonly("cost_ms", &SearchResult::cost_ms)
       .def_readonly("dp_cost_ms", &SearchResult::dp_cost_ms)
@@ -165,6 +178,10 @@ PYBIND11_MODULE(_core, m) {
         py::arg("alpha") = 1.2, py::arg("seed") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("search_unity", &search_unity, py::arg("problem"), py::arg("beam") = 4096, py::arg("refine_iters") = 500,
         py::arg("alpha") = 1.2, py::arg("seed") = 0, py::call_guard<py::gil_scoped_release>());
+
+  m.def("sequence_bottlenecks", &sequence_bottlenecks, py::arg("problem"));
+  m.def("search_split", &search_split, py::arg("problem"), py::arg("base"), py::arg("beam") = 4096,
+        py::call_guard<py::gil_scoped_release>());
 
   py::class_<RuleParam>(m, "RuleParam").def_readonly("key", &RuleParam::key).def_readonly("value", &RuleParam::value);
   py::class_<RuleTensor>(m, "RuleTensor").def_readonly("op_id", &RuleTensor::op_id).def_readonly("ts_id", &RuleTensor::ts_id);

@@ -142,7 +142,20 @@ class Simulator {
   mutable std::unordered_map<uint64_t, double> edge_cache_;
 };
 
+// One parallel-branch region examined by the non-sequence (resource-split) refinement.
+struct SplitInfo {
+  int start = -1, end = -1;      // bottleneck nodes bracketing the region (fork, join)
+  int components = 0;            // independent branches between them
+  int groups = 0;                // device groups tried (0: no feasible split)
+  std::vector<int> group_of;     // branch -> device group of the best split
+  double whole_ms = 0;           // additive region cost with every branch on the baseline configs
+  double split_ms = 0;           // max over device groups of the groups' additive costs
+  double sim_before_ms = 0, sim_after_ms = 0;  // whole-graph simulated makespans
+  bool accepted = false;
+};
+
 struct SearchResult {
+  std::vector<SplitInfo> splits;
   std::vector<int> choice;
   double cost_ms = 0;
   double dp_cost_ms = 0;
@@ -155,6 +168,13 @@ struct SearchResult {
 SearchResult search_dp(const Problem& p, int beam);
 SearchResult search_mcmc(const Problem& p, const std::vector<int>& init, int iterations, double alpha, uint64_t seed);
 SearchResult search_unity(const Problem& p, int beam, int refine_iters, double alpha, uint64_t seed);
+// Sequence split points: node i such that no producer -> consumer edge jumps over it.
+std::vector<int> sequence_bottlenecks(const Problem& p);
+// Non-sequence split refinement (reference SearchHelper::execute_nonsequence_split, graph.cc:188-330,
+// GraphSearchHelper::find_split_node, substitution.cc:2094): between two bottlenecks, independent
+// branches are re-searched on disjoint device groups; a split is kept when the simulator's makespan
+// (which runs branches on disjoint devices concurrently) improves.
+SearchResult search_split(const Problem& p, const std::vector<int>& base, int beam);
 
 // ------------------------------------------------------------------------------ substitutions
 struct RuleParam {

@@ -49,6 +49,7 @@ class FFConfig:
         self.allow_tensor_op_math_conversion = False
         self.import_strategy_file = ""
         self.export_strategy_file = ""
+        self.import_rewrites_file = ""  # graph rewrites of a joint search (strategy JSON or a list)
         self.export_strategy_task_graph_file = ""
         self.export_strategy_computation_graph_file = ""
         self.include_costs_dot_graph = False
@@ -142,6 +143,8 @@ class FFConfig:
                     self.import_strategy_file = nxt()
                 elif a in ("--export", "--export-strategy"):
                     self.export_strategy_file = nxt()
+                elif a == "--import-rewrites":
+                    self.import_rewrites_file = nxt()
                 elif a == "--only-data-parallel":
                     self.only_data_parallel = True
                 elif a == "--enable-parameter-parallel":

@@ -30,11 +30,28 @@ def _broadcast_strategy(model, strategy):
     return {k: OpConfig.from_json(v) for k, v in obj[0].items()}
 
 
+def _file_rewrites(path):
+    """Rewrite sequence stored in a strategy file's search report (joint search), or a bare list."""
+    if not path or path.endswith((".pb", ".strategy")):
+        return []
+    with open(path) as f:
+        doc = json.load(f)
+    rw = doc if isinstance(doc, list) else ((doc.get("search") or {}).get("rewrites") or doc.get("rewrites") or [])
+    return [(r["xfer"], r["match"]) if isinstance(r, dict) else tuple(r) for r in rw]
+
+
 def choose_strategy(model):
     cfg = model.config
-    layers = model.layers
     n = cfg.num_devices
     report = {"algo": None}
+    # a joint search's graph rewrites travel with its strategy file (or --import-rewrites): the
+    # imported configs name the rewritten layers, so the graph is rebuilt first
+    seq = _file_rewrites(cfg.import_rewrites_file) or _file_rewrites(cfg.import_strategy_file)
+    if seq:
+        from .joint import replay_broadcast
+        replay_broadcast(model, seq)
+        report["rewrites"] = [{"xfer": a, "match": b} for a, b in seq]
+    layers = model.layers
     if cfg.import_strategy_file:
         if cfg.import_strategy_file.endswith(".pb"):  # the reference's protobuf strategy files
             strat = load_strategy_pb(cfg.import_strategy_file, layers, n)
@@ -64,12 +81,24 @@ def choose_strategy(model):
         report["algo"] = "data_parallel(fallback: native core not built)"
         return data_parallel_strategy(layers, n), report
     distributed = dist.is_available() and dist.is_initialized() and cfg.world_size > 1
+    # joint Unity search (graph rewrites x parallelization) by default at N > 1; --search mcmc and
+    # FF_JOINT=0 search configs on the graph as written
+    joint = algo == "unity" and os.environ.get("FF_JOINT", "1") != "0" and not seq
     if distributed and cfg.rank != 0:
-        # rank 0 searches (its measured costs decide); everyone else receives the result
-        obj = [None, None]
+        # rank 0 searches (its measured costs decide); everyone else receives the result and, for
+        # the joint search, replays rank 0's rewrite sequence on its own copy of the graph
+        obj = [None, None, None]
         dist.broadcast_object_list(obj, src=0)
+        if obj[2]:
+            from .joint import replay_broadcast
+            replay_broadcast(model, obj[2])
         return {k: OpConfig.from_json(v) for k, v in obj[0].items()}, obj[1]
-    strat, report = native_search(model, algo)
+    seq = []
+    if joint:
+        from .joint import joint_search
+        strat, report, seq = joint_search(model, algo)
+    else:
+        strat, report = native_search(model, algo)
     if distributed:
-        dist.broadcast_object_list([{k: v.to_json() for k, v in strat.items()}, report], src=0)
+        dist.broadcast_object_list([{k: v.to_json() for k, v in strat.items()}, report, seq], src=0)
     return strat, report

@@ -183,9 +183,43 @@ def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute
         degs[a] = 1
 
     rec(0, 1)
-    # prefer configs using more devices first; cap the list
-    out.sort(key=lambda c: (-c.num_parts, c.devices[0], c.degrees))
-    return out[:max_configs]
+    pinned = layer.attrs.get("pin")
+    if pinned is not None:  # a pin_parallel rewrite (pcg/joint.py) fixed this op's degrees
+        out = [c for c in out if tuple(c.degrees) == tuple(pinned)] or \
+            [OpConfig(tuple(pinned), tuple(range(int(math.prod(pinned)))))]
+    return _cap_candidates(out, max_configs)
+
+
+def _cap_candidates(cands: List[OpConfig], max_configs: int) -> List[OpConfig]:
+    """Cap the candidate list with a quota per part count (1, 2, 4, 8, ... devices), each quota
+    filled round-robin over the machine views of that size. Sorting by part count and truncating
+    (round 2) dropped every placement on fewer devices at 8 GPUs — a Linear has 34 configs using
+    8/4/2 devices — so operator placement and branch-parallel resource splits never reached the
+    DP. Any budget a small group leaves unused goes to the larger part counts."""
+    if len(cands) <= max_configs:
+        return sorted(cands, key=lambda c: (-c.num_parts, c.devices[0], c.degrees))
+    groups: Dict[int, List[OpConfig]] = {}
+    for c in sorted(cands, key=lambda c: (c.degrees, c.devices)):
+        groups.setdefault(c.num_parts, []).append(c)
+    for P, lst in groups.items():  # interleave the views: every device block shows up early
+        by_view: Dict[Tuple[int, ...], List[OpConfig]] = {}
+        for c in lst:
+            by_view.setdefault(c.devices, []).append(c)
+        views = sorted(by_view, key=lambda v: v[0])
+        inter = []
+        for k in range(max(len(v) for v in by_view.values())):
+            inter += [by_view[v][k] for v in views if k < len(by_view[v])]
+        groups[P] = inter
+    order = sorted(groups, reverse=True)
+    quota = max(1, max_configs // len(order))
+    take = {P: min(quota, len(groups[P])) for P in order}
+    spare = max_configs - sum(take.values())
+    for P in order:
+        extra = min(spare, len(groups[P]) - take[P])
+        take[P] += extra
+        spare -= extra
+    out = [c for P in order for c in groups[P][:take[P]]]
+    return out
 
 
 def data_parallel_config(layer, num_devices: int) -> OpConfig:
@@ -194,6 +228,9 @@ def data_parallel_config(layer, num_devices: int) -> OpConfig:
     pin = getattr(layer.impl, "pinned_config", None)
     if pin is not None:
         return pin(num_devices)
+    if layer.attrs.get("pin") is not None:  # pinned by a joint-search rewrite: its only layout
+        degs = tuple(layer.attrs["pin"])
+        return OpConfig(degs, tuple(range(int(math.prod(degs)))))
     sizes = layer.impl.axis_sizes()
     n = len(sizes)
     for d in sorted(divisors(num_devices), reverse=True):

@@ -172,6 +172,20 @@ def search(model, algo: str):
     else:
         res = run_search()
     choice = list(res.choice)
+    split_report = []
+    if algo != "mcmc" and n > 1 and os.environ.get("FF_NONSEQ_SPLIT", "1") != "0":
+        # resource-split refinement: parallel branches re-searched on disjoint device groups
+        sr = core.search_split(prob, choice, 4096)
+        for si in sr.splits:
+            split_report.append({"fork": model.layers[si.start].name, "join": model.layers[si.end].name,
+                                 "branches": si.components, "groups": si.groups,
+                                 "whole_ms": round(si.whole_ms, 4), "split_ms": round(si.split_ms, 4),
+                                 "sim_before_ms": round(si.sim_before_ms, 4), "sim_after_ms": round(si.sim_after_ms, 4),
+                                 "accepted": bool(si.accepted)})
+        if sr.cost_ms < res.cost_ms:
+            choice = list(sr.choice)
+            res = SimpleNamespace(choice=choice, cost_ms=sr.cost_ms, dp_cost_ms=res.dp_cost_ms, states=res.states,
+                                  iterations=res.iterations)
     if res.cost_ms > dp_sim:  # never pick something the simulator thinks is worse than DP
         choice = dp_choice
     strat = {L.name: cands[i][choice[i]] for i, L in enumerate(model.layers)}
@@ -183,6 +197,8 @@ def search(model, algo: str):
               "candidates": sum(len(c) for c in cands)}
     if mem_report is not None:
         report["memory_search"] = mem_report
+    if split_report:
+        report["nonsequence_splits"] = split_report
     return strat, report
 
 

@@ -227,7 +227,15 @@ class Executor:
                 unit = 16 * len(grp)
                 ar.size = (ar.size + unit - 1) // unit * unit
             ar.materialize()
-        self._rank_sets += [g for g in self.arenas.keys()]
+        # process groups are created collectively: every rank must list EVERY gradient-sync group
+        # (also those it is not part of) in the same order, not just its own arenas' groups —
+        # otherwise ranks call new_group on different sets and a strategy with replica subgroups
+        # smaller than the world (e.g. sample 2 x parameter 4 on 8 ranks) deadlocks at compile
+        all_groups = set()
+        for wl in self.weight_layout.values():
+            for blk in wl.blocks():
+                all_groups.add(tuple(sorted(wl.replica_group(blk))))
+        self._rank_sets += sorted(all_groups)
         bucket_bytes = int(self.config.grad_bucket_mb * (1 << 20))
         self.bucketer = GradBucketer(self.comm, bucket_bytes)
         self.zero_buckets = {}  # arena group -> sharded buckets

@@ -1,0 +1,198 @@
+"""Multi-rank (gloo, world 4 and 8) runs of SEARCHED and hand-built multi-axis strategies on CPU,
+each compared with a single-process run of the same graph (reference tests/multi_gpu_tests.sh:36-39
+runs every model at 1..N GPUs).
+
+* searched: the default compile() path at N > 1 — rank 0 runs the joint Unity search (graph
+  rewrites x per-op configs x resource splits) on the analytic cost model, broadcasts the rewrite
+  sequence and the strategy, every rank rebuilds the graph and trains 2 SGD steps. The single-
+  process reference replays the same rewrites (--import-rewrites) and trains data parallel.
+* 2-axis / 3-axis: Linear layers split over sample x parameter (2, 4) and sample x out x
+  reduction (2, 2, 2), with replica subgroups smaller than the world and several process groups.
+"""
+import json
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+B = 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _build(case, ff):
+    from flexflow_amd.core import ActiMode, DataType, LossType
+    rng = np.random.default_rng(3)
+    if case in ("dlrm_small", "inception_small"):
+        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
+    if case == "siblings":
+        # two Linears reading the same tensor: the joint search merges them (merge_siblings_linear)
+        x = ff.create_tensor([B, 32], DataType.DT_FLOAT, name="x")
+        a = ff.dense(x, 64, ActiMode.AC_MODE_RELU, name="da")
+        b = ff.dense(x, 64, ActiMode.AC_MODE_RELU, name="db")
+        t = ff.add(a, b, name="sum")
+        t = ff.dense(t, 10, name="head")
+        ff.softmax(t, name="sm")
+        feeds = [rng.standard_normal((B, 32)).astype(np.float32)]
+        lab = rng.integers(0, 10, (B, 1)).astype(np.int32)
+        return [x], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+    if case == "mlp2d":
+        x = ff.create_tensor([B, 16], DataType.DT_FLOAT, name="x")
+        t = ff.dense(x, 32, ActiMode.AC_MODE_RELU, name="d1")
+        t = ff.dense(t, 24, name="d2")
+        t = ff.dense(t, 16, name="d3")
+        ff.softmax(t, name="sm")
+        feeds = [rng.standard_normal((B, 16)).astype(np.float32)]
+        lab = rng.integers(0, 16, (B, 1)).astype(np.int32)
+        return [x], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+    if case == "bert_tiny":
+        from flexflow_amd.models.bert import BertConfig, build_bert
+        bc = BertConfig(hidden=32, heads=4, layers=2, ffn=64, vocab=64, max_pos=16, seq=8)
+        ids, pos, _ = build_bert(ff, B, bc)
+        feeds = [rng.integers(0, bc.vocab, (B, bc.seq)).astype(np.int32),
+                 np.tile(np.arange(bc.seq, dtype=np.int32), (B, 1))]
+        lab = rng.integers(0, bc.vocab, (B, bc.seq, 1)).astype(np.int32)
+        return [ids, pos], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+    from flexflow_amd.models import build
+    name = {"dlrm_small": "dlrm", "inception_small": "inception_v3"}[case]
+    inputs, _, loss, _, make_batch = build(name, ff, B, small=True)
+    arrs, lab = make_batch(rng)
+    return inputs, list(arrs), lab, loss
+
+
+def _strategy(case, ff, world):
+    """Hand-built multi-axis strategies (None: search)."""
+    from flexflow_amd.pcg.strategy import OpConfig
+    L = {l.name: l for l in ff.layers}
+
+    def cfg(name, degs, devs=None):
+        n = len(L[name].impl.axis_sizes())
+        d = list(degs) + [1] * (n - len(degs))
+        return OpConfig(tuple(d), tuple(devs if devs is not None else range(int(np.prod(d)))))
+
+    if case == "mlp2d" and world == 8:
+        # d1: sample 2 x out 4; d2: sample 2 x reduction 4 (partial sums over 4-rank subgroups);
+        # d3: sample 2 x out 2 x reduction 2; the loss on 4 ranks of sample parallelism
+        return {"x": cfg("x", [2], [0, 4]), "d1": cfg("d1", [2, 4]), "d2": cfg("d2", [2, 1, 4]),
+                "d3": cfg("d3", [2, 2, 2]), "sm": cfg("sm", [4], [1, 3, 5, 7])}
+    if case == "mlp2d" and world == 4:
+        return {"x": cfg("x", [4]), "d1": cfg("d1", [2, 2]), "d2": cfg("d2", [1, 2, 2]),
+                "d3": cfg("d3", [2, 2], [3, 2, 1, 0]), "sm": cfg("sm", [2], [2, 3])}
+    return None
+
+
+def _train(case, flags, world, out_file=None):
+    from flexflow_amd.core import FFConfig, FFModel, MetricsType, SGDOptimizer
+    cfg = FFConfig(["--no-hip-graphs"] + list(flags))
+    cfg.batch_size = B
+    ff = FFModel(cfg)
+    inputs, feeds, lab, loss = _build(case, ff)
+    ff.optimizer = SGDOptimizer(ff, 0.05)
+    ff.compile(loss_type=loss, metrics=[MetricsType.METRICS_ACCURACY])
+    for t, v in zip(inputs, feeds):
+        t.set_tensor(ff, v)
+    ff.label_tensor.set_tensor(ff, lab)
+    for _ in range(2):
+        ff.forward()
+        ff.zero_gradients()
+        ff.backward()
+        ff.update()
+    # positional keys: auto-generated layer names depend on how many layers the process built before
+    res = {f"{li}:{l.op_type.name}.{i}": np.asarray(w.get_weights(ff))
+           for li, l in enumerate(ff.layers) for i, w in enumerate(l.weights)}
+    res["__output__"] = np.asarray(ff._get_tensor_value(ff.output_tensor()), dtype=np.float32)
+    return ff, res
+
+
+def _worker(rank, world, port, case, flags, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), CUDA_VISIBLE_DEVICES="")
+    import torch
+    torch.set_num_threads(1)
+    ff, res = _train(case, flags, world)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "out.npz"), **res)
+        rep = ff.search_report or {}
+        with open(os.path.join(out_dir, "search.json"), "w") as f:
+            json.dump({"rewrites": rep.get("rewrites", []), "report": {k: v for k, v in rep.items() if k != "tried"},
+                       "strategy": {k: v.to_json() for k, v in ff.strategy.items()}}, f, default=str)
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(case, world, flags=()):
+    from flexflow_amd.core import FFConfig, FFModel
+    from flexflow_amd.pcg.strategy import save_strategy
+    tmp = tempfile.mkdtemp()
+    flags = list(flags)
+    ff = FFModel(FFConfig([]))
+    ff.config.batch_size = B
+    _build(case, ff)
+    s = _strategy(case, ff, world)
+    if s is not None:
+        sf = os.path.join(tmp, "s.json")
+        save_strategy(sf, s, world)
+        flags += ["--import-strategy", sf]
+    mp.start_processes(_worker, args=(world, _free_port(), case, flags, tmp), nprocs=world, join=True,
+                       start_method="spawn")
+    with open(os.path.join(tmp, "search.json")) as f:
+        search = json.load(f)
+    return dict(np.load(os.path.join(tmp, "out.npz"))), search, tmp
+
+
+def _single(case, rewrites_file=None):
+    old = {k: os.environ.pop(k, None) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    try:
+        flags = ["--import-rewrites", rewrites_file] if rewrites_file else []
+        return _train(case, flags, 1)[1]
+    finally:
+        for k, v in old.items():
+            if v is not None:
+                os.environ[k] = v
+
+
+def _compare(par, ref, tag, rtol=3e-4, atol=3e-5):
+    assert set(ref) == set(par), (tag, sorted(set(ref) ^ set(par)))
+    for k, v in ref.items():
+        np.testing.assert_allclose(par[k], v, rtol=rtol, atol=atol, err_msg=f"{tag}: {k}")
+
+
+@pytest.mark.parametrize("case,world", [("siblings", 2), ("bert_tiny", 4), ("dlrm_small", 8), ("bert_tiny", 8),
+                                        ("inception_small", 4)])
+def test_searched_strategy_matches_single(case, world, monkeypatch):
+    monkeypatch.setenv("FF_JOINT_BUDGET", "3")
+    par, search, tmp = _run(case, world)
+    rw = os.path.join(tmp, "rw.json")
+    with open(rw, "w") as f:
+        json.dump(search["rewrites"], f)
+    ref = _single(case, rw)
+    _compare(par, ref, f"{case}@{world}")
+    used = {d for v in search["strategy"].values() for d in v["devices"]}
+    print(case, world, "devices used", sorted(used), "rewrites", search["rewrites"],
+          {k: search["report"].get(k) for k in ("predicted_ms", "predicted_dp_ms", "graphs_costed")})
+    if case in ("dlrm_small", "inception_small"):
+        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
+    if case == "siblings":
+        # the accepted rewrite changed the graph the strategy is chosen for
+        assert any(r["xfer"] == "merge_siblings_linear" for r in search["rewrites"]), search["rewrites"]
+        assert any("&" in name for name in search["strategy"]), search["strategy"]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_multi_axis_strategy_matches_single(world):
+    par, _, _ = _run("mlp2d", world)
+    ref = _single("mlp2d")
+    _compare(par, ref, f"mlp2d@{world}")
