@@ -11,6 +11,7 @@
 #define FLEXFLOW_AMD_HPP
 
 #include <chrono>
+#include <iterator>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
@@ -84,12 +85,11 @@ class Tensor {
   flexflow_tensor_t raw() const { return h_.raw(); }
   bool valid() const { return h_.valid(); }
   int num_dims() const { return flexflow_tensor_get_num_dims(raw()); }
-  std::vector<int> dims() const {
-    std::vector<int> d(16);
-    const int n = flexflow_tensor_get_dims(raw(), d.data());
-    detail::check(n >= 0, "Tensor::dims");
-    d.resize(n);
-    return d;
+  std::vector<int> dims() const {  // outermost first (the C API reports Legion order)
+    const int n = flexflow_tensor_get_num_dims(raw());
+    const int* d = flexflow_tensor_get_dims(raw());
+    detail::check(n >= 0 && d != nullptr, "Tensor::dims");
+    return std::vector<int>(std::reverse_iterator<const int*>(d + n), std::reverse_iterator<const int*>(d));
   }
   int dim(int i) const {
     const auto d = dims();
@@ -120,14 +120,64 @@ class FFModel;
 
 class Optimizer {
  public:
-  flexflow_optimizer_t raw() const { return h_.raw(); }
-  void set_learning_rate(double lr) { flexflow_optimizer_set_lr(raw(), lr); }
+  flexflow_optimizer_t raw() const {
+    flexflow_optimizer_t o;
+    o.impl = h_.raw().impl;
+    return o;
+  }
+  // the typed C handles share one implementation (a Python optimizer object), so the SGD entry
+  // points serve both kinds here
+  void set_learning_rate(double lr) { flexflow_sgd_optimizer_set_lr(h_.raw(), lr); }
 
  protected:
-  Optimizer(flexflow_optimizer_t h, const char* what) : h_(h, what) {}
+  template <typename H>
+  Optimizer(H h, const char* what) : h_(as_sgd(h.impl), what) {}
 
  private:
-  detail::Handle<flexflow_optimizer_t, flexflow_optimizer_destroy> h_;
+  static flexflow_sgd_optimizer_t as_sgd(void* impl) {
+    flexflow_sgd_optimizer_t s;
+    s.impl = impl;
+    return s;
+  }
+  detail::Handle<flexflow_sgd_optimizer_t, flexflow_sgd_optimizer_destroy> h_;
+};
+
+// weight initializers (reference include/flexflow/initializer.h); a default-constructed one is the
+// op's default initializer
+class Initializer {
+ public:
+  Initializer() = default;
+  flexflow_initializer_t raw() const {
+    flexflow_initializer_t i;
+    i.impl = h_.valid() ? h_.raw().impl : nullptr;
+    return i;
+  }
+
+ protected:
+  template <typename H>
+  Initializer(H h, const char* what) : h_(as_generic(h.impl), what) {}
+
+ private:
+  static flexflow_norm_initializer_t as_generic(void* impl) {
+    flexflow_norm_initializer_t n;
+    n.impl = impl;
+    return n;
+  }
+  detail::Handle<flexflow_norm_initializer_t, flexflow_norm_initializer_destroy> h_;
+};
+struct GlorotUniformInitializer : Initializer {
+  explicit GlorotUniformInitializer(int seed) : Initializer(flexflow_glorot_uniform_initializer_create(seed), "glorot") {}
+};
+struct ZeroInitializer : Initializer {
+  ZeroInitializer() : Initializer(flexflow_zero_initializer_create(), "zero") {}
+};
+struct UniformInitializer : Initializer {
+  UniformInitializer(int seed, float mn, float mx)
+      : Initializer(flexflow_uniform_initializer_create(seed, mn, mx), "uniform") {}
+};
+struct NormInitializer : Initializer {
+  NormInitializer(int seed, float mean, float stddev)
+      : Initializer(flexflow_norm_initializer_create(seed, mean, stddev), "norm") {}
 };
 
 class FFModel {
@@ -160,13 +210,17 @@ class FFModel {
 
   // ------------------------------------------------------------------ layers
   Tensor dense(const Tensor& x, int out_dim, ActiMode act = AC_MODE_NONE, bool use_bias = true,
-               const char* name = nullptr) {
-    return Tensor(flexflow_model_add_dense(raw(), x.raw(), out_dim, act, use_bias, name), "dense");
+               const char* name = nullptr, const Initializer& kernel_init = Initializer(),
+               const Initializer& bias_init = Initializer()) {
+    return Tensor(flexflow_model_add_dense(raw(), x.raw(), out_dim, act, use_bias, DT_FLOAT, no_op(), kernel_init.raw(),
+                                           bias_init.raw(), 17 /* REG_MODE_NONE */, 0.f, name),
+                  "dense");
   }
   Tensor conv2d(const Tensor& x, int out_channels, int kh, int kw, int sh, int sw, int ph, int pw,
-                ActiMode act = AC_MODE_NONE, int groups = 1, bool use_bias = true, const char* name = nullptr) {
+                ActiMode act = AC_MODE_NONE, int groups = 1, bool use_bias = true, const char* name = nullptr,
+                const Initializer& kernel_init = Initializer(), const Initializer& bias_init = Initializer()) {
     return Tensor(flexflow_model_add_conv2d(raw(), x.raw(), out_channels, kh, kw, sh, sw, ph, pw, act, groups,
-                                            use_bias, name),
+                                            use_bias, no_op(), kernel_init.raw(), bias_init.raw(), name),
                   "conv2d");
   }
   Tensor pool2d(const Tensor& x, int kh, int kw, int sh, int sw, int ph, int pw, PoolType type = POOL_MAX,
@@ -178,7 +232,8 @@ class FFModel {
   }
   Tensor layer_norm(const Tensor& x, const std::vector<int>& axes, bool affine = true, float eps = 1e-5f,
                     const char* name = nullptr) {
-    return Tensor(flexflow_model_add_layer_norm(raw(), x.raw(), (int)axes.size(), axes.data(), affine, eps, name),
+    std::vector<int> a(axes);
+    return Tensor(flexflow_model_add_layer_norm(raw(), x.raw(), (int)a.size(), a.data(), affine, eps, name),
                   "layer_norm");
   }
   Tensor rms_norm(const Tensor& x, float eps = 1e-6f, const char* name = nullptr) {
@@ -193,11 +248,13 @@ class FFModel {
                              int kdim = 0, int vdim = 0, float dropout = 0.f, bool bias = true,
                              const char* name = nullptr) {
     return Tensor(flexflow_model_add_multihead_attention(raw(), q.raw(), k.raw(), v.raw(), embed_dim, num_heads,
-                                                         kdim, vdim, dropout, bias, name),
+                                                         kdim, vdim, dropout, bias, false, false,
+                                                         Initializer().raw(), name),
                   "multihead_attention");
   }
-  Tensor batch_matmul(const Tensor& a, const Tensor& b, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_batch_matmul(raw(), a.raw(), b.raw(), name), "batch_matmul");
+  Tensor batch_matmul(const Tensor& a, const Tensor& b, int a_seq_length_dim = -1, int b_seq_length_dim = -1) {
+    return Tensor(flexflow_model_add_batch_matmul(raw(), a.raw(), b.raw(), a_seq_length_dim, b_seq_length_dim),
+                  "batch_matmul");
   }
   Tensor flat(const Tensor& x, const char* name = nullptr) {
     return Tensor(flexflow_model_add_flat(raw(), x.raw(), name), "flat");
@@ -209,26 +266,32 @@ class FFModel {
     return Tensor(flexflow_model_add_dropout(raw(), x.raw(), rate, seed, name), "dropout");
   }
   Tensor reshape(const Tensor& x, const std::vector<int>& shape, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_reshape(raw(), x.raw(), (int)shape.size(), shape.data(), name), "reshape");
+    std::vector<int> v(shape);
+    return Tensor(flexflow_model_add_reshape(raw(), x.raw(), (int)v.size(), v.data(), name), "reshape");
   }
   Tensor transpose(const Tensor& x, const std::vector<int>& perm, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_transpose(raw(), x.raw(), (int)perm.size(), perm.data(), name), "transpose");
+    std::vector<int> v(perm);
+    return Tensor(flexflow_model_add_transpose(raw(), x.raw(), (int)v.size(), v.data(), name), "transpose");
   }
   Tensor concat(const std::vector<Tensor>& xs, int axis, const char* name = nullptr) {
-    const auto r = raws(xs);
+    auto r = raws(xs);
     return Tensor(flexflow_model_add_concat(raw(), (int)r.size(), r.data(), axis, name), "concat");
   }
   std::vector<Tensor> split(const Tensor& x, const std::vector<int>& sizes, int axis, const char* name = nullptr) {
     std::vector<flexflow_tensor_t> out(sizes.size());
-    const int n = flexflow_model_add_split(raw(), x.raw(), (int)sizes.size(), sizes.data(), axis, out.data(), name);
-    return adopt(out, n, "split");
+    std::vector<int> v(sizes);
+    for (auto& o : out) o.impl = nullptr;
+    flexflow_model_add_split(raw(), x.raw(), (int)v.size(), out.data(), v.data(), axis, name);
+    return adopt(out, out.empty() || out.back().impl ? (int)out.size() : -1, "split");
   }
   Tensor mean(const Tensor& x, const std::vector<int>& dims, bool keepdims = false, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_mean(raw(), x.raw(), (int)dims.size(), dims.data(), keepdims, name), "mean");
+    std::vector<int> v(dims);
+    return Tensor(flexflow_model_add_mean(raw(), x.raw(), v.data(), (int)v.size(), keepdims, name), "mean");
   }
   Tensor reduce_sum(const Tensor& x, const std::vector<int>& axes, bool keepdims = false,
                     const char* name = nullptr) {
-    return Tensor(flexflow_model_add_reduce_sum(raw(), x.raw(), (int)axes.size(), axes.data(), keepdims, name),
+    std::vector<int> v(axes);
+    return Tensor(flexflow_model_add_reduce_sum(raw(), x.raw(), v.data(), (int)v.size(), keepdims, name),
                   "reduce_sum");
   }
   Tensor gather(const Tensor& x, const Tensor& index, int dim, const char* name = nullptr) {
@@ -269,20 +332,24 @@ class FFModel {
   Tensor fn(const Tensor& x, const char* name = nullptr) {                   \
     return Tensor(flexflow_model_add_##fn(raw(), x.raw(), name), #fn);      \
   }
-  FF_UNARY(relu)
   FF_UNARY(gelu)
   FF_UNARY(sigmoid)
   FF_UNARY(tanh)
-  FF_UNARY(elu)
   FF_UNARY(identity)
   FF_UNARY(exp)
   FF_UNARY(sin)
   FF_UNARY(cos)
   FF_UNARY(rsqrt)
 #undef FF_UNARY
-#define FF_BINARY(fn)                                                             \
-  Tensor fn(const Tensor& a, const Tensor& b, const char* name = nullptr) {       \
-    return Tensor(flexflow_model_add_##fn(raw(), a.raw(), b.raw(), name), #fn);  \
+  Tensor relu(const Tensor& x, const char* name = nullptr) {
+    return Tensor(flexflow_model_add_relu(raw(), x.raw(), false, name), "relu");
+  }
+  Tensor elu(const Tensor& x, const char* name = nullptr) {
+    return Tensor(flexflow_model_add_elu(raw(), x.raw(), false, name), "elu");
+  }
+#define FF_BINARY(fn)                                                                    \
+  Tensor fn(const Tensor& a, const Tensor& b, const char* name = nullptr) {              \
+    return Tensor(flexflow_model_add_##fn(raw(), a.raw(), b.raw(), false, name), #fn);  \
   }
   FF_BINARY(add)
   FF_BINARY(subtract)
@@ -292,10 +359,10 @@ class FFModel {
   FF_BINARY(min)
 #undef FF_BINARY
   Tensor scalar_multiply(const Tensor& x, float s, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_scalar_multiply(raw(), x.raw(), s, name), "scalar_multiply");
+    return Tensor(flexflow_model_add_scalar_multiply(raw(), x.raw(), s, false, name), "scalar_multiply");
   }
   Tensor scalar_add(const Tensor& x, float s, const char* name = nullptr) {
-    return Tensor(flexflow_model_add_scalar_add(raw(), x.raw(), s, name), "scalar_add");
+    return Tensor(flexflow_model_add_scalar_add(raw(), x.raw(), s, false, name), "scalar_add");
   }
   Tensor pow(const Tensor& x, float e, const char* name = nullptr) {
     return Tensor(flexflow_model_add_pow(raw(), x.raw(), e, name), "pow");
@@ -325,6 +392,11 @@ class FFModel {
   std::string strategy_name() { return flexflow_model_get_strategy_name(raw()); }
 
  private:
+  static flexflow_op_t no_op() {
+    flexflow_op_t o;
+    o.impl = nullptr;
+    return o;
+  }
   static std::vector<flexflow_tensor_t> raws(const std::vector<Tensor>& xs) {
     std::vector<flexflow_tensor_t> r;
     r.reserve(xs.size());

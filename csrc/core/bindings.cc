@@ -161,6 +161,7 @@ PYBIND11_MODULE(_core, m) {
       .value("ALL_REDUCE", XferKind::ALL_REDUCE)
       .value("REDUCE_SCATTER", XferKind::REDUCE_SCATTER)
       .value("ALL_GATHER", XferKind::ALL_GATHER)
+      .value("ALL_TO_ALL", XferKind::ALL_TO_ALL)
       .value("GENERIC", XferKind::GENERIC);
 
   py::class_<XferCost>(m, "XferCost")

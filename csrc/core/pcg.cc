@@ -110,6 +110,38 @@ int64_t overlap(const Region& a, const Region& b) {
 
 }  // namespace
 
+// D re-partitions S from dim a to dim b, k ways, on the same devices, no replicas (runtime:
+// flexflow_amd.parallel.comm._a2a_dims, executed as one all_to_all per group).
+static bool is_all_to_all(const Layout& S, const Layout& D) {
+  if (S.replicas != 1 || D.replicas != 1 || !S.halo.empty() || !D.halo.empty() || S.degrees.size() != D.degrees.size())
+    return false;
+  int a = -1, b = -1, ndiff = 0;
+  for (size_t d = 0; d < S.degrees.size(); ++d) {
+    if (S.degrees[d] == D.degrees[d]) continue;
+    ++ndiff;
+    if (S.degrees[d] > 1 && D.degrees[d] == 1) a = (int)d;
+    else if (D.degrees[d] > 1 && S.degrees[d] == 1) b = (int)d;
+  }
+  if (ndiff != 2 || a < 0 || b < 0 || S.degrees[a] != D.degrees[b]) return false;
+  const int k = S.degrees[a];
+  for (int blk = 0; blk < S.num_blocks(); ++blk) {
+    auto c = S.block_coords(blk);
+    if (c[a] != 0) continue;
+    std::set<int> sd, dd;
+    for (int i = 0; i < k; ++i) {
+      auto o = c;
+      o[a] = i;
+      sd.insert(S.devices[S.part_index(o, 0)]);
+      o = c;
+      o[a] = 0;
+      o[b] = i;
+      dd.insert(D.devices[D.part_index(o, 0)]);
+    }
+    if ((int)sd.size() != k || sd != dd) return false;
+  }
+  return true;
+}
+
 XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const MachineModel& mm) {
   XferCost x;
   const bool same_blocks = S.degrees == D.degrees;
@@ -185,8 +217,9 @@ XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const 
       }
     }
   }
-  // generic point-to-point plan: same region-intersection rule as the runtime's plan_transfer
-  x.kind = XferKind::GENERIC;
+  // generic point-to-point plan: same region-intersection rule as the runtime's plan_transfer;
+  // an all-to-all is priced the same way (every pair over its own xGMI link at once)
+  x.kind = (!sp && is_all_to_all(S, D)) ? XferKind::ALL_TO_ALL : XferKind::GENERIC;
   std::map<std::pair<int, int>, double> link;
   const bool halo_sum = !S.halo.empty() && sp;
   for (int q = 0; q < D.num_parts(); ++q) {

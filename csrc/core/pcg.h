@@ -101,7 +101,7 @@ struct MachineModel {
 };
 
 // Collective classification of a layout conversion (mirror of flexflow_amd.parallel.comm.Transfer).
-enum class XferKind { IDENTITY, LOCAL_SLICE, ALL_REDUCE, REDUCE_SCATTER, ALL_GATHER, GENERIC };
+enum class XferKind { IDENTITY, LOCAL_SLICE, ALL_REDUCE, REDUCE_SCATTER, ALL_GATHER, ALL_TO_ALL, GENERIC };
 
 struct XferCost {
   XferKind kind = XferKind::IDENTITY;

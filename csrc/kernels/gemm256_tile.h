@@ -1,5 +1,5 @@
 // Shared tile machinery of the 256-row MFMA GEMMs (gemm256.hip: one output tile per workgroup;
-// gemm_persist.hip: persistent workgroups whose LDS-DMA ring runs on across tile boundaries).
+// kept separate so that variants can be built as their own translation units, guide rule 19).
 #pragma once
 #include "common.h"
 #include "gemm.h"

@@ -76,6 +76,7 @@ class FFConfig:
         self.search_algo = "unity"  # unity | mcmc | dp (data-parallel only) | none
         self.mcmc_iterations = 2000
         self.grad_bucket_mb = 64.0
+        self.grad_comm_dtype = "fp32"  # --grad-comm-dtype bf16: gradient buckets travel as bf16
         self.zero_optimizer = False   # --zero: ZeRO-1 sharded optimizer state / update on DP arenas
         # train_step runs each gradient bucket's optimizer update on a side stream as soon as the
         # bucket is final (all-reduced), overlapping the rest of the backward (runtime/executor.py
@@ -226,6 +227,10 @@ class FFConfig:
                     self.overlap_update = False
                 elif a == "--grad-bucket-mb":
                     self.grad_bucket_mb = float(nxt())
+                elif a == "--grad-comm-dtype":
+                    self.grad_comm_dtype = nxt()
+                    if self.grad_comm_dtype not in ("fp32", "bf16"):
+                        raise ValueError(f"--grad-comm-dtype must be fp32 or bf16, not {self.grad_comm_dtype!r}")
                 elif a == "--seed":
                     self.seed = int(nxt())
                 elif a == "--trace-dir":

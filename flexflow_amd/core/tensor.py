@@ -74,7 +74,10 @@ class Tensor:
             np_array = ffconfig
         self._attached = np.ascontiguousarray(np_array)
         if getattr(ffmodel, "_compiled", False):
-            ffmodel._set_tensor_value(self, self._attached)
+            try:
+                ffmodel._set_tensor_value(self, self._attached)  # a graph input: feed it now
+            except KeyError:
+                pass  # not part of the compiled graph (e.g. a whole dataset for a data loader)
         self.mapped = True
 
     def detach_numpy_array(self, ffconfig=None):
@@ -91,12 +94,15 @@ class Tensor:
         """The tensor's values as numpy. Before compile (or when called with an FFConfig, as the
         reference's `get_array(ffconfig, dtype)` after `inline_map`) this is the host array the
         tensor is attached to — writable, and fed to the model at compile."""
-        if not getattr(ffmodel, "_compiled", False):
-            if self._attached is None:
-                self._attached = np.zeros(tuple(self.dims), dtype=np.int32 if self.data_type in (
-                    DataType.DT_INT32, DataType.DT_INT64) else np.float32)
-            return self._attached
-        return self.get_tensor(ffmodel)
+        if getattr(ffmodel, "_compiled", False):
+            try:
+                return self.get_tensor(ffmodel)
+            except KeyError:
+                pass  # not part of the compiled graph: the host array it is attached to
+        if self._attached is None:
+            self._attached = np.zeros(tuple(self.dims), dtype=np.int32 if self.data_type in (
+                DataType.DT_INT32, DataType.DT_INT64) else np.float32)
+        return self._attached
 
     def get_flat_array(self, ffmodel, ffconfig=None):
         return self.get_tensor(ffmodel).reshape(-1)

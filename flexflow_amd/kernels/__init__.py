@@ -72,7 +72,7 @@ import os as _os
 
 _TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
 # our kernels: 256-row ping-pong (csrc/kernels/gemm256.hip), 256x128 LDS-DMA (gemm_big.hip), 128x128
-IMPLS = {"p256": 3, "k256": 2, "big": 1, "128": 0}
+IMPLS = {"k256": 2, "big": 1, "128": 0}
 IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []
@@ -486,12 +486,13 @@ def linear_fwd(x2d, w, bias, act, save_z):
     return y, z
 
 
-def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None):
+def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None, on_dx=None):
     """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+= ; dw_beta=0 overwrites dw
     when the executor knows this op is the weight's only user). dx_out: an existing input gradient
     [M, K] to accumulate into (dgrad GEMM with beta = 1, no separate add). dact = (z, act, db) of
     the Linear that produced x: the returned dx is then already that producer's pre-activation
-    gradient (and its bias gradient is summed), see gemm_dact. Returns dx (or None)."""
+    gradient (and its bias gradient is summed), see gemm_dact. on_dx(dx) is called between the
+    dgrad and the wgrad GEMM (the executor starts dx's collective there). Returns dx (or None)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     if act != ACT_NONE:
@@ -506,6 +507,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
         dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
         gemm_dact(dz, w, dx, dact[0], dact[2], M, K, N, True, False, N, K, K, dact[1])
         need_dx = False
+        if on_dx is not None:
+            on_dx(dx)
     if native(dy2d) and dy2d.dtype == torch.bfloat16:
         if need_dx:
             if dx_out is not None:
@@ -514,6 +517,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
             else:
                 dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
                 gemm(dz, w, dx, M, K, N, True, False, N, K, K)
+            if on_dx is not None:
+                on_dx(dx)
         if dw is not None:
             gemm(dz, x2d, dw, N, K, M, False, False, N, K, K, beta=dw_beta)
         return dx
@@ -525,6 +530,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
             dx = dx_out
         else:
             dx = dxf.to(dy2d.dtype)
+        if on_dx is not None:
+            on_dx(dx)
     if dw is not None:
         if dw_beta == 0.0:
             dw.copy_(dzf.t() @ x2d.float())
@@ -576,6 +583,14 @@ def bmm(a, b, trans_a=False, trans_b=False, out=None):
 # ------------------------------------------------------------------------------ attention
 def attn_supported(x, D):
     return native(x) and x.dtype == torch.bfloat16 and D in (64, 128)
+
+
+def attn_padded_dim(x, kd, vd):
+    """Head dim (64 / 128) the MFMA attention runs a smaller equal q/k/v head dim at, zero-padded;
+    0 when the kernels cannot run it (different q/k and v dims, or above 128)."""
+    if not (native(x) and x.dtype == torch.bfloat16) or kd != vd or kd > 128:
+        return 0
+    return 64 if kd <= 64 else 128
 
 
 def flash_attn_fwd(q, qs, k, ks, v, vs, o, os_, B, H, Sq, Sk, D, scale, causal):

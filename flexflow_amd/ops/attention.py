@@ -14,12 +14,20 @@ projection GEMM; the backward mirrors it (flash bwd writes dQ/dK/dV straight int
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from .. import kernels as K
 from ..type import OperatorType
 from .base import OpImpl, WeightSpec, register
+
+
+def _pad_heads(t, st, B, S, H, d, Dp):
+    """[B, S, H, Dp] zero-padded copy of the strided per-head view (batch, head, row strides st)."""
+    out = torch.zeros(B, S, H, Dp, device=t.device, dtype=t.dtype)
+    out[..., :d].copy_(t.as_strided((B, H, S, d), (st[0], st[1], st[2], 1)).permute(0, 2, 1, 3))
+    return out
 
 
 def _attn_ref(q, k, v, scale, causal):
@@ -143,7 +151,25 @@ class MultiHeadAttention(OpImpl):
         if K.attn_supported(q_in, kd) and kd == vd:
             lse = K.flash_attn_fwd(qv, qs, kv, ks, vv, vs, o, os_, B, Hl, Sq, Sk, kd, scale, causal)
             s["lse"] = lse
+        elif K.attn_padded_dim(q_in, kd, vd):
+            # head dims the MFMA kernels have no instance for (e.g. 16, 32, 80, 96): zero-pad Q, K,
+            # V to the next instance (64 / 128). Zero columns add nothing to Q.K^T and give zero
+            # output columns, so the softmax and the sliced output are exact; the scale stays
+            # 1/sqrt(kd)
+            Dp = K.attn_padded_dim(q_in, kd, vd)
+            pq, pk, pv = (_pad_heads(t, st, Bq, S_, Hl, kd, Dp) for t, st, Bq, S_ in
+                          ((qv, qs, B, Sq), (kv, ks, B, Sk), (vv, vs, B, Sk)))
+            po = torch.empty(B, Sq, Hl, Dp, device=q_in.device, dtype=q_in.dtype)
+            pst = [Sq * Hl * Dp, Dp, Hl * Dp]
+            kst = [Sk * Hl * Dp, Dp, Hl * Dp]
+            lse = K.flash_attn_fwd(pq, pst, pk, kst, pv, kst, po, pst, B, Hl, Sq, Sk, Dp, scale, causal)
+            o.copy_(po[..., :vd])
+            s.update(lse=lse, pad=(Dp, pq, pk, pv, po))
         else:
+            if K.native(q_in) and q_in.dtype == torch.bfloat16 and os.environ.get("FF_ATTN_REF_FALLBACK") != "1":
+                raise NotImplementedError(
+                    f"{self.layer.name}: no MFMA attention kernel for head dims q/k {kd}, v {vd} (supported: equal "
+                    "q/k/v head dims up to 128; FF_ATTN_REF_FALLBACK=1 runs the fp32 PyTorch reference instead)")
             q4 = qv.as_strided((B, Hl, Sq, kd), (qs[0], qs[1], qs[2], 1)).float()
             k4 = kv.as_strided((B, Hl, Sk, kd), (ks[0], ks[1], ks[2], 1)).float()
             v4 = vv.as_strided((B, Hl, Sk, vd), (vs[0], vs[1], vs[2], 1)).float()
@@ -187,7 +213,18 @@ class MultiHeadAttention(OpImpl):
         else:
             qv, kv, vv = s["q"], s["k"], s["v"]
             dq, dk, dv = torch.empty_like(qv), torch.empty_like(kv), torch.empty_like(vv)
-        if "lse" in s:
+        if "pad" in s:
+            Dp, pq, pk, pv, po = s["pad"]
+            pdo = torch.zeros_like(po)
+            pdo[..., :vd] = do
+            pdq, pdk, pdv = torch.empty_like(pq), torch.empty_like(pk), torch.empty_like(pv)
+            pst = [Sq * Hl * Dp, Dp, Hl * Dp]
+            kst = [Sk * Hl * Dp, Dp, Hl * Dp]
+            K.flash_attn_bwd(pq, pst, pk, kst, pv, kst, po, pst, pdo, pst, s["lse"], pdq, pst, pdk, kst, pdv, kst,
+                             B, Hl, Sq, Sk, Dp, scale, causal)
+            for g, st, pg, S_, d in ((dq, qs, pdq, Sq, kd), (dk, ks, pdk, Sk, kd), (dv, vs, pdv, Sk, vd)):
+                g.as_strided((B, Hl, S_, d), (st[0], st[1], st[2], 1)).copy_(pg[..., :d].permute(0, 2, 1, 3))
+        elif "lse" in s:
             K.flash_attn_bwd(qv, qs, kv, ks, vv, vs, o, os_, do, os_, s["lse"], dq, qs, dk, ks, dv, vs,
                              B, Hl, Sq, Sk, kd, scale, causal)
         else:

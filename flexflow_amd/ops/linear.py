@@ -105,13 +105,19 @@ class Linear(OpImpl):
             if len(pctx.wgrads) > 1 and pctx.saved.get("has_b") and not pctx.extra.get("bias_grad_fused"):
                 pdb = pctx.wgrads[1]
             dact = (pctx.saved["z"].reshape(-1, x2.shape[1]), pact, pdb)
+        ready = ctx.extra.get("dx_ready")
+        out_shape = tuple(dy.shape[:-1]) + (x2.shape[1],)
+        on_dx = None
+        if ready is not None:
+            def on_dx(d):  # the executor starts dx's transfer before the wgrad GEMM
+                ready(0, acc if acc is not None else d.reshape(out_shape))
         dx = K.linear_bwd(dy2, x2, w, z, act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
                           dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0,
-                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None, dact=dact)
+                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None, dact=dact, on_dx=on_dx)
         ctx.saved.clear()
         if dx is None:
             return [None]
-        return [acc if acc is not None else dx.reshape(tuple(dy.shape[:-1]) + (x2.shape[1],))]
+        return [acc if acc is not None else dx.reshape(out_shape)]
 
     def accumulates_dx(self):
         return True

@@ -9,13 +9,23 @@ src/parallel_ops/kernels/*.cu) with explicit collectives chosen per edge:
     all_gather        partitioned -> replicated                      (Combine / Replicate)
     reduce_scatter    partial    -> partitioned                      (Reduction + Repartition)
     all_reduce        partial    -> replicated                       (Reduction + Replicate)
+    all_to_all        partitioned along a -> partitioned along b     (Combine(a) + Repartition(b)
+                      on the same devices: every rank sends 1/k of its shard to each peer,
+                      one link per peer on the fully connected xGMI node)
     generic P2P       anything else (placement changes, halos, uneven device sets):
                       batched isend/irecv of exactly the overlapping blocks.
 
 and the weight-gradient synchronisation (reference: one ncclAllReduce per weight followed by an
 execution fence, src/runtime/optimizer_kernel.cu:88-94 / optimizer.cc:193) with bucketed
 all-reduces over flat fp32 gradient arenas, issued asynchronously as soon as a bucket's last
-gradient is produced so they overlap the rest of the backward pass.
+gradient is produced so they overlap the rest of the backward pass (optionally in bf16, halving
+the bytes: --grad-comm-dtype bf16).
+
+Every transfer can be started asynchronously (`Transfer.start` -> `Pending`): with RCCL the
+collective is enqueued on the process group's own stream behind an event on the compute stream,
+and `Pending.wait()` makes the compute stream (not the host) wait for it, so the executor issues
+activation collectives as soon as their producer has run and waits only where the consumer needs
+the value (runtime/executor.py).
 """
 from __future__ import annotations
 
@@ -83,6 +93,64 @@ def _find_split_dim(a: Layout, b: Layout, factor: int) -> Optional[int]:
     return cand
 
 
+class Pending:
+    """An in-flight transfer: wait() returns this rank's destination part (or None)."""
+
+    def __init__(self, handles=(), finish=None, value=None, kind="identity", nbytes=0):
+        self.handles = [h for h in handles if h is not None]
+        self.finish = finish
+        self.value = value
+        self.kind = kind
+        self.nbytes = nbytes
+        self.done = not self.handles and finish is None
+
+    def wait(self):
+        if not self.done:
+            for h in self.handles:
+                h.wait()
+            if self.finish is not None:
+                self.value = self.finish()
+            self.done = True
+            self.handles = []
+            self.finish = None
+        return self.value
+
+
+def _a2a_dims(S: Layout, D: Layout):
+    """(a, b, k) when D re-partitions S from dim a to dim b k ways on the same devices, no replicas."""
+    if S.replicas != 1 or D.replicas != 1 or S.halo or D.halo or len(S.degrees) != len(D.degrees):
+        return None
+    diff = [d for d in range(len(S.degrees)) if S.degrees[d] != D.degrees[d]]
+    if len(diff) != 2:
+        return None
+    a = [d for d in diff if S.degrees[d] > 1 and D.degrees[d] == 1]
+    b = [d for d in diff if D.degrees[d] > 1 and S.degrees[d] == 1]
+    if len(a) != 1 or len(b) != 1 or S.degrees[a[0]] != D.degrees[b[0]]:
+        return None
+    a, b = a[0], b[0]
+    k = S.degrees[a]
+    for blk in S.blocks():
+        if blk[a] != 0:
+            continue
+        sd, dd = _a2a_devices(S, D, blk, a, b, k)
+        if len(set(sd)) != k or set(sd) != set(dd):
+            return None
+    return a, b, k
+
+
+def _a2a_devices(S, D, blk, a, b, k):
+    sd, dd = [], []
+    for i in range(k):
+        o = list(blk)
+        o[a] = i
+        sd.append(S.devices[S.part_index(o, 0)])
+        o = list(blk)
+        o[a] = 0
+        o[b] = i
+        dd.append(D.devices[D.part_index(o, 0)])
+    return sd, dd
+
+
 class Transfer:
     """A planned layout conversion for one tensor edge, executed by every rank (SPMD)."""
 
@@ -126,6 +194,11 @@ class Transfer:
             if d is not None and self._subblock_devices_match(S, D, d, S.replicas, subset=True):
                 self.kind, self.dim = "local_slice", d
                 return
+        if not sp:
+            a2a = _a2a_dims(S, D)
+            if a2a is not None:
+                self.kind, self.dim = "all_to_all", a2a
+                return
 
     @staticmethod
     def _subblock_devices_match(coarse: Layout, fine: Layout, d: int, k: int, subset=False) -> bool:
@@ -156,6 +229,11 @@ class Transfer:
         elif self.kind == "all_gather":
             for b in self.dst.blocks():
                 out.append(tuple(sorted(self.dst.replica_group(b))))
+        elif self.kind == "all_to_all":
+            a, b, k = self.dim
+            for blk in self.src.blocks():
+                if blk[a] == 0:
+                    out.append(tuple(sorted(_a2a_devices(self.src, self.dst, blk, a, b, k)[0])))
         return out
 
     def bytes_moved(self, elem_bytes: int) -> int:
@@ -177,6 +255,9 @@ class Transfer:
             return int((r - 1) / r * n * elem_bytes)
         if self.kind == "all_gather":
             return int((self.dst.replicas - 1) * n * elem_bytes)
+        if self.kind == "all_to_all":
+            k = self.dim[2]
+            return int((k - 1) / k * n * elem_bytes)
         tot = 0
         for it in self.items or []:
             if S.devices[it.src_part] == self.rank and self.dst.devices[it.dst_part] != self.rank:
@@ -189,31 +270,62 @@ class Transfer:
     # ------------------------------------------------------------------ execution
     def run(self, comm: Communicator, x: Optional[torch.Tensor], like: Optional[torch.Tensor] = None):
         """x: this rank's src part (or None). Returns this rank's dst part (or None)."""
+        return self.start(comm, x, like).wait()
+
+    def start(self, comm: Communicator, x: Optional[torch.Tensor], like: Optional[torch.Tensor] = None) -> Pending:
+        """Issue the transfer without waiting for it (every rank, same order); see Pending."""
         S, D, r = self.src, self.dst, self.rank
         dparts = D.parts_on(r)
         sparts = S.parts_on(r)
         if self.kind == "identity":
-            return x
+            return Pending(value=x)
         if self.kind == "local_slice":
             if not dparts:
-                return None
+                return Pending(value=None)
             q = dparts[0]
-            return x[_slices(D.region(q), S.region(sparts[0]))].contiguous()
+            return Pending(value=x[_slices(D.region(q), S.region(sparts[0]))].contiguous(), kind=self.kind)
+        nb = self.bytes_moved(x.element_size() if x is not None else 2)
         if self.kind == "all_reduce":
             if x is None:
-                return None
+                return Pending(value=None)
             grp = tuple(sorted(S.replica_group(S.coords(sparts[0])[0])))
             y = x.contiguous().clone() if not x.is_contiguous() else x
-            if len(grp) > 1:
-                dist.all_reduce(y, group=comm.group(grp))
-            return y
+            if len(grp) <= 1:
+                return Pending(value=y)
+            h = dist.all_reduce(y, group=comm.group(grp), async_op=True)
+            return Pending([h], lambda: y, kind=self.kind, nbytes=nb)
         if self.kind == "reduce_scatter":
             if x is None:
-                return None
+                return Pending(value=None)
             return self._reduce_scatter(comm, x)
         if self.kind == "all_gather":
-            return self._all_gather(comm, x) if (x is not None or dparts) else None
+            if x is None and not dparts:
+                return Pending(value=None)
+            return self._all_gather(comm, x)
+        if self.kind == "all_to_all":
+            if x is None:
+                return Pending(value=None)
+            return self._all_to_all(comm, x)
         return self._generic(comm, x, like)
+
+    def _all_to_all(self, comm, x):
+        S, D, r = self.src, self.dst, self.rank
+        a, b, k = self.dim
+        blk = list(S.coords(S.parts_on(r)[0])[0])
+        me = blk[a]
+        blk[a] = 0
+        sdev, ddev = _a2a_devices(S, D, blk, a, b, k)
+        grp = sorted(sdev)
+        chunks = x.chunk(k, dim=b)  # chunk j belongs to the rank holding dst block j along b
+        inp = torch.stack([chunks[ddev.index(g)] for g in grp], 0).contiguous()
+        out = torch.empty_like(inp)
+        h = dist.all_to_all_single(out, inp, group=comm.group(grp), async_op=True)
+
+        def finish():
+            # out[q] came from group rank q, which holds src block sdev.index(grp[q]) along a
+            return torch.cat([out[grp.index(sdev[i])] for i in range(k)], dim=a).contiguous()
+        del me
+        return Pending([h], finish, kind="all_to_all", nbytes=self.bytes_moved(x.element_size()))
 
     def _reduce_scatter(self, comm, x):
         S, D, d, r = self.src, self.dst, self.dim, self.rank
@@ -234,13 +346,15 @@ class Transfer:
         out_shape[0] //= k
         out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
         g = comm.group(grp)
+        nb = self.bytes_moved(x.element_size())
         if comm.is_nccl:
-            dist.reduce_scatter_tensor(out, inp, group=g)
-        else:  # gloo: no reduce_scatter; all_reduce then keep own chunk
-            tmp = inp.clone()
-            dist.all_reduce(tmp, group=g)
-            out.copy_(tmp.chunk(k, 0)[grp.index(r)])
-        return out.movedim(0, d).contiguous()
+            h = dist.reduce_scatter_tensor(out, inp, group=g, async_op=True)
+            return Pending([h], lambda: out.movedim(0, d).contiguous(), kind="reduce_scatter", nbytes=nb)
+        # gloo: no reduce_scatter; all_reduce then keep own chunk
+        tmp = inp.clone()
+        h = dist.all_reduce(tmp, group=g, async_op=True)
+        return Pending([h], lambda: tmp.chunk(k, 0)[grp.index(r)].movedim(0, d).contiguous(), kind="reduce_scatter",
+                       nbytes=nb)
 
     def _all_gather(self, comm, x):
         S, D, d, r = self.src, self.dst, self.dim, self.rank
@@ -254,16 +368,20 @@ class Transfer:
             sub_dev.append(S.devices[S.part_index(fb, 0)])
         xm = x.movedim(d, 0).contiguous()
         g = comm.group(grp)
+        nb = self.bytes_moved(x.element_size())
         if comm.is_nccl:
             out = torch.empty((k * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
-            dist.all_gather_into_tensor(out, xm, group=g)
+            h = dist.all_gather_into_tensor(out, xm, group=g, async_op=True)
             chunks = list(out.chunk(k, 0))
         else:
             chunks = [torch.empty_like(xm) for _ in range(k)]
-            dist.all_gather(chunks, xm, group=g)
-        # chunks[i] came from group-rank i == device grp[i]; reorder to dim order
-        ordered = [chunks[grp.index(dev)] for dev in sub_dev]
-        return torch.cat(ordered, 0).movedim(0, d).contiguous()
+            h = dist.all_gather(chunks, xm, group=g, async_op=True)
+
+        def finish():
+            # chunks[i] came from group-rank i == device grp[i]; reorder to dim order
+            ordered = [chunks[grp.index(dev)] for dev in sub_dev]
+            return torch.cat(ordered, 0).movedim(0, d).contiguous()
+        return Pending([h], finish, kind="all_gather", nbytes=nb)
 
     def _generic(self, comm, x, like):
         S, D, r = self.src, self.dst, self.rank
@@ -296,18 +414,36 @@ class Transfer:
                 buf = torch.empty(shp, dtype=ref.dtype, device=ref.device)
                 ops.append(dist.P2POp(dist.irecv, buf, sd))
                 pending.append(("recv", buf, it, None))
-        if ops:
-            reqs = dist.batch_isend_irecv(ops)
-            for q in reqs:
-                q.wait()
-        for kind, buf, it, _ in pending:
-            if kind == "recv":
-                dst_view = out[_slices(it.region, D.region(it.dst_part))]
-                if it.reduce:
-                    dst_view.add_(buf)
-                else:
-                    dst_view.copy_(buf)
-        return out
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+
+        def finish():
+            for kind, buf, it, _ in pending:
+                if kind == "recv":
+                    dst_view = out[_slices(it.region, D.region(it.dst_part))]
+                    if it.reduce:
+                        dst_view.add_(buf)
+                    else:
+                        dst_view.copy_(buf)
+            return out
+        return Pending(reqs, finish, kind="generic", nbytes=sum(b.numel() * b.element_size()
+                                                               for k_, b, _, _ in pending if k_ == "send"))
+
+
+class _WidenBack:
+    """Handle of a bf16 gradient collective: wait() waits for it, then widens the summed bf16
+    bucket back into its fp32 arena slice (on the waiting stream)."""
+
+    def __init__(self, handle, low, dst, keep=None):
+        self.handle, self.low, self.dst, self.keep = handle, low, dst, keep
+        self.done = False
+
+    def wait(self):
+        if not self.done:
+            self.handle.wait()
+            self.dst.copy_(self.low)
+            self.done = True
+            self.low = self.keep = None
+        return True
 
 
 class GradBucketer:
@@ -319,9 +455,12 @@ class GradBucketer:
     (config.grad_bucket_mb, default 64 MiB: few, large collectives).
     """
 
-    def __init__(self, comm: Communicator, bucket_bytes: int):
+    def __init__(self, comm: Communicator, bucket_bytes: int, comm_dtype: Optional[torch.dtype] = None):
         self.comm = comm
         self.bucket_bytes = bucket_bytes
+        # bf16 gradient collectives (--grad-comm-dtype bf16): the bucket travels as bf16 (half the
+        # xGMI bytes) and is widened back into the fp32 arena, where the optimizer accumulates
+        self.comm_dtype = comm_dtype if comm_dtype not in (None, torch.float32) else None
         self.arenas = []  # (group_ranks, flat_grad, [buckets]) ; bucket = dict(lo, hi, params:set, ready:set)
         self.param_bucket = {}
         self.param_buckets = {}  # sharded arenas: a parameter may straddle bucket boundaries
@@ -394,7 +533,16 @@ class GradBucketer:
             return None
         view = b["flat"][b["lo"]:b["hi"]]
         g = self.comm.group(b["group"])
-        if b.get("sharded"):  # in-place reduce-scatter: this rank's chunk of the bucket gets the sum
+        if self.comm_dtype is not None:
+            low = view.to(self.comm_dtype)
+            if b.get("sharded"):
+                lo, hi = b["own"]
+                out_low = torch.empty(hi - lo, dtype=self.comm_dtype, device=view.device)
+                h = _WidenBack(dist.reduce_scatter_tensor(out_low, low, group=g, async_op=True), out_low,
+                               b["flat"][lo:hi], keep=low)
+            else:
+                h = _WidenBack(dist.all_reduce(low, group=g, async_op=True), low, view)
+        elif b.get("sharded"):  # in-place reduce-scatter: this rank's chunk of the bucket gets the sum
             out = b["flat"][b["own"][0]:b["own"][1]]
             h = dist.reduce_scatter_tensor(out, view, group=g, async_op=True)
         else:

@@ -175,6 +175,22 @@ class Executor:
                     if p:
                         self.ctx[L.name].extra["out_region"] = lo.outputs[0].region(p[0])
         self._rank_sets = rank_sets
+        # forward consumers of every tensor, in layer order (the order every rank issues the
+        # prefetched transfers in: collectives must be issued in the same order on all ranks)
+        self._consumers: Dict[int, List[Tuple[str, int]]] = {}
+        for L in self.layers:
+            if L.op_type == OperatorType.OP_INPUT:
+                continue
+            seen = set()
+            for j, t in enumerate(L.inputs):
+                k = (t.guid, self.lay[L.name].inputs[j].key())
+                if k in seen:
+                    continue  # a repeated (tensor, layout) input is moved once (forward's cache)
+                seen.add(k)
+                self._consumers.setdefault(t.guid, []).append((L.name, j))
+        self.overlap_comm = os.environ.get("FF_OVERLAP_COMM", "1") != "0"
+        self.comm_trace = None  # list of (event, kind, edge, op counter) when tracing (profiler / tests)
+        self._op_counter = 0
 
     def _alloc_weights(self):
         lowp = torch.bfloat16 if self.cdt == DataType.DT_BF16 else None
@@ -237,7 +253,8 @@ class Executor:
                 all_groups.add(tuple(sorted(wl.replica_group(blk))))
         self._rank_sets += sorted(all_groups)
         bucket_bytes = int(self.config.grad_bucket_mb * (1 << 20))
-        self.bucketer = GradBucketer(self.comm, bucket_bytes)
+        cdt = torch.bfloat16 if getattr(self.config, "grad_comm_dtype", "fp32") == "bf16" else None
+        self.bucketer = GradBucketer(self.comm, bucket_bytes, cdt)
         self.zero_buckets = {}  # arena group -> sharded buckets
         self._w_buckets = {}    # weight guid -> [(arena group, bucket index)]
         self._ag_pending = {}   # (arena group, bucket index) -> async all-gather handle
@@ -390,20 +407,50 @@ class Executor:
             for o, v in zip(L.outputs, outs):
                 vals[o.guid] = v
 
+    def _trace(self, event, kind, edge):
+        if self.comm_trace is not None:
+            self.comm_trace.append((event, kind, edge, self._op_counter))
+        for h in self.hooks:
+            if hasattr(h, "comm_event"):
+                h.comm_event(event, kind, edge)
+
+    def _prefetch(self, L, inflight):
+        """Start the forward transfers of L's outputs to every consumer right after L ran (every
+        rank, layer order): with RCCL the collective runs on the process group's stream while the
+        compute stream goes on with the ops in between; the consumer waits only for its own input."""
+        if not self.overlap_comm:
+            return
+        vals = self.values
+        for o in L.outputs:
+            for cname, j in self._consumers.get(o.guid, ()):
+                tx = self.fwd_tx[(cname, j)]
+                if tx.kind in ("identity", "local_slice"):
+                    continue
+                p = inflight[(cname, j)] = tx.start(self.comm, vals.get(o.guid), self._like(o))
+                p.edge = ("fwd", cname, j)
+                self._trace("issue", tx.kind, p.edge)
+
     def forward(self, training: Optional[bool] = None):
         tr = self.training if training is None else training
         self._fwd_training = tr
         vals = self.values
+        inflight = {}
         for L in self.layers:
             if L.op_type == OperatorType.OP_INPUT:
                 o = L.outputs[0]
                 vals[o.guid] = self.inputs.get(o.guid) if self.local[L.name] else None
+                self._prefetch(L, inflight)
                 continue
             xs, cache = [], {}
             for j, t in enumerate(L.inputs):
                 key = (t.guid, self.lay[L.name].inputs[j].key())
                 if key not in cache:
-                    cache[key] = self.fwd_tx[(L.name, j)].run(self.comm, vals.get(t.guid), self._like(t))
+                    p = inflight.pop((L.name, j), None)
+                    if p is not None:
+                        cache[key] = p.wait()
+                        self._trace("wait", p.kind, p.edge)
+                    else:
+                        cache[key] = self.fwd_tx[(L.name, j)].run(self.comm, vals.get(t.guid), self._like(t))
                 xs.append(cache[key])
             if self.local[L.name]:
                 ctx = self.ctx[L.name]
@@ -424,6 +471,10 @@ class Executor:
             else:
                 for o in L.outputs:
                     vals[o.guid] = None
+            self._op_counter += 1
+            self._prefetch(L, inflight)
+        for p in inflight.values():  # outputs nobody consumed (e.g. the model output's own edges)
+            p.wait()
 
     def compute_loss_grad(self):
         """Loss gradient w.r.t. the model output (reference Loss::backward, scale 1/batch or
@@ -563,6 +614,17 @@ class Executor:
             self._opt_next_done = self.model.optimizer
         self._wdone = {}
         grads: Dict[int, torch.Tensor] = {}
+        gpend: Dict[int, list] = {}  # tensor guid -> in-flight gradient transfers (summed on use)
+
+        def resolve(guid):
+            for p in gpend.pop(guid, ()):
+                v = p.wait()
+                self._trace("wait", p.kind, p.edge)
+                if v is None:
+                    continue
+                prev = grads.get(guid)
+                grads[guid] = v if (prev is None or prev is v) else prev + v
+
         if self.output_tensor is not None and self.loss_type is not None:
             g = self.compute_loss_grad()
             if g is not None:
@@ -571,7 +633,10 @@ class Executor:
             if not self.layer_bwd.get(L.name):
                 continue
             dxs = None
+            early = {}
             if self.local[L.name]:
+                for o in L.outputs:
+                    resolve(o.guid)
                 douts = [grads.pop(o.guid, None) for o in L.outputs]
                 if any(d is not None for d in douts):
                     ref = [d for d in douts if d is not None][0]
@@ -579,17 +644,26 @@ class Executor:
                     douts = [d if d is not None else (torch.zeros_like(v) if v is not None else None)
                              for d, v in zip(douts, vals)]
                     ctx = self.ctx[L.name]
+                    for t in L.inputs:
+                        resolve(t.guid)  # in-place dgrad accumulation needs the concrete tensor
                     ctx.extra["dx_accum"] = self._accum_targets(L, grads, douts)
+                    ctx.extra["dx_ready"] = self._dx_ready_cb(L, early) if self.overlap_comm else None
                     if self.hooks:
                         with self._hooked(L, "bwd"):
                             dxs = L.impl.backward(ctx, douts)
                     else:
                         dxs = L.impl.backward(ctx, douts)
                     ctx.extra["dx_accum"] = None
+                    ctx.extra["dx_ready"] = None
                 for w in L.weights:
                     self._wdone[w.guid] = self._wdone.get(w.guid, 0) + 1
                     if self._wdone[w.guid] == self.weight_users.get(w.guid, 1):
                         self.bucketer.mark_ready(w.guid)
+            else:
+                for o in L.outputs:
+                    resolve(o.guid)
+                    grads.pop(o.guid, None)
+            self._op_counter += 1
             pending = {}
             for j, t in enumerate(L.inputs):
                 if not self.in_grad.get((L.name, j)):
@@ -603,10 +677,44 @@ class Executor:
                 else:
                     pending[key] = [t, j, gj]
             for key, (t, j, gj) in pending.items():
-                gp = self.bwd_tx[(L.name, j)].run(self.comm, gj, self._like(t))
-                if gp is not None:
-                    prev = grads.get(t.guid)
-                    grads[t.guid] = gp if (prev is None or prev is gp) else prev + gp
+                tx = self.bwd_tx[(L.name, j)]
+                p = early.pop(j, None)
+                same = p is not None and gj is not None and p[1].data_ptr() == gj.data_ptr() and \
+                    p[1].shape == gj.shape
+                if not same:
+                    if p is not None:
+                        p[0].wait()  # superseded (the op changed the tensor after announcing it)
+                    if tx.kind == "identity" or not self.overlap_comm:
+                        gp = tx.run(self.comm, gj, self._like(t))
+                        if gp is not None:
+                            prev = grads.get(t.guid)
+                            grads[t.guid] = gp if (prev is None or prev is gp) else prev + gp
+                        continue
+                    p = (tx.start(self.comm, gj, self._like(t)), gj)
+                    p[0].edge = ("bwd", L.name, j)
+                    self._trace("issue", tx.kind, p[0].edge)
+                gpend.setdefault(t.guid, []).append(p[0])
+        for guid in list(gpend):
+            resolve(guid)
+
+    def _dx_ready_cb(self, L, early):
+        """Callback an op's backward may call as soon as input j's gradient is final (Linear: after
+        the dgrad GEMM, before the wgrad GEMM): the gradient's transfer (e.g. the all-reduce of a
+        row-parallel layer's partial dx) starts then and runs beside the wgrad GEMM."""
+        counts = {}
+        for t in L.inputs:
+            counts[t.guid] = counts.get(t.guid, 0) + 1
+
+        def ready(j, g):
+            t = L.inputs[j]
+            tx = self.bwd_tx.get((L.name, j))
+            if (tx is None or not self.in_grad.get((L.name, j)) or counts[t.guid] != 1
+                    or tx.kind == "identity" or j in early or g is None):
+                return
+            early[j] = (tx.start(self.comm, g, self._like(t)), g)
+            early[j][0].edge = ("bwd", L.name, j)
+            self._trace("issue", tx.kind, early[j][0].edge)
+        return ready
 
     def _plan_inplace(self):
         """Reference in-place optimisation (model.cc:2885-2919): an element-wise op whose gradient

@@ -25,6 +25,8 @@ class OpProfiler:
         self.rank = rank
         self.cuda = executor.device.type == "cuda"
         self.records: List[tuple] = []  # (step, layer name, op type, phase, start, end)
+        self.comm: List[tuple] = []     # (step, kind, edge, issue mark, wait mark)
+        self._issued: Dict[tuple, tuple] = {}
         self.step = 0
         self._t0 = None
 
@@ -43,6 +45,17 @@ class OpProfiler:
         yield
         e = self._mark()
         self.records.append((self.step, layer.name, layer.op_type.name, phase, s, e))
+
+    def comm_event(self, event, kind, edge):
+        """Executor hook: an asynchronous transfer was issued / waited for. Each becomes a span on
+        the trace's communication track (tid 2), beside the op spans of the compute stream."""
+        if self._t0 is None:
+            self._t0 = self._mark()
+        if event == "issue":
+            self._issued[edge] = (kind, self._mark())
+        elif edge in self._issued:
+            k, s = self._issued.pop(edge)
+            self.comm.append((self.step, k, edge, s, self._mark()))
 
     def next_step(self):
         self.step += 1
@@ -89,6 +102,10 @@ class OpProfiler:
             dur = self._ms(s, e) * 1e3
             ev.append({"name": f"{name} {phase}", "cat": op, "ph": "X", "ts": ts, "dur": max(dur, 0.001),
                        "pid": self.rank, "tid": 0 if phase == "fwd" else 1, "args": {"step": step}})
+        for step, kind, edge, s, e in self.comm:
+            ev.append({"name": f"{kind} {'/'.join(str(x) for x in edge)}", "cat": "comm", "ph": "X",
+                       "ts": self._ms(self._t0, s) * 1e3, "dur": max(self._ms(s, e) * 1e3, 0.001),
+                       "pid": self.rank, "tid": 2, "args": {"step": step, "stream": "process-group"}})
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
         with open(path, "w") as f:
             json.dump({"traceEvents": ev, "displayTimeUnit": "ms"}, f)

@@ -2,7 +2,7 @@
 """Every BERT-Large (batch 32, seq 512) GEMM call-site shape, our MFMA kernels against the vendor
 library, timed in ONE process in interleaved rounds (best of rounds), on uniform random data.
 
-usage: gemm_bert_probe.py [impls=p256,k256,lib] [rounds=3] [reps=20] [filter=fwd,dgrad,wgrad]
+usage: gemm_bert_probe.py [impls=k256,lib] [rounds=3] [reps=20] [filter=fwd,dgrad,wgrad]
 Prints one line per (shape, impl) plus a per-orientation summary weighted by call counts.
 """
 import sys
@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 from flexflow_amd import kernels as Kn  # noqa: E402
 
-impls = (sys.argv[1] if len(sys.argv) > 1 else "p256,k256,lib").split(",")
+impls = (sys.argv[1] if len(sys.argv) > 1 else "k256,lib").split(",")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 kinds = (sys.argv[4] if len(sys.argv) > 4 else "fwd,dgrad,wgrad").split(",")
@@ -35,7 +35,7 @@ SHAPES = [
     ("wgrad", 1024, 4096, T, False, False, 24, True),
     ("wgrad", 30522, 1024, T, False, False, 1, True),
 ]
-IMP = {"p256": 3, "k256": 2, "big": 1, "128": 0}
+IMP = {"k256": 2, "big": 1, "128": 0}
 dev = "cuda"
 X = Kn.ext()
 

@@ -44,7 +44,8 @@ def _core_layout(l: Layout):
 
 
 KIND = {"identity": "IDENTITY", "local_slice": "LOCAL_SLICE", "all_reduce": "ALL_REDUCE",
-        "reduce_scatter": "REDUCE_SCATTER", "all_gather": "ALL_GATHER", "generic": "GENERIC"}
+        "reduce_scatter": "REDUCE_SCATTER", "all_gather": "ALL_GATHER", "all_to_all": "ALL_TO_ALL",
+        "generic": "GENERIC"}
 
 
 @pytest.mark.parametrize("src_deg,dst_deg,rep_s,rep_d,partial", [
@@ -53,7 +54,7 @@ KIND = {"identity": "IDENTITY", "local_slice": "LOCAL_SLICE", "all_reduce": "ALL
     ((4, 1), (1, 1), 1, 4, False),     # sharded -> replicated: all-gather
     ((1, 1), (1, 1), 4, 4, True),      # partial sums -> replicated: all-reduce
     ((1, 1), (4, 1), 4, 1, True),      # partial sums -> sharded: reduce-scatter
-    ((4, 1), (1, 4), 1, 1, False),     # row -> column sharding: generic P2P (all-to-all)
+    ((4, 1), (1, 4), 1, 1, False),     # row -> column sharding on the same ranks: all-to-all
 ])
 def test_transfer_classification_matches_runtime(src_deg, dst_deg, rep_s, rep_d, partial):
     shape = (16, 8)

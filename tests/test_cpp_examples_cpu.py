@@ -13,6 +13,9 @@ PROGRAMS = ["AlexNet/alexnet", "ResNet/resnet", "resnext50/resnext", "InceptionV
             "DLRM/dlrm", "XDL/xdl", "candle_uno/candle_uno", "Transformer/transformer", "mixture_of_experts/moe",
             "split_test/split_test", "split_test_2/split_test_2"]
 
+# the examples are rebuilt when their source or any API header is newer than the binary
+_HDRS = max(os.path.getmtime(os.path.join(ROOT, "csrc", "capi", h)) for h in ("flexflow_c.h", "flexflow.hpp"))
+
 
 def build_examples():
     if not os.path.exists(os.path.join(ROOT, "flexflow_amd", "libflexflow_c.so")):
@@ -20,7 +23,7 @@ def build_examples():
         import build_ext
         build_ext.build_capi()
     missing = [p for p in PROGRAMS if not os.path.exists(os.path.join(EX, p))
-               or os.path.getmtime(os.path.join(EX, p)) < os.path.getmtime(os.path.join(EX, p + ".cc"))]
+               or os.path.getmtime(os.path.join(EX, p)) < max(os.path.getmtime(os.path.join(EX, p + ".cc")), _HDRS)]
     if missing:
         subprocess.run([os.path.join(EX, "build.sh")] + sorted({p.split("/")[0] for p in missing}), check=True)
 

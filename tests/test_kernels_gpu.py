@@ -27,7 +27,7 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
                                    (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
-@pytest.mark.parametrize("impl", [3, 2, 1, 0])
+@pytest.mark.parametrize("impl", [2, 1, 0])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -57,30 +57,6 @@ def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk):
     assert _rel(C, ref) < 1e-2
     C32 = torch.ones(M, N, device=DEV)
     _gemm(ffC, A, B, C32, M, N, K, a_k, b_k, beta=1.0, splitk=splitk, ws=ws, impl=2)
-    assert _rel(C32, ref + 1.0) < 1e-3
-
-
-@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(16384, 4096, 1024), (8192, 1024, 4096), (4096, 3072, 1024), (3000, 2000, 512),
-                                   (1024, 30522, 256)])
-def test_gemm_persistent_shapes(ffC, a_k, b_k, M, N, K):
-    """Persistent kernel (impl 3): several tiles per workgroup with the operand ring running on
-    across tile boundaries (BERT-Large forward / dgrad shapes, ragged edge tiles, odd N), fused
-    bias + GELU + pre-activation store, and an fp32 beta = 1 output."""
-    torch.manual_seed(5)
-    Am = torch.randn(M, K, device=DEV).bfloat16()
-    Bn = torch.randn(N, K, device=DEV).bfloat16()
-    A = Am if a_k else Am.t().contiguous()
-    B = Bn if b_k else Bn.t().contiguous()
-    ref = Am.float() @ Bn.float().t()
-    bias = torch.randn(N, device=DEV)
-    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    Z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    _gemm(ffC, A, B, C, M, N, K, a_k, b_k, bias=bias, Z=Z, act=14, impl=3)
-    assert _rel(Z, ref + bias) < 1e-2
-    assert _rel(C, torch.nn.functional.gelu(ref + bias)) < 1e-2
-    C32 = torch.ones(M, N, device=DEV)
-    _gemm(ffC, A, B, C32, M, N, K, a_k, b_k, beta=1.0, impl=3)
     assert _rel(C32, ref + 1.0) < 1e-3
 
 

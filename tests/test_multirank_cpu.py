@@ -35,8 +35,6 @@ def _free_port():
 def _build(case, ff):
     from flexflow_amd.core import ActiMode, DataType, LossType
     rng = np.random.default_rng(3)
-    if case in ("dlrm_small", "inception_small"):
-        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
     if case == "siblings":
         # two Linears reading the same tensor: the joint search merges them (merge_siblings_linear)
         x = ff.create_tensor([B, 32], DataType.DT_FLOAT, name="x")
@@ -56,6 +54,15 @@ def _build(case, ff):
         ff.softmax(t, name="sm")
         feeds = [rng.standard_normal((B, 16)).astype(np.float32)]
         lab = rng.integers(0, 16, (B, 1)).astype(np.int32)
+        return [x], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
+    if case == "a2a":
+        x = ff.create_tensor([B, 16], DataType.DT_FLOAT, name="x")
+        t = ff.dense(x, 32, name="d1")
+        t = ff.relu(t, name="r")
+        t = ff.dense(t, 12, name="d2")
+        ff.softmax(t, name="sm")
+        feeds = [rng.standard_normal((B, 16)).astype(np.float32)]
+        lab = rng.integers(0, 12, (B, 1)).astype(np.int32)
         return [x], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
     if case == "bert_tiny":
         from flexflow_amd.models.bert import BertConfig, build_bert
@@ -87,6 +94,16 @@ def _strategy(case, ff, world):
         # d3: sample 2 x out 2 x reduction 2; the loss on 4 ranks of sample parallelism
         return {"x": cfg("x", [2], [0, 4]), "d1": cfg("d1", [2, 4]), "d2": cfg("d2", [2, 1, 4]),
                 "d3": cfg("d3", [2, 2, 2]), "sm": cfg("sm", [4], [1, 3, 5, 7])}
+    if case == "a2a":
+        # sample-partitioned Linear -> ReLU partitioned along features on the same ranks -> sample
+        # again: both edges (and their gradients) are all-to-all exchanges
+        return {"x": cfg("x", [world]), "d1": cfg("d1", [world]), "r": cfg("r", [1, world]),
+                "d2": cfg("d2", [world]), "sm": cfg("sm", [world])}
+    if case == "tp" or (case == "mlp2d" and world == 2):
+        # column-parallel d2: its input gradient is a partial sum, reduce-scattered back to the
+        # sample-parallel producer d1; the executor starts it between d2's dgrad and wgrad GEMMs
+        return {"x": cfg("x", [world]), "d1": cfg("d1", [world]), "d2": cfg("d2", [1, world]),
+                "d3": cfg("d3", [world]), "sm": cfg("sm", [world])}
     if case == "mlp2d" and world == 4:
         return {"x": cfg("x", [4]), "d1": cfg("d1", [2, 2]), "d2": cfg("d2", [1, 2, 2]),
                 "d3": cfg("d3", [2, 2], [3, 2, 1, 0]), "sm": cfg("sm", [2], [2, 3])}
@@ -101,6 +118,8 @@ def _train(case, flags, world, out_file=None):
     inputs, feeds, lab, loss = _build(case, ff)
     ff.optimizer = SGDOptimizer(ff, 0.05)
     ff.compile(loss_type=loss, metrics=[MetricsType.METRICS_ACCURACY])
+    if os.environ.get("FF_TEST_COMM_TRACE") == "1":
+        ff.executor.comm_trace = []
     for t, v in zip(inputs, feeds):
         t.set_tensor(ff, v)
     ff.label_tensor.set_tensor(ff, lab)
@@ -122,6 +141,9 @@ def _worker(rank, world, port, case, flags, out_dir):
     import torch
     torch.set_num_threads(1)
     ff, res = _train(case, flags, world)
+    if rank == 0 and ff.executor.comm_trace is not None:
+        with open(os.path.join(out_dir, "comm_trace.json"), "w") as f:
+            json.dump([[e, k, list(edge), c] for e, k, edge, c in ff.executor.comm_trace], f)
     if rank == 0:
         np.savez(os.path.join(out_dir, "out.npz"), **res)
         rep = ff.search_report or {}
@@ -133,7 +155,7 @@ def _worker(rank, world, port, case, flags, out_dir):
     dist.destroy_process_group()
 
 
-def _run(case, world, flags=()):
+def _run(case, world, flags=(), strat_case=None):
     from flexflow_amd.core import FFConfig, FFModel
     from flexflow_amd.pcg.strategy import save_strategy
     tmp = tempfile.mkdtemp()
@@ -141,7 +163,7 @@ def _run(case, world, flags=()):
     ff = FFModel(FFConfig([]))
     ff.config.batch_size = B
     _build(case, ff)
-    s = _strategy(case, ff, world)
+    s = _strategy(strat_case or case, ff, world)
     if s is not None:
         sf = os.path.join(tmp, "s.json")
         save_strategy(sf, s, world)
@@ -185,6 +207,8 @@ def test_searched_strategy_matches_single(case, world, monkeypatch):
           {k: search["report"].get(k) for k in ("predicted_ms", "predicted_dp_ms", "graphs_costed")})
     if case in ("dlrm_small", "inception_small"):
         assert len(used) > 1, used  # the searched plan spreads these models over several ranks
+    if case in ("dlrm_small", "inception_small"):
+        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
     if case == "siblings":
         # the accepted rewrite changed the graph the strategy is chosen for
         assert any(r["xfer"] == "merge_siblings_linear" for r in search["rewrites"]), search["rewrites"]
@@ -196,3 +220,36 @@ def test_multi_axis_strategy_matches_single(world):
     par, _, _ = _run("mlp2d", world)
     ref = _single("mlp2d")
     _compare(par, ref, f"mlp2d@{world}")
+
+
+def test_all_to_all_strategy_matches_single():
+    from flexflow_amd.parallel.comm import Transfer
+    from flexflow_amd.parallel.layout import Layout
+    t = Transfer(Layout((8, 16), (4, 1), 1, (0, 1, 2, 3)), Layout((8, 16), (1, 4), 1, (2, 0, 3, 1)), False, 0)
+    assert t.kind == "all_to_all" and t.rank_sets() == [(0, 1, 2, 3)]
+    par, _, _ = _run("a2a", 4)
+    ref = _single("a2a")
+    _compare(par, ref, "a2a@4")
+
+
+def test_backward_collective_issued_before_wgrad_and_waited_at_consumer(monkeypatch):
+    """Trace of the asynchronous transfers: the reduce-scatter of the column-parallel layer's
+    input gradient is issued inside that layer's backward (between its dgrad and wgrad GEMMs) and
+    waited for only when the producing layer's backward needs it; forward gathers are prefetched
+    when their producer finishes."""
+    monkeypatch.setenv("FF_TEST_COMM_TRACE", "1")
+    _, _, tmp = _run("mlp2d", 2, strat_case="tp")
+    with open(os.path.join(tmp, "comm_trace.json")) as f:
+        tr = json.load(f)
+    issue = [e for e in tr if e[0] == "issue" and e[2][:2] == ["bwd", "d2"]]
+    wait = [e for e in tr if e[0] == "wait" and e[2][:2] == ["bwd", "d2"]]
+    assert issue and wait and issue[0][1] == "reduce_scatter"
+    assert wait[0][3] > issue[0][3]  # waited in a LATER op's backward (the producer's)
+    fwd = [e for e in tr if e[2][0] == "fwd" and e[2][1] == "d2"]
+    assert fwd[0][0] == "issue" and fwd[0][1] == "all_gather" and fwd[1][0] == "wait"
+
+
+def test_bf16_gradient_comm_matches_single():
+    par, _, _ = _run("mlp2d", 2, flags=["--only-data-parallel", "--grad-comm-dtype", "bf16"], strat_case="none")
+    ref = _single("mlp2d")
+    _compare(par, ref, "bf16-grad-comm", rtol=2e-2, atol=2e-3)

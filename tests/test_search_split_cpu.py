@@ -104,3 +104,20 @@ def test_candidate_quota_keeps_small_placements():
     # both halves of the machine appear among the 4-device views
     starts = {c.devices[0] for c in cands if c.num_parts == 4}
     assert {0, 4} <= starts
+
+
+def test_native_cost_model_classifies_all_to_all():
+    def lay(degs, devs):
+        lo = core.Layout()
+        lo.shape = [64, 1024]
+        lo.degrees = list(degs)
+        lo.replicas = 1
+        lo.devices = list(devs)
+        lo.partial = False
+        lo.halo = []
+        return lo
+    mm = core.MachineModel()
+    x = core.transfer_cost(lay([8, 1], range(8)), lay([1, 8], [3, 1, 0, 2, 7, 5, 6, 4]), False, 2, mm)
+    assert x.kind == core.XferKind.ALL_TO_ALL and x.ms > 0
+    g = core.transfer_cost(lay([8, 1], range(8)), lay([1, 4], range(4)), False, 2, mm)
+    assert g.kind == core.XferKind.GENERIC
