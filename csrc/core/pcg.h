@@ -116,7 +116,9 @@ XferCost transfer_cost(const Layout& src, const Layout& dst, bool src_partial, i
 struct Problem {
   std::vector<Node> nodes;  // topological order
   MachineModel machine;
-  double update_ms_per_mb = 0.0052;  // fused Adam over a flat arena: ~30 B/param at ~5.8 TB/s
+  // fused Adam over a flat arena, per MB of fp32 parameters: ~30 B of traffic per parameter at the
+  // 4.3 TB/s the kernel measures (BERT-Large: 2.58 ms for 366 M parameters, scripts/calibrate_sim.py)
+  double update_ms_per_mb = 0.00176;
   bool overlap_grad_sync = true;
 };
 

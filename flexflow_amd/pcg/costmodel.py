@@ -138,9 +138,56 @@ def mem_bytes(layer, cfg: OpConfig, compute_dtype: DataType, training: bool = Tr
     return float(act + wbytes)
 
 
+def _loss_fused_softmax(layer) -> bool:
+    """The model's output softmax under a cross-entropy loss: the executor runs it as ONE fused
+    softmax-cross-entropy pass over the logits inside the loss (ops/softmax.py emits the logits
+    unchanged), so its standalone softmax forward/backward never runs."""
+    from ..type import LossType
+    m = getattr(layer, "model", None)
+    if m is None or layer.op_type != OperatorType.OP_SOFTMAX:
+        return False
+    if getattr(m, "loss_type", None) not in (LossType.LOSS_CATEGORICAL_CROSSENTROPY,
+                                             LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY):
+        return False
+    out = m.output_tensor()
+    n = len(layer.outputs[0].dims)
+    return out is not None and out.guid == layer.outputs[0].guid and layer.attrs.get("dim", -1) % n == n - 1
+
+
+def fused_xent_cost(layer, cfg: OpConfig, compute_dtype: DataType, measure: bool, device=None):
+    """Cost of the fused softmax-cross-entropy pass on this config's shard (forward + backward in
+    one kernel: read the logits, write their gradient), charged to the forward."""
+    lo = op_layouts(layer, cfg)
+    shp = lo.inputs[0].local_shape(0)
+    V = shp[-1]
+    rows = int(math.prod(shp[:-1]))
+    if measure and device is not None and device.type == "cuda" and compute_dtype == DataType.DT_BF16:
+        key = ("xent", rows, V)
+        if key not in _measured:
+            from .. import kernels as K
+            x = torch.randn(rows, V, device=device, dtype=torch.bfloat16)
+            lab = torch.randint(0, V, (rows,), device=device, dtype=torch.int32)
+            acc = torch.zeros(3, device=device, dtype=torch.float32)
+            K.softmax_xent(x, lab, 1.0, acc)
+            torch.cuda.synchronize()
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            for _ in range(5):
+                K.softmax_xent(x, lab, 1.0, acc)
+            en.record()
+            en.synchronize()
+            _measured[key] = (st.elapsed_time(en) / 5, 0.0)
+        return _measured[key]
+    elem = 2 if compute_dtype == DataType.DT_BF16 else 4
+    t = 2.0 * rows * V * elem / HBM + LAUNCH_S
+    return t * 1e3, 0.0
+
+
 def op_cost(layer, cfg: OpConfig, compute_dtype: DataType, measure: bool, device=None):
     if layer.op_type == OperatorType.OP_INPUT:
         return 0.0, 0.0
+    if _loss_fused_softmax(layer):
+        return fused_xent_cost(layer, cfg, compute_dtype, measure, device)
     if measure and device is not None and device.type == "cuda":
         return measure_cost(layer, cfg, compute_dtype, device)
     return analytic_cost(layer, cfg, compute_dtype)
