@@ -109,9 +109,18 @@ int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t
   return ffk::gemm_pick_splitk(M, N, K, batch, (int)impl);
 }
 
+// two tensors whose elements sit at the same offsets of dense memory (both NCHW-contiguous or both
+// channel-last-contiguous): elementwise kernels index them flat
+bool same_dense(const Tensor& a, const Tensor& b) {
+  if (a.numel() != b.numel()) return false;
+  if (a.is_contiguous() && b.is_contiguous()) return true;
+  return a.dim() == 4 && b.dim() == 4 && a.sizes() == b.sizes() && a.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+         b.is_contiguous(at::MemoryFormat::ChannelsLast);
+}
+
 void unary_fwd(Tensor x, Tensor y, int64_t op, double s) {
   check_dev(x, "x");
-  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous());
+  TORCH_CHECK(x.numel() == y.numel() && same_dense(x, y), "unary_fwd: x / y must be dense in one memory order");
   ffk::unary_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), x.numel(), op, s, cur_stream());
 }
 void bias_act_fwd(Tensor z, optional<Tensor> bias, optional<Tensor> zout, Tensor y, int64_t rows, int64_t cols,
@@ -125,18 +134,27 @@ void bias_act_fwd(Tensor z, optional<Tensor> bias, optional<Tensor> zout, Tensor
 }
 void unary_bwd(Tensor x, Tensor y, Tensor dy, Tensor dx, int64_t op, double s, bool acc) {
   TORCH_CHECK(x.numel() == dx.numel() && dy.numel() == dx.numel() && y.numel() == dx.numel());
+  TORCH_CHECK(same_dense(x, dx) && same_dense(y, dx) && same_dense(dy, dx),
+              "unary_bwd: x / y / dy / dx must be dense in one memory order");
   ffk::unary_bwd(dtcode(x), x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), op, s, acc,
                  cur_stream());
 }
 void binary_fwd(Tensor a, Tensor b, Tensor c, int64_t op, std::vector<int64_t> shape, std::vector<int64_t> sa,
                 std::vector<int64_t> sb, bool same) {
   TORCH_CHECK(shape.size() <= 6 && sa.size() == shape.size() && sb.size() == shape.size());
+  TORCH_CHECK(!same || (same_dense(a, c) && same_dense(b, c)), "binary_fwd: flat operands must share a memory order");
+  TORCH_CHECK(same || c.is_contiguous(), "binary_fwd: broadcast output must be contiguous");
   ffk::binary_fwd(dtcode(c), a.data_ptr(), b.data_ptr(), c.data_ptr(), c.numel(), op, shape.size(), shape.data(),
                   sa.data(), sb.data(), same, cur_stream());
 }
 void binary_bwd(Tensor a, Tensor b, Tensor dc, optional<Tensor> da, optional<Tensor> db, int64_t op,
                 std::vector<int64_t> shape, std::vector<int64_t> sa, std::vector<int64_t> sb, bool same) {
   TORCH_CHECK(shape.size() <= 6);
+  TORCH_CHECK(!same || (same_dense(a, dc) && same_dense(b, dc) && (!da || same_dense(*da, dc)) &&
+                        (!db || same_dense(*db, dc))),
+              "binary_bwd: flat operands must share a memory order");
+  TORCH_CHECK(same || (dc.is_contiguous() && (!da || da->is_contiguous()) && (!db || db->is_contiguous())),
+              "binary_bwd: broadcast gradients must be contiguous");
   ffk::binary_bwd(dtcode(dc), a.data_ptr(), b.data_ptr(), dc.data_ptr(), ptr(da), ptr(db), dc.numel(), op,
                   shape.size(), shape.data(), sa.data(), sb.data(), same, cur_stream());
 }
@@ -362,10 +380,24 @@ void lstm_bwd_cell(Tensor G, int64_t ldg, Tensor c, Tensor c_prev, optional<Tens
                      ptr(dh_rec), dc.data_ptr<float>(), dG.data_ptr(), B, H, cur_stream());
 }
 
+// layout of a 4-D activation operand: NCHW-contiguous, or (nhwc) channel-last-contiguous bf16
+// with C % 8 == 0
+void check_layout(const Tensor& t, bool nhwc, int64_t C, const char* what) {
+  if (!nhwc) {
+    TORCH_CHECK(t.is_contiguous(), what, ": NCHW-contiguous tensor expected");
+    return;
+  }
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && C % 8 == 0, what, ": channel-last path needs bf16 and C % 8 == 0");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast), what,
+              ": channel-last-contiguous tensor expected");
+}
+
 void batchnorm_fwd(Tensor x, Tensor y, Tensor g, Tensor b, Tensor mean, Tensor rstd, Tensor run_mean,
                    Tensor run_var, Tensor ws, int64_t N, int64_t C, int64_t HW, double eps, double momentum,
-                   bool training, bool relu) {
+                   bool training, bool relu, bool nhwc) {
   check_dev(x, "x");
+  check_layout(x, nhwc, C, "batchnorm_fwd x");
+  check_layout(y, nhwc, C, "batchnorm_fwd y");
   TORCH_CHECK(x.numel() == N * C * HW && y.numel() == x.numel(), "batchnorm_fwd: x/y size");
   TORCH_CHECK(g.numel() >= C && b.numel() >= C && g.scalar_type() == x.scalar_type() &&
               b.scalar_type() == x.scalar_type(), "batchnorm_fwd: scale/bias");
@@ -374,18 +406,22 @@ void batchnorm_fwd(Tensor x, Tensor y, Tensor g, Tensor b, Tensor mean, Tensor r
   TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "batchnorm_fwd: workspace too small");
   ffk::batchnorm_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), g.data_ptr(), b.data_ptr(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), run_mean.data_ptr<float>(), run_var.data_ptr<float>(),
-                     ws.data_ptr<float>(), N, C, HW, eps, momentum, training, relu, cur_stream());
+                     ws.data_ptr<float>(), N, C, HW, eps, momentum, training, relu, nhwc, cur_stream());
 }
 void batchnorm_bwd(Tensor x, Tensor dy, Tensor g, Tensor b, Tensor mean, Tensor rstd, Tensor dx,
-                   optional<Tensor> dg, optional<Tensor> db, Tensor ws, int64_t N, int64_t C, int64_t HW, bool relu) {
+                   optional<Tensor> dg, optional<Tensor> db, Tensor ws, int64_t N, int64_t C, int64_t HW, bool relu,
+                   bool nhwc) {
   check_dev(x, "x");
+  check_layout(x, nhwc, C, "batchnorm_bwd x");
+  check_layout(dy, nhwc, C, "batchnorm_bwd dy");
+  check_layout(dx, nhwc, C, "batchnorm_bwd dx");
   TORCH_CHECK(x.numel() == N * C * HW && dy.numel() == x.numel() && dx.numel() == x.numel(), "batchnorm_bwd: size");
   TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "batchnorm_bwd: workspace too small");
   TORCH_CHECK(!dg.has_value() || (dg->scalar_type() == at::kFloat && dg->numel() >= C), "batchnorm_bwd: dg fp32");
   TORCH_CHECK(!db.has_value() || (db->scalar_type() == at::kFloat && db->numel() >= C), "batchnorm_bwd: db fp32");
   ffk::batchnorm_bwd(dtcode(x), x.data_ptr(), dy.data_ptr(), g.data_ptr(), b.data_ptr(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dx.data_ptr(), ptr<float>(dg), ptr<float>(db), ws.data_ptr<float>(), N,
-                     C, HW, relu, cur_stream());
+                     C, HW, relu, nhwc, cur_stream());
 }
 int64_t bn_ws(int64_t N, int64_t C, int64_t HW) { return ffk::bn_partial_floats(N, C, HW); }
 void rmsnorm_fwd(Tensor x, Tensor w, Tensor y, Tensor rstd, int64_t rows, int64_t d, double eps) {
@@ -406,16 +442,19 @@ void rmsnorm_bwd(Tensor x, Tensor w, Tensor dy, Tensor rstd, Tensor dx, optional
                    ptr<float>(dw), rows, d, cur_stream());
 }
 void channel_sum(Tensor dy, optional<Tensor> y, optional<Tensor> dz, optional<Tensor> db, Tensor ws, int64_t N,
-                 int64_t C, int64_t HW) {
+                 int64_t C, int64_t HW, bool nhwc) {
   check_dev(dy, "dy");
-  TORCH_CHECK(dy.is_contiguous() && dy.numel() == N * C * HW, "channel_sum: dy");
+  TORCH_CHECK(dy.numel() == N * C * HW, "channel_sum: dy");
+  check_layout(dy, nhwc, C, "channel_sum dy");
+  if (y.has_value()) check_layout(*y, nhwc, C, "channel_sum y");
+  if (dz.has_value()) check_layout(*dz, nhwc, C, "channel_sum dz");
   TORCH_CHECK(!y.has_value() || (y->numel() == dy.numel() && y->scalar_type() == dy.scalar_type()), "channel_sum: y");
   TORCH_CHECK(!dz.has_value() || (dz->numel() == dy.numel() && dz->scalar_type() == dy.scalar_type()),
               "channel_sum: dz");
   TORCH_CHECK(!db.has_value() || (db->scalar_type() == at::kFloat && db->numel() >= C), "channel_sum: db fp32");
   TORCH_CHECK(ws.numel() >= ffk::bn_partial_floats(N, C, HW), "channel_sum: workspace too small");
   ffk::channel_sum(dtcode(dy), dy.data_ptr(), ptr(y), ptr(dz), ptr<float>(db), ws.data_ptr<float>(), N, C, HW,
-                   cur_stream());
+                   nhwc, cur_stream());
 }
 std::vector<int> pool_geom(const std::vector<int64_t>& g) {
   TORCH_CHECK(g.size() == 14, "pool2d: geometry is N C H W OH OW kh kw sh sw pad_t pad_b pad_l pad_r");
@@ -427,24 +466,30 @@ std::vector<int> pool_geom(const std::vector<int64_t>& g) {
   return std::vector<int>(g.begin(), g.end());
 }
 void pool2d_fwd(Tensor x, Tensor y, optional<Tensor> idx, std::vector<int64_t> g, bool is_max, bool include_pad,
-                bool relu) {
+                bool relu, bool nhwc) {
   check_dev(x, "x");
   const auto gi = pool_geom(g);
+  check_layout(x, nhwc, g[1], "pool2d_fwd x");
+  check_layout(y, nhwc, g[1], "pool2d_fwd y");
   TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && y.numel() == g[0] * g[1] * g[4] * g[5], "pool2d_fwd: size");
   TORCH_CHECK(!idx.has_value() || idx->numel() >= y.numel(), "pool2d_fwd: idx");
   ffk::pool2d_fwd(dtcode(x), x.data_ptr(), y.data_ptr(), ptr<uint8_t>(idx), gi.data(), is_max, include_pad, relu,
-                  cur_stream());
+                  nhwc, cur_stream());
 }
 void pool2d_bwd(Tensor x, optional<Tensor> y, Tensor dy, optional<Tensor> idx, Tensor dx, std::vector<int64_t> g,
-                bool is_max, bool include_pad, bool relu) {
+                bool is_max, bool include_pad, bool relu, bool nhwc) {
   check_dev(x, "x");
   const auto gi = pool_geom(g);
+  check_layout(x, nhwc, g[1], "pool2d_bwd x");
+  check_layout(dy, nhwc, g[1], "pool2d_bwd dy");
+  check_layout(dx, nhwc, g[1], "pool2d_bwd dx");
+  if (y.has_value()) check_layout(*y, nhwc, g[1], "pool2d_bwd y");
   TORCH_CHECK(dx.numel() == x.numel() && x.numel() == g[0] * g[1] * g[2] * g[3] &&
               dy.numel() == g[0] * g[1] * g[4] * g[5], "pool2d_bwd: size");
   TORCH_CHECK(!is_max || (idx.has_value() && idx->numel() >= dy.numel()), "pool2d_bwd: max pooling needs idx");
   TORCH_CHECK(is_max || !relu || (y.has_value() && y->numel() == dy.numel()), "pool2d_bwd: avg + relu needs y");
   ffk::pool2d_bwd(dtcode(x), x.data_ptr(), ptr(y), dy.data_ptr(), ptr<uint8_t>(idx), dx.data_ptr(), gi.data(), is_max,
-                  include_pad, relu, cur_stream());
+                  include_pad, relu, nhwc, cur_stream());
 }
 
 std::vector<int> conv_geom(const std::vector<int64_t>& g) {
@@ -459,32 +504,38 @@ int64_t conv_ws(std::vector<int64_t> g) {
   const auto gi = conv_geom(g);
   return ffk::conv_ws_elems(gi[0], gi[1], gi[2], gi[3], gi[4], gi[5], gi[6], gi[7], gi[8], gi[13]);
 }
-void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, std::vector<int64_t> g, bool relu) {
+void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, std::vector<int64_t> g, bool relu,
+                bool x_nhwc, bool y_nhwc) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
               "conv2d: bf16 tensors");
-  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "conv2d: contiguous tensors");
+  TORCH_CHECK(w.is_contiguous(), "conv2d: contiguous weights");
+  check_layout(x, x_nhwc, g[1] / g[13], "conv2d_fwd x");
+  check_layout(y, y_nhwc, g[4] / g[13], "conv2d_fwd y");
   TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && y.numel() == g[0] * g[4] * g[5] * g[6] &&
               w.numel() == g[4] * (g[1] / g[13]) * g[7] * g[8], "conv2d_fwd: sizes");
   TORCH_CHECK(!bias.has_value() || (bias->scalar_type() == at::kBFloat16 && bias->numel() >= g[4]), "conv2d: bias");
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_fwd: workspace too small");
-  ffk::conv2d_fwd(x.data_ptr(), w.data_ptr(), ptr(bias), y.data_ptr(), ws.data_ptr(), gi.data(), relu, cur_stream());
+  ffk::conv2d_fwd(x.data_ptr(), w.data_ptr(), ptr(bias), y.data_ptr(), ws.data_ptr(), gi.data(), relu, x_nhwc, y_nhwc,
+                  cur_stream());
 }
 void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Tensor> dw, Tensor ws,
-                std::vector<int64_t> g) {
+                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv2d: bf16 tensors");
-  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && dy.is_contiguous(), "conv2d: contiguous tensors");
+  TORCH_CHECK(w.is_contiguous(), "conv2d: contiguous weights");
+  check_layout(x, x_nhwc, g[1] / g[13], "conv2d_bwd x");
+  check_layout(dy, dy_nhwc, g[4] / g[13], "conv2d_bwd dy");
+  if (dx.has_value()) check_layout(*dx, x_nhwc, g[1] / g[13], "conv2d_bwd dx (x's layout)");
   TORCH_CHECK(x.numel() == g[0] * g[1] * g[2] * g[3] && dy.numel() == g[0] * g[4] * g[5] * g[6], "conv2d_bwd: sizes");
-  TORCH_CHECK(!dx.has_value() || (dx->numel() == x.numel() && dx->scalar_type() == at::kBFloat16 &&
-                                  dx->is_contiguous()), "conv2d_bwd: dx");
+  TORCH_CHECK(!dx.has_value() || (dx->numel() == x.numel() && dx->scalar_type() == at::kBFloat16), "conv2d_bwd: dx");
   TORCH_CHECK(!dw.has_value() || (dw->numel() == w.numel() && dw->scalar_type() == at::kFloat && dw->is_contiguous()),
               "conv2d_bwd: dw must be fp32 like w");
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_bwd: workspace too small");
   ffk::conv2d_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), ptr(dx), ptr<float>(dw), ws.data_ptr(), gi.data(),
-                  dx.has_value(), cur_stream());
+                  dx.has_value(), x_nhwc, dy_nhwc, cur_stream());
 }
 
 }  // namespace

@@ -1,4 +1,4 @@
-// CNN support kernels (NCHW): batch normalization and 2-D pooling, forward and backward.
+// CNN support kernels (NCHW and NHWC): batch normalization and 2-D pooling, forward and backward.
 //
 // Reference: src/ops/batch_norm.cu (cuDNN spatial batch norm, fused ReLU) and src/ops/pool_2d.cu
 // (cuDNN max / average pooling). Here:
@@ -169,8 +169,9 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int C, in
   if (c >= C) return;
   float s1 = 0.f, s2 = 0.f;
   for (int s = 0; s < S; ++s) {
-    s1 += part[((int64_t)c * S + s) * 2];
-    s2 += part[((int64_t)c * S + s) * 2 + 1];
+    const float* p = part + ((int64_t)c * S + s) * 2;
+    s1 += p[0];
+    s2 += p[1];
   }
   sums[2 * c] = s1;
   sums[2 * c + 1] = s2;
@@ -262,12 +263,273 @@ __global__ void chan_sum_finalize_kernel(const float* __restrict__ part, int C, 
   db[c] += s1;
 }
 
+// ------------------------------------------------------------------------------- NHWC (bf16)
+// Channel-last activations ([M = N*H*W rows][C], C % 8 == 0): a per-channel statistic is a column
+// reduction. A workgroup owns up to 256 channels — L = min(32, C/8) lanes of 8 channels (one 16-B
+// load) per row — and R = 256 / L rows at a time, U rows in flight per thread; the R row partials
+// merge through LDS and each (split, channel) partial lands at part[s][c][NV], coalesced for the
+// finalize pass. Elementwise passes read 8 channels per thread.
+struct ColGeom {
+  int64_t M;
+  int C, C8, L, R, S;
+};
+enum { CR_STATS = 0, CR_BWD = 1, CR_SUM = 2 };
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
+  const uint4 raw = *reinterpret_cast<const uint4*>(p);
+  const bf16_t* e = reinterpret_cast<const bf16_t*>(&raw);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = bf2f(e[k]);
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
+  uint4 raw;
+  bf16_t* e = reinterpret_cast<bf16_t*>(&raw);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = f2bf(v[k]);
+  *reinterpret_cast<uint4*>(p) = raw;
+}
+
+// STATS: a = x -> Welford (n, mean, M2); BWD: a = x, b = dy -> (sum d, sum d * xhat) with the ReLU
+// mask recomputed; SUM: a = dy, b = y (optional ReLU mask) -> sum dz, dz written when requested
+template <int MODE>
+__global__ void __launch_bounds__(256) nhwc_colred_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                          bf16_t* __restrict__ dz, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, const bf16_t* __restrict__ g,
+                                                          const bf16_t* __restrict__ bb, float* __restrict__ part,
+                                                          ColGeom q, int relu) {
+  constexpr int NV = MODE == CR_STATS ? 3 : MODE == CR_BWD ? 2 : 1, U = 4;
+  __shared__ float sh[256 * 8 * NV];
+  const int t = threadIdx.x, l = t % q.L, r = t / q.L;
+  const int c8 = blockIdx.x * 32 + l, s = blockIdx.y;
+  const bool act = r < q.R && c8 < q.C8;
+  const int64_t j0 = q.M * s / q.S, j1 = q.M * (s + 1) / q.S;
+  float n = 0.f, v0[8], v1[8];
+  float mu[8], rs[8], gc[8], bc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { v0[k] = 0.f; v1[k] = 0.f; }
+  if (MODE == CR_BWD && act) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 * 8 + k;
+      mu[k] = mean[c]; rs[k] = rstd[c]; gc[k] = bf2f(g[c]); bc[k] = bf2f(bb[c]);
+    }
+  }
+  if (act) {
+    for (int64_t j = j0 + r; j < j1; j += (int64_t)U * q.R) {
+      float xa[U][8], xb[U][8];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = j + (int64_t)u * q.R;
+        ok[u] = row < j1;
+        const int64_t o = row * q.C + c8 * 8;
+        if (ok[u]) {
+          ld8(a + o, xa[u]);
+          if (MODE == CR_BWD || (MODE == CR_SUM && b)) ld8(b + o, xb[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (MODE == CR_STATS) {
+          n += 1.f;
+          const float inv = 1.f / n;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float d = xa[u][k] - v0[k];
+            v0[k] += d * inv;
+            v1[k] += d * (xa[u][k] - v0[k]);
+          }
+        } else if (MODE == CR_BWD) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float xh = (xa[u][k] - mu[k]) * rs[k];
+            float d = xb[u][k];
+            if (relu && xh * gc[k] + bc[k] <= 0.f) d = 0.f;
+            v0[k] += d;
+            v1[k] += d * xh;
+          }
+        } else {
+          float d[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            d[k] = (b && !(xb[u][k] > 0.f)) ? 0.f : xa[u][k];
+            v0[k] += d[k];
+          }
+          if (dz) st8(dz + (j + (int64_t)u * q.R) * q.C + c8 * 8, d);
+        }
+      }
+    }
+  }
+  float* my = sh + (size_t)t * 8 * NV;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (MODE == CR_STATS) {
+      my[k * 3] = n;
+      my[k * 3 + 1] = v0[k];
+      my[k * 3 + 2] = v1[k];
+    } else if (MODE == CR_BWD) {
+      my[k * 2] = v0[k];
+      my[k * 2 + 1] = v1[k];
+    } else {
+      my[k] = v0[k];
+    }
+  }
+  __syncthreads();
+  // thread t < 8 L folds channel t of this block over the R row partials
+  if (t < 8 * q.L) {
+    const int lc = t >> 3, k = t & 7;
+    const int c = (blockIdx.x * 32 + lc) * 8 + k;
+    if (c < q.C) {
+      float f[3] = {0.f, 0.f, 0.f};
+      for (int rr = 0; rr < q.R; ++rr) {
+        const float* p = sh + ((size_t)(rr * q.L + lc) * 8 + k) * NV;
+        if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], p[0], p[1], p[2]);
+        else {
+          f[0] += p[0];
+          if (NV == 2) f[1] += p[1];
+        }
+      }
+      float* o = part + ((int64_t)s * q.C + c) * NV;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) o[v] = f[v];
+    }
+  }
+}
+
+// finalize of the NHWC partials part[S][C][NV]: a workgroup owns 32 channels, its 8 thread groups
+// fold strided subsets of the S splits (independent loads, 4 in flight) and merge through LDS
+template <int MODE>
+__global__ void __launch_bounds__(256) nhwc_finalize_kernel(const float* __restrict__ part, int C, int S, float eps,
+                                                            float momentum, float* __restrict__ out0,
+                                                            float* __restrict__ out1, float* __restrict__ run_mean,
+                                                            float* __restrict__ run_var, float* __restrict__ dg,
+                                                            float* __restrict__ db) {
+  constexpr int NV = MODE == CR_STATS ? 3 : MODE == CR_BWD ? 2 : 1;
+  __shared__ float sh[8][32][NV];
+  const int cl = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float f[3] = {0.f, 0.f, 0.f};
+  if (c < C) {
+    int s = sg;
+    for (; s + 24 < S; s += 32) {
+      float v[4][NV];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[u][k] = part[((int64_t)(s + 8 * u) * C + c) * NV + k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], v[u][0], v[u][1], v[u][2]);
+        else
+#pragma unroll
+          for (int k = 0; k < NV; ++k) f[k] += v[u][k];
+      }
+    }
+    for (; s < S; s += 8) {
+      const float* p = part + ((int64_t)s * C + c) * NV;
+      if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], p[0], p[1], p[2]);
+      else
+#pragma unroll
+        for (int k = 0; k < NV; ++k) f[k] += p[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) sh[sg][cl][k] = f[k];
+  __syncthreads();
+  if (sg != 0 || c >= C) return;
+  for (int g = 1; g < 8; ++g) {
+    if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], sh[g][cl][0], sh[g][cl][1], sh[g][cl][2]);
+    else
+#pragma unroll
+      for (int k = 0; k < NV; ++k) f[k] += sh[g][cl][k];
+  }
+  if (MODE == CR_STATS) {
+    const float n = f[0], mean = f[1], m2 = f[2];
+    const float var = n > 0.f ? m2 / n : 0.f;
+    out0[c] = mean;
+    out1[c] = rsqrtf(var + eps);
+    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (n > 1.f ? m2 / (n - 1.f) : var);
+  } else if (MODE == CR_BWD) {
+    out0[2 * c] = f[0];
+    out0[2 * c + 1] = f[1];
+    if (dg) dg[c] += f[1];
+    if (db) db[c] += f[0];
+  } else {
+    if (db) db[c] += f[0];
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_apply_nhwc_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
+                                                            uint32_t n8, int C8, int relu) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % (uint32_t)C8) * 8;
+    float v[8];
+    ld8(x + (size_t)i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      v[k] = (v[k] - mean[c]) * rstd[c] * bf2f(g[c]) + bf2f(b[c]);
+      if (relu) v[k] = fmaxf(v[k], 0.f);
+    }
+    st8(y + (size_t)i * 8, v);
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_dx_nhwc_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const bf16_t* __restrict__ g,
+                                                             const bf16_t* __restrict__ b,
+                                                             const float* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                             uint32_t n8, int C8, float inv_m, int relu) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % (uint32_t)C8) * 8;
+    float xv[8], d[8];
+    ld8(x + (size_t)i * 8, xv);
+    ld8(dy + (size_t)i * 8, d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float rs = rstd[c], gc = bf2f(g[c]);
+      const float xh = (xv[k] - mean[c]) * rs;
+      if (relu && xh * gc + bf2f(b[c]) <= 0.f) d[k] = 0.f;
+      d[k] = gc * rs * (d[k] - sums[2 * c] * inv_m - xh * sums[2 * c + 1] * inv_m);
+    }
+    st8(dx + (size_t)i * 8, d);
+  }
+}
+
+// splits of the NHWC column reduction: ~1k workgroups over (channel blocks x splits), each split
+// at least one full trip of U x R rows
+static ColGeom nhwc_geom(int64_t M, int C) {
+  ColGeom q;
+  q.M = M;
+  q.C = C;
+  q.C8 = C / 8;
+  q.L = std::min(32, q.C8);
+  q.R = 256 / q.L;
+  const int ncb = (q.C8 + 31) / 32;
+  const int64_t trips = (M + 4LL * q.R - 1) / (4LL * q.R);
+  q.S = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(1024 + ncb - 1) / ncb, trips, 1024}));
+  return q;
+}
+
 static int bn_splits(int C, int64_t M) {
   int64_t s = (1024 + C - 1) / C;
   s = std::min<int64_t>(s, std::max<int64_t>(1, M / 2048));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 1024));
 }
-int bn_partial_floats(int N, int C, int HW) { return C * bn_splits(C, (int64_t)N * HW) * 3 + 2 * C; }
+int bn_partial_floats(int N, int C, int HW) {
+  const int64_t M = (int64_t)N * HW;
+  int s = bn_splits(C, M);
+  if (C % 8 == 0 && C > 0) s = std::max(s, nhwc_geom(M, C).S);
+  return C * s * 3 + 2 * C;
+}
 
 #define DT_DISPATCH(dt, ...)                                        \
   do {                                                              \
@@ -277,13 +539,30 @@ int bn_partial_floats(int N, int C, int HW) { return C * bn_splits(C, (int64_t)N
 
 void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b, float* mean, float* rstd,
                    float* run_mean, float* run_var, float* ws, int N, int C, int HW, float eps, float momentum,
-                   int training, int relu, hipStream_t st) {
+                   int training, int relu, int nhwc, hipStream_t st) {
   const int64_t total = (int64_t)N * C * HW;
   if (total == 0) return;
+  if (nhwc) {  // bf16, C % 8 == 0 (checked by the binding)
+    const ColGeom q = nhwc_geom((int64_t)N * HW, C);
+    if (training) {
+      hipLaunchKernelGGL(nhwc_colred_kernel<CR_STATS>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)x,
+                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
+      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_STATS>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, eps,
+                         momentum, mean, rstd, run_mean, run_var, nullptr, nullptr);
+    } else {
+      hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps, mean,
+                         rstd);
+    }
+    const uint32_t n8 = (uint32_t)(total / 8);
+    hipLaunchKernelGGL(bn_apply_nhwc_kernel, dim3(ew_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y,
+                       mean, rstd, (const bf16_t*)g, (const bf16_t*)b, n8, C / 8, relu);
+    return;
+  }
   if (training) {
     const int S = bn_splits(C, (int64_t)N * HW);
     DT_DISPATCH(dt, hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(C, S), dim3(256), 0, st, (const T*)x, ws, N, C, HW, S));
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, C, S, eps, momentum, mean, rstd,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, C, S, eps, momentum, mean,
+                       rstd,
                        run_mean, run_var);
   } else {
     hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps, mean,
@@ -299,9 +578,22 @@ void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b,
 
 void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const void* b, const float* mean,
                    const float* rstd, void* dx, float* dg, float* db, float* ws, int N, int C, int HW, int relu,
-                   hipStream_t st) {
+                   int nhwc, hipStream_t st) {
   const int64_t total = (int64_t)N * C * HW;
   if (total == 0) return;
+  if (nhwc) {
+    const ColGeom q = nhwc_geom((int64_t)N * HW, C);
+    float* sums = ws + (int64_t)C * q.S * 3;
+    hipLaunchKernelGGL(nhwc_colred_kernel<CR_BWD>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)dy, nullptr, mean, rstd, (const bf16_t*)g, (const bf16_t*)b, ws, q, relu);
+    hipLaunchKernelGGL(nhwc_finalize_kernel<CR_BWD>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f, sums,
+                       nullptr, nullptr, nullptr, dg, db);
+    const uint32_t n8 = (uint32_t)(total / 8);
+    hipLaunchKernelGGL(bn_bwd_dx_nhwc_kernel, dim3(ew_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)dy, mean, rstd, (const bf16_t*)g, (const bf16_t*)b, sums, (bf16_t*)dx, n8, C / 8,
+                       1.f / (float)((int64_t)N * HW), relu);
+    return;
+  }
   const int S = bn_splits(C, (int64_t)N * HW);
   float* sums = ws + (int64_t)C * S * 3;  // after the (3-float) partial area sized by bn_partial_floats
   DT_DISPATCH(dt, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(C, S), dim3(256), 0, st, (const T*)x, (const T*)dy,
@@ -319,8 +611,17 @@ void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const v
 }
 
 void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, float* ws, int N, int C, int HW,
-                 hipStream_t st) {
+                 int nhwc, hipStream_t st) {
   if ((int64_t)N * C * HW == 0) return;
+  if (nhwc) {
+    const ColGeom q = nhwc_geom((int64_t)N * HW, C);
+    hipLaunchKernelGGL(nhwc_colred_kernel<CR_SUM>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
+    if (db)
+      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_SUM>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f,
+                         nullptr, nullptr, nullptr, nullptr, nullptr, db);
+    return;
+  }
   const int S = bn_splits(C, (int64_t)N * HW);
   DT_DISPATCH(dt, hipLaunchKernelGGL(chan_sum_kernel<T>, dim3(C, S), dim3(256), 0, st, (const T*)dy, (const T*)y,
                                      (T*)dz, ws, N, C, HW, S));
@@ -468,24 +769,153 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const T* __restrict__ x, 
   }
 }
 
+
+// NHWC (bf16, C % 8 == 0): one thread per (pixel, 8-channel chunk), 16-B loads of each window tap;
+// consecutive lanes on consecutive chunks of one pixel, so every tap is a coalesced row read.
+// The winner bytes are stored in the output's NHWC order (8 per thread, one 8-B store).
+__global__ void __launch_bounds__(256) pool_fwd_nhwc_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ idx, PoolGeom p, int is_max,
+                                                            int include_pad, int relu) {
+  const int C8 = p.C / 8;
+  const unsigned total = (unsigned)p.N * p.OH * p.OW * C8;
+  for (unsigned o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const unsigned pix = o / (unsigned)C8;
+    const int c8 = (int)(o - pix * C8);
+    const int ow = (int)(pix % (unsigned)p.OW);
+    const unsigned t = pix / (unsigned)p.OW;
+    const int oh = (int)(t % (unsigned)p.OH), n = (int)(t / (unsigned)p.OH);
+    const int h0 = oh * p.sh - p.ph, w0 = ow * p.sw - p.pw;
+    const int i0 = max(0, -h0), i1 = min(p.kh, p.H - h0), j0 = max(0, -w0), j1 = min(p.kw, p.W - w0);
+    const bf16_t* xp = x + (size_t)n * p.H * p.W * p.C + c8 * 8;
+    float res[8];
+    if (is_max) {
+      int bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { res[k] = -INFINITY; bi[k] = 0; }
+      for (int i = i0; i < i1; ++i)
+        for (int j = j0; j < j1; ++j) {
+          float v[8];
+          ld8(xp + ((size_t)(h0 + i) * p.W + w0 + j) * p.C, v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (v[k] > res[k] || v[k] != v[k]) { res[k] = v[k]; bi[k] = i * p.kw + j; }
+        }
+      if (idx) {
+        uint2 packed;
+        packed.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+        packed.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+        *reinterpret_cast<uint2*>(idx + (size_t)o * 8) = packed;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) res[k] = 0.f;
+      for (int i = i0; i < i1; ++i)
+        for (int j = j0; j < j1; ++j) {
+          float v[8];
+          ld8(xp + ((size_t)(h0 + i) * p.W + w0 + j) * p.C, v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) res[k] += v[k];
+        }
+      const float inv = 1.f / pool_divisor(p, oh, ow, include_pad);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) res[k] *= inv;
+    }
+    if (relu)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) res[k] = fmaxf(res[k], 0.f);
+    st8(y + (size_t)o * 8, res);
+  }
+}
+
+// input-centric: every (input pixel, chunk) sums dy over the outputs whose window covers it (max:
+// whose recorded winner it is), reading 16 B of dy (+ 8 winner bytes) per covering output
+__global__ void __launch_bounds__(256) pool_bwd_nhwc_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                                                            const bf16_t* __restrict__ dy,
+                                                            const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+                                                            PoolGeom p, int is_max, int include_pad, int relu) {
+  const int C8 = p.C / 8;
+  const unsigned total = (unsigned)p.N * p.H * p.W * C8;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const unsigned pix = e / (unsigned)C8;
+    const int c8 = (int)(e - pix * C8);
+    const int iw = (int)(pix % (unsigned)p.W);
+    const unsigned t = pix / (unsigned)p.W;
+    const int ih = (int)(t % (unsigned)p.H), n = (int)(t / (unsigned)p.H);
+    const int oh0 = ih + p.ph - p.kh < 0 ? 0 : (ih + p.ph - p.kh) / p.sh + 1;
+    const int oh1 = min((ih + p.ph) / p.sh, p.OH - 1);
+    const int ow0 = iw + p.pw - p.kw < 0 ? 0 : (iw + p.pw - p.kw) / p.sw + 1;
+    const int ow1 = min((iw + p.pw) / p.sw, p.OW - 1);
+    float gsum[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gsum[k] = 0.f;
+    bool live[8];
+    if (is_max && relu) {
+      float xv[8];
+      ld8(x + (size_t)e * 8, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) live[k] = xv[k] > 0.f;  // a window it won has output relu(x) = 0
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) live[k] = true;
+    }
+    for (int oh = oh0; oh <= oh1; ++oh)
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const size_t o8 = (((size_t)n * p.OH + oh) * p.OW + ow) * C8 + c8;
+        float d[8];
+        ld8(dy + o8 * 8, d);
+        if (is_max) {
+          const uint2 packed = *reinterpret_cast<const uint2*>(idx + o8 * 8);
+          const int win = (ih - (oh * p.sh - p.ph)) * p.kw + (iw - (ow * p.sw - p.pw));
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t word = k < 4 ? packed.x : packed.y;
+            if ((int)((word >> (8 * (k & 3))) & 0xff) == win && live[k]) gsum[k] += d[k];
+          }
+        } else {
+          const float inv = 1.f / pool_divisor(p, oh, ow, include_pad);
+          float yv[8];
+          if (relu) ld8(y + o8 * 8, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (!relu || yv[k] > 0.f) gsum[k] += d[k] * inv;
+        }
+      }
+    st8(dx + (size_t)e * 8, gsum);
+  }
+}
+
 void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, int is_max, int include_pad, int relu,
-                hipStream_t st) {
+                int nhwc, hipStream_t st) {
   const PoolGeom p{geom[0], geom[1], geom[2], geom[3], geom[4],  geom[5],  geom[6],
                    geom[7], geom[8], geom[9], geom[10], geom[11], geom[12], geom[13]};
   const int64_t total = (int64_t)p.N * p.C * p.OH * p.OW;
   if (total == 0) return;
   if (total >= (1ll << 31) || (int64_t)p.N * p.C * p.H * p.W >= (1ll << 31))
     throw std::runtime_error("pool2d: tensors of 2^31 or more elements are not supported");
+  if (nhwc) {
+    const int64_t n8 = total / 8;
+    hipLaunchKernelGGL(pool_fwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 16384)), dim3(256), 0,
+                       st, (const bf16_t*)x, (bf16_t*)y, idx, p, is_max, include_pad, relu);
+    return;
+  }
   DT_DISPATCH(dt, hipLaunchKernelGGL(pool_fwd_kernel<T>, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)),
                                      dim3(256), 0, st, (const T*)x, (T*)y, idx, p, is_max, include_pad, relu));
 }
 
 void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint8_t* idx, void* dx, const int* geom,
-                int is_max, int include_pad, int relu, hipStream_t st) {
+                int is_max, int include_pad, int relu, int nhwc, hipStream_t st) {
   const PoolGeom p{geom[0], geom[1], geom[2], geom[3], geom[4],  geom[5],  geom[6],
                    geom[7], geom[8], geom[9], geom[10], geom[11], geom[12], geom[13]};
   const int64_t total = (int64_t)p.N * p.C * p.H * p.W;
   if (total == 0) return;
+  if (nhwc) {
+    if (total >= (1ll << 31)) throw std::runtime_error("pool2d: tensors of 2^31 or more elements are not supported");
+    const int64_t n8 = total / 8;
+    hipLaunchKernelGGL(pool_bwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 16384)), dim3(256), 0,
+                       st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, idx, (bf16_t*)dx, p, is_max,
+                       include_pad, relu);
+    return;
+  }
   const int nout = p.OH * p.OW, HW = p.H * p.W, nplanes = p.N * p.C;
   constexpr int LDS_BYTES = 64 * 1024;
   if (total < (1ll << 31) && nout * 5 <= LDS_BYTES) {

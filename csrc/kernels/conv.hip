@@ -1,17 +1,22 @@
-// 2-D convolution (NCHW tensors, bf16, fp32 accumulate) as implicit GEMMs on MFMA 32x32x16.
+// 2-D convolution (NCHW or channel-last tensors, bf16, fp32 accumulate) as implicit GEMMs on MFMA 32x32x16.
 //
 // Reference: src/ops/conv_2d.cu (cuDNN forward / backward-data / backward-filter with algorithm
 // search). MI355X design:
-//   * Activations are re-laid out once per call as channel-last, channel-padded copies
-//     ([N][H][W][G][Cp], Cp = channels per group rounded up to 8) so that every MFMA operand
-//     fragment — 8 consecutive reduction elements — is ONE 16-B load of 8 channels at one pixel;
-//     the weights are packed the same way ([G][rows][KH][KW][Cp], zero tail to the K tile).
+//   * Activations are channel-last ([N][H][W][G][Cp]) so that every MFMA operand fragment — 8
+//     consecutive reduction elements — is ONE 16-B load of 8 channels at one pixel. The framework
+//     keeps CNN activations channel-last end to end (kernels.CHANNELS_LAST), so such an operand
+//     with Cg % 8 == 0 is read in place; NCHW operands (and channel counts that are not a multiple
+//     of 8, e.g. an RGB input) are re-laid out per call into channel-padded copies (Cp = Cg
+//     rounded up to 8). The weights are packed the same way ([G][rows][KH][KW][Cp], zero tail to
+//     the K tile).
 //   * forward and backward-data are the same kernel (conv_igemm_kernel): rows = output channels
 //     (forward) / input channels (backward-data), columns = output pixels of the call, reduction
 //     = (kh, kw, 8-channel chunk). The gather of a chunk is a bounds test on the shifted pixel
 //     (forward: ih = oh*s - p + kh; backward-data: oh = (ih + p - kh) / s when divisible). Tiles
 //     128 x 128 x 32 through double-buffered, XOR-swizzled LDS images (conflict-free b128 reads),
-//     4 waves x (2 x 2) MFMA tiles, bias + ReLU fused into the NCHW store.
+//     4 waves x (2 x 2) MFMA tiles, bias + ReLU fused into the store: NCHW straight from the
+//     accumulators, channel-last through an LDS [pixel][channel] image so that each pixel's
+//     channels leave as whole 16-B chunks.
 //   * backward-filter (conv_wgrad_kernel): rows = output channels, columns = input channels of
 //     one (kh, kw), reduction = output pixels, split over workgroups. Both operands arrive as
 //     [pixel][channel] images (the channel-last copies) and are read transposed with
@@ -103,20 +108,23 @@ __global__ void __launch_bounds__(256) conv_pack_kernel(const bf16_t* __restrict
 struct IGemmArgs {
   const bf16_t* A;   // packed weights [G][M][Kp]
   const bf16_t* B;   // channel-last source [N][Hs][Ws][G][Cs]
-  bf16_t* out;       // NCHW [N][G*M][Ho][Wo]
+  bf16_t* out;       // NCHW [N][G*M][Ho][Wo], or (out_nhwc) channel-last [N][Ho][Wo][G][M]
   const bf16_t* bias;
   int N, G, M, Kp;   // rows per group, padded reduction length (multiple of 32)
   int Hs, Ws, Cs;    // source geometry (Cs = padded channels per group)
   int Ho, Wo;        // output geometry (columns = N * Ho * Wo)
   int KH, KW, sh, sw, ph, pw;
   int relu;
+  int out_nhwc;      // channel-last output (M % 8 == 0)
 };
 
 template <bool BWD, int BN>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
   constexpr int BM = 128, BK = 32, NB = BN / 64;  // NB: pixel rows per thread / MFMA columns per wave
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TA + TB)];
+  constexpr int RS = BM * 2 + 16;  // channel-last epilogue: [pixel][BM channels] rows, 16-B pad
+  constexpr int SMEM = 2 * (TA + TB) > BN * RS ? 2 * (TA + TB) : BN * RS;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int g = blockIdx.z;
@@ -221,6 +229,46 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     __syncthreads();
   }
   // epilogue: acc[i][j] row = channel (r&3) + 8(r>>2) + 4h, column = pixel lane & 31
+  if (a.out_nhwc) {
+    // stage the tile as [pixel][channel] in LDS (the K loop's buffers are free after its last
+    // barrier), then store whole 16-B channel chunks: a pixel's BM channels are one contiguous run
+    // of the channel-last output, consecutive lanes on consecutive chunks
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int px = (BN / 2) * wn + 32 * j + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ml = 64 * wm + 32 * i + 8 * q + 4 * h;
+          uint16_t e[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int m = m0 + ml + k;
+            float v = acc[i][j][4 * q + k];
+            if (a.bias && m < a.M) v += bf2f(a.bias[g * a.M + m]);
+            if (a.relu) v = fmaxf(v, 0.f);
+            e[k] = f2bf(v);
+          }
+          uint2 pk;
+          pk.x = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
+          pk.y = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+          *reinterpret_cast<uint2*>(smem + px * RS + ml * 2) = pk;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t ldo = (int64_t)a.G * a.M;
+    for (int k = tid; k < BN * (BM / 8); k += 256) {
+      const int px = k / (BM / 8), c = k % (BM / 8);
+      const int64_t p = p0 + px;
+      const int m = m0 + c * 8;
+      if (p < P && m < a.M)
+        *reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m) =
+            *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
+    }
+    return;
+  }
   const int64_t HoWo = (int64_t)a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -407,39 +455,54 @@ int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH,
 }
 
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
-                hipStream_t st) {
+                int x_nhwc, int y_nhwc, hipStream_t st) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg);
   bf16_t* xt = (bf16_t*)ws;
   bf16_t* wp = xt + (int64_t)N * H * W * G * Cp + (int64_t)N * OH * OW * G * round8(Kg);
   const int Kp = kpad(KH, KW, Cp);
-  launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
+  // a channel-last input (Cg % 8 == 0, so Cp == Cg) is the implicit GEMM's B operand as it is
+  const bf16_t* src = (const bf16_t*)x;
+  if (!x_nhwc) {
+    launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
+    src = xt;
+  }
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Kg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                      wp, G, Kg, Cg, KH, KW, Kp, 0);
-  IGemmArgs a{wp, xt, (bf16_t*)y, (const bf16_t*)bias, N, G, Kg, Kp, H, W, Cp, OH, OW, KH, KW, sh, sw, ph, pw, relu};
+  IGemmArgs a{wp, src, (bf16_t*)y, (const bf16_t*)bias, N, G, Kg, Kp, H, W, Cp, OH, OW, KH, KW, sh, sw, ph, pw, relu,
+              y_nhwc};
   launch_igemm<false>(a, (int64_t)N * OH * OW, Kg, G, st);
 }
 
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, hipStream_t st) {
+                int need_dx, int x_nhwc, int dy_nhwc, hipStream_t st) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
   bf16_t* xt = (bf16_t*)ws;
   bf16_t* yt = xt + (int64_t)N * H * W * G * Cp;
   bf16_t* wp = yt + (int64_t)N * OH * OW * G * Kgp;
-  launch_nhwc((const bf16_t*)dy, yt, N, G, Kg, OH * OW, Kgp, st);
+  const bf16_t* ysrc = (const bf16_t*)dy;
+  if (!dy_nhwc) {
+    launch_nhwc((const bf16_t*)dy, yt, N, G, Kg, OH * OW, Kgp, st);
+    ysrc = yt;
+  }
   if (need_dx) {
     const int Kp = kpad(KH, KW, Kgp);
     hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                        wp, G, Kg, Cg, KH, KW, Kp, 1);
-    IGemmArgs a{wp, yt, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0};
+    IGemmArgs a{wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc};
     launch_igemm<true>(a, (int64_t)N * H * W, Cg, G, st);
   }
   if (dw) {
-    // the forward's channel-last input copy is rebuilt here (the workspace is per call)
-    launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
+    // the forward's channel-last input copy is rebuilt here (the workspace is per call) unless
+    // the input is channel-last already
+    const bf16_t* xsrc = (const bf16_t*)x;
+    if (!x_nhwc) {
+      launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
+      xsrc = xt;
+    }
     // 64-channel tiles (the 128-channel variant measured no faster); split the pixels so that
     // about 1k workgroups run, each over at least 16 steps of 64 pixels (2k workgroups of 8+
     // steps measured slower: more atomics, more prologues; scripts/conv_probe.py)
@@ -447,7 +510,7 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
     const int tiles = ((Kg + TC - 1) / TC) * ((Cg + TC - 1) / TC) * KH * KW * G;
     const int64_t nsteps = ((int64_t)N * OH * OW + 63) / 64;
     const int splits = (int)std::max<int64_t>(1, std::min<int64_t>((nsteps + 15) / 16, (1024 + tiles - 1) / tiles));
-    WGradArgs b{yt, xt, dw, N, G, Kg, Kgp, Cg, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, splits};
+    WGradArgs b{ysrc, xsrc, dw, N, G, Kg, Kgp, Cg, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, splits};
     const dim3 grid((Kg + TC - 1) / TC, ((Cg + TC - 1) / TC) * KH * KW, G * splits);
     if (TC == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(256), 0, st, b);

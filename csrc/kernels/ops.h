@@ -113,29 +113,32 @@ void rmsnorm_fwd(int dt, const void* x, const void* w, void* y, float* rstd, int
                  hipStream_t st);
 void rmsnorm_bwd(int dt, const void* x, const void* w, const void* dy, const float* rstd, void* dx, float* dw,
                  int rows, int d, hipStream_t st);
-// cnn.hip: NCHW batch norm (split Welford statistics, fused ReLU) and 2-D pooling
+// cnn.hip: batch norm (split Welford statistics, fused ReLU) and 2-D pooling of NCHW tensors, or
+// (nhwc = 1: bf16, C % 8 == 0) of channel-last tensors
 int bn_partial_floats(int N, int C, int HW);  // ws floats for batchnorm_fwd / batchnorm_bwd
 void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b, float* mean, float* rstd,
                    float* run_mean, float* run_var, float* ws, int N, int C, int HW, float eps, float momentum,
-                   int training, int relu, hipStream_t st);
+                   int training, int relu, int nhwc, hipStream_t st);
 void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const void* b, const float* mean,
                    const float* rstd, void* dx, float* dg, float* db, float* ws, int N, int C, int HW, int relu,
-                   hipStream_t st);
+                   int nhwc, hipStream_t st);
 // db (fp32) += per-channel sum of dy; with y, dy is ReLU-masked by y > 0 (written to dz if given)
 void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, float* ws, int N, int C, int HW,
-                 hipStream_t st);
+                 int nhwc, hipStream_t st);
 // geom: N C H W OH OW kh kw sh sw pad_top pad_bottom pad_left pad_right
 void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, int is_max, int include_pad, int relu,
-                hipStream_t st);
+                int nhwc, hipStream_t st);
 void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint8_t* idx, void* dx, const int* geom,
-                int is_max, int include_pad, int relu, hipStream_t st);
+                int is_max, int include_pad, int relu, int nhwc, hipStream_t st);
 
-// conv.hip: NCHW bf16 convolution as implicit GEMMs on MFMA (channel-last padded staging copies in
-// ws). geom: N C H W K OH OW KH KW sh sw ph pw G
+// conv.hip: bf16 convolution as implicit GEMMs on MFMA. x / y / dy / dx are NCHW or (*_nhwc = 1)
+// channel-last; a channel-last operand with channels per group % 8 == 0 is read in place, others are
+// staged through channel-last padded copies in ws; dx takes x's layout. geom: N C H W K OH OW KH KW
+// sh sw ph pw G
 int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH, int KW, int G);  // bf16 elems
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
-                hipStream_t st);
+                int x_nhwc, int y_nhwc, hipStream_t st);
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, hipStream_t st);
+                int need_dx, int x_nhwc, int dy_nhwc, hipStream_t st);
 
 }  // namespace ffk

@@ -744,10 +744,62 @@ def unary_ref(name, x, s):
     return r.to(x.dtype)
 
 
+# ------------------------------------------------------------------ activation layout
+# CNN activations live channel-last on the device in bf16 (NCHW logical shape, NHWC memory:
+# torch.channels_last): the convolutions' implicit GEMMs read them in place and write their outputs
+# channel-last, batch norm / pooling / channel sums have channel-last kernels (csrc/kernels/cnn.hip)
+# and the elementwise ops preserve the layout, so no per-op NCHW <-> NHWC copies remain.
+# FF_CHANNELS_LAST=0 keeps NCHW everywhere. CPU / fp32 tensors are always NCHW.
+CHANNELS_LAST = _os.environ.get("FF_CHANNELS_LAST", "1") != "0"
+
+
+def is_nhwc(t):
+    return t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def cl_ok(t, c):
+    """May t (per-group channel count c) be processed channel-last?"""
+    return CHANNELS_LAST and t.dim() == 4 and t.dtype == torch.bfloat16 and c % 8 == 0 and native(t)
+
+
+def cl_dense(t, nhwc):
+    """t dense in the requested layout (no copy when it already is)."""
+    if nhwc:
+        return t if is_nhwc(t) else t.contiguous(memory_format=torch.channels_last)
+    return t.contiguous()
+
+
+def act_dense(t):
+    """A 4-D activation dense in the layout its kernels take (channel-last when cl_ok)."""
+    if t.dim() != 4:
+        return t.contiguous()
+    return cl_dense(t, cl_ok(t, t.shape[1]))
+
+
+def _dense(t):
+    """t itself when its memory is dense in NCHW or channel-last order, else a dense copy keeping
+    a channel-last view (e.g. a channel slice of a channel-last tensor) channel-last."""
+    if t.is_contiguous() or is_nhwc(t):
+        return t
+    if t.dim() == 4 and t.stride(1) == 1:
+        return t.contiguous(memory_format=torch.channels_last)
+    return t.contiguous()
+
+
+dense = _dense
+
+
+def _like(t, ref):
+    """t dense in ref's memory order (ref dense, same shape): elementwise kernels index both flat."""
+    if ref.is_contiguous():
+        return t.contiguous()
+    return cl_dense(t, True)
+
+
 def unary_fwd(name, x, s=0.0, out=None):
     """y = f(x); out=x computes in place (elementwise, same index: safe)."""
     if native(x) and x.dtype in (torch.bfloat16, torch.float32):
-        xc = x.contiguous()
+        xc = _dense(x)
         y = out if out is not None else torch.empty_like(xc)
         ext().unary_fwd(xc, y, U[name], float(s))
         return y
@@ -760,8 +812,10 @@ def unary_fwd(name, x, s=0.0, out=None):
 
 def unary_bwd(name, x, y, dy, s=0.0):
     if native(x) and x.dtype in (torch.bfloat16, torch.float32):
-        dx = torch.empty_like(dy)
-        ext().unary_bwd(x.contiguous(), y.contiguous(), dy.contiguous(), dx, U[name], float(s), False)
+        xc = _dense(x)
+        dyc = _like(dy, xc)
+        dx = torch.empty_like(dyc)
+        ext().unary_bwd(xc, _like(y, xc), dyc, dx, U[name], float(s), False)
         return dx
     xr = x.detach().float().requires_grad_()
     out = unary_ref(name, xr, s).float() if name != "identity" else xr * 1.0
@@ -788,8 +842,13 @@ def binary_fwd(name, a, b):
     if native(a) and a.dtype in (torch.bfloat16, torch.float32) and len(out_shape) <= 6:
         if b.dtype != a.dtype:
             b = b.to(a.dtype)
-        c = torch.empty(out_shape, device=a.device, dtype=a.dtype)
-        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape) and a.is_contiguous() and b.is_contiguous()
+        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape)
+        if same:  # flat over the common memory order (NCHW or channel-last)
+            a = _dense(a)
+            b = _like(b, a)
+            c = torch.empty_like(a)
+        else:
+            c = torch.empty(out_shape, device=a.device, dtype=a.dtype)
         shp, sa, sb = _bcast_desc(a, b, out_shape)
         ext().binary_fwd(a, b, c, B[name], shp, sa, sb, same)
         return c
@@ -813,11 +872,18 @@ def binary_bwd(name, a, b, dc, need_a=True, need_b=True):
     out_shape = dc.shape
     if native(dc) and dc.dtype in (torch.bfloat16, torch.float32) and len(out_shape) <= 6:
         bb = b.to(a.dtype) if b.dtype != a.dtype else b
-        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape) and a.is_contiguous() and b.is_contiguous()
+        same = tuple(a.shape) == tuple(b.shape) == tuple(out_shape)
+        if same:  # flat over dc's memory order
+            dc = _dense(dc)
+            a, bb = _like(a, dc), _like(bb, dc)
+            da = torch.empty_like(dc) if need_a else None
+            db = torch.empty_like(dc) if need_b else None
+        else:
+            dc = dc.contiguous()
+            da = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_a else None
+            db = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_b else None
         shp, sa, sb = _bcast_desc(a, bb, out_shape)
-        da = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_a else None
-        db = torch.empty(out_shape, device=dc.device, dtype=dc.dtype) if need_b else None
-        ext().binary_bwd(a, bb, dc.contiguous(), da, db, B[name], shp, sa, sb, same)
+        ext().binary_bwd(a, bb, dc, da, db, B[name], shp, sa, sb, same)
         return (_reduce_to(da, a.shape) if need_a else None), (_reduce_to(db, b.shape) if need_b else None)
     ar = a.detach().float().requires_grad_()
     br = b.detach().float().requires_grad_()
@@ -1028,7 +1094,7 @@ def metrics_classify(probs2d, labels, acc3):
     acc3[2] += p.shape[0]
 
 
-# ------------------------------------------------------------------ batch norm / pooling (NCHW)
+# ------------------------------------------------------------------ batch norm / pooling (NCHW / channel-last)
 @torch.no_grad()
 def batchnorm_fwd(x, g, b, run_mean, run_var, training, relu, eps=1e-5, momentum=0.1):
     """Spatial batch norm (+ReLU) of an NCHW tensor (csrc/kernels/cnn.hip). Training normalizes with
@@ -1037,11 +1103,14 @@ def batchnorm_fwd(x, g, b, run_mean, run_var, training, relu, eps=1e-5, momentum
     N, C = x.shape[0], x.shape[1]
     HW = x.numel() // max(1, N * C)
     if native(x):
+        nhwc = cl_ok(x, C)
+        x = cl_dense(x, nhwc)
         y = torch.empty_like(x)
         mean = torch.empty(C, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         ws = torch.empty(ext().bn_ws(N, C, HW), device=x.device, dtype=torch.float32)
-        ext().batchnorm_fwd(x, y, g, b, mean, rstd, run_mean, run_var, ws, N, C, HW, eps, momentum, training, relu)
+        ext().batchnorm_fwd(x, y, g, b, mean, rstd, run_mean, run_var, ws, N, C, HW, eps, momentum, training, relu,
+                            nhwc)
         return y, mean, rstd
     xf = x.float().reshape(N, C, HW)
     if training:
@@ -1065,9 +1134,11 @@ def batchnorm_bwd(x, dy, g, b, mean, rstd, dg, db, relu):
     N, C = x.shape[0], x.shape[1]
     HW = x.numel() // max(1, N * C)
     if native(x):
+        nhwc = cl_ok(x, C)
+        x = cl_dense(x, nhwc)
         dx = torch.empty_like(x)
         ws = torch.empty(ext().bn_ws(N, C, HW), device=x.device, dtype=torch.float32)
-        ext().batchnorm_bwd(x, dy.contiguous(), g, b, mean, rstd, dx, dg, db, ws, N, C, HW, relu)
+        ext().batchnorm_bwd(x, cl_dense(dy, nhwc), g, b, mean, rstd, dx, dg, db, ws, N, C, HW, relu, nhwc)
         return dx
     xf = x.float().reshape(N, C, HW)
     xh = (xf - mean[None, :, None]) * rstd[None, :, None]
@@ -1114,10 +1185,12 @@ def pool2d_fwd(x, kh, kw, sh, sw, pads, is_max, include_pad, relu, need_idx):
     OH = pool_out_size(H, kh, sh, pads[0], pads[1])
     OW = pool_out_size(W, kw, sw, pads[2], pads[3])
     if native(x):
-        y = torch.empty((N, C, OH, OW), device=x.device, dtype=x.dtype)
+        nhwc = cl_ok(x, C)
+        x = cl_dense(x, nhwc)
+        y = torch.empty((N, C, OH, OW), device=x.device, dtype=x.dtype,
+                        memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         idx = torch.empty(y.numel(), device=x.device, dtype=torch.uint8) if (is_max and need_idx) else None
-        ext().pool2d_fwd(x.contiguous(), y, idx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads], is_max, include_pad,
-                         relu)
+        ext().pool2d_fwd(x, y, idx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads], is_max, include_pad, relu, nhwc)
         return y, idx
     return _pool_ref(x.float(), kh, kw, sh, sw, pads, is_max, include_pad, relu).to(x.dtype), None
 
@@ -1126,10 +1199,12 @@ def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
     """dx of pool2d_fwd (gather over the covering outputs; max pooling routes dy to the winners)."""
     N, C, H, W = x.shape
     if native(x):
+        nhwc = cl_ok(x, C)  # the forward's decision: idx is in its output's memory order
+        x = cl_dense(x, nhwc)
         dx = torch.empty_like(x)
         OH, OW = dy.shape[-2:]
-        ext().pool2d_bwd(x.contiguous(), y, dy.contiguous(), idx, dx, [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads],
-                         is_max, include_pad, relu)
+        ext().pool2d_bwd(x, cl_dense(y, nhwc) if y is not None else None, cl_dense(dy, nhwc), idx, dx,
+                         [N, C, H, W, OH, OW, kh, kw, sh, sw, *pads], is_max, include_pad, relu, nhwc)
         return dx
     xr = x.detach().float().requires_grad_()
     with torch.enable_grad():
@@ -1138,7 +1213,7 @@ def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
     return dx.to(x.dtype)
 
 
-# ------------------------------------------------------------------ convolution (NCHW)
+# ------------------------------------------------------------------ convolution (NCHW / channel-last)
 # Our implicit-GEMM MFMA kernels (csrc/kernels/conv.hip) and MIOpen (through torch) are both
 # timed once per call site (geometry) outside graph capture and the faster one is kept, as for
 # GEMMs; FF_CONV_IMPL=ours|lib forces one. The choices land in TUNE_LOG.
@@ -1167,16 +1242,21 @@ def _conv_lib_bwd(x, w, dy, g, need_dx, need_dw):
     return dx, dw
 
 
-def _conv_ours_fwd(x, w, b, g, relu):
-    y = torch.empty((g[0], g[4], g[5], g[6]), device=x.device, dtype=x.dtype)
+def _conv_ours_fwd(x, w, b, g, relu, y_nhwc):
+    y = torch.empty((g[0], g[4], g[5], g[6]), device=x.device, dtype=x.dtype,
+                    memory_format=torch.channels_last if y_nhwc else torch.contiguous_format)
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
-    ext().conv2d_fwd(x, w, b, y, ws, g, relu)
+    ext().conv2d_fwd(x, w, b, y, ws, g, relu, _nhwc_flag(x, g[1] // g[13]), y_nhwc)
     return y
+
+
+def _nhwc_flag(t, c):
+    return cl_ok(t, c) and is_nhwc(t)
 
 
 def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out):
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
-    ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g)
+    ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g, _nhwc_flag(x, g[1] // g[13]), _nhwc_flag(dy, g[4] // g[13]))
 
 
 def _conv_pick(kind, key, cands):
@@ -1195,16 +1275,26 @@ def _conv_pick(kind, key, cands):
 
 
 def conv2d_fwd(x, w, b, stride, pad, groups, relu):
-    """y = [relu](conv2d(x, w) + b), NCHW. bf16 on the device: our implicit-GEMM kernel or MIOpen,
-    whichever the per-geometry timing picked; otherwise torch (fp32 / CPU reference)."""
+    """y = [relu](conv2d(x, w) + b) (NCHW logical shapes). bf16 on the device: our implicit-GEMM
+    kernel or MIOpen, whichever the per-geometry timing picked, with a channel-last output when
+    CHANNELS_LAST (and the output channels per group are a multiple of 8); otherwise torch (fp32 /
+    CPU reference)."""
     g = conv_geometry(x, w, stride, pad, groups)
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
-        x, w = x.contiguous(), w.contiguous()
+        x = cl_dense(x, cl_ok(x, g[1] // groups))
+        w = w.contiguous()
         b = b.contiguous() if b is not None else None
-        choice = _conv_pick("fwd", tuple(g), {"ours": lambda: _conv_ours_fwd(x, w, b, g, relu),
-                                              "lib": lambda: _conv_lib_fwd(x, w, b, g, relu)})
+        y_nhwc = cl_ok(x, g[4] // groups)
+
+        def lib():
+            y = _conv_lib_fwd(x, w, b, g, relu)
+            return cl_dense(y, y_nhwc)
+
+        choice = _conv_pick("fwd", tuple(g) + (is_nhwc(x),),
+                            {"ours": lambda: _conv_ours_fwd(x, w, b, g, relu, y_nhwc), "lib": lib})
         if choice == "ours":
-            return _conv_ours_fwd(x, w, b, g, relu)
+            return _conv_ours_fwd(x, w, b, g, relu, y_nhwc)
+        return lib()
     return _conv_lib_fwd(x, w, b, g, relu)
 
 
@@ -1212,7 +1302,9 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx):
     """Backward of conv2d_fwd for geometry g (conv_geometry): returns dx (or None) and adds the
     weight gradient into dw (fp32, shaped like w, may be None)."""
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16:
-        x, w, dy = x.contiguous(), w.contiguous(), dy.contiguous()
+        x = cl_dense(x, cl_ok(x, g[1] // g[13]))
+        dy = cl_dense(dy, cl_ok(dy, g[4] // g[13]))
+        w = w.contiguous()
 
         def ours():
             dxo = torch.empty_like(x) if need_dx else None
@@ -1220,7 +1312,7 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx):
             _conv_ours_bwd(x, w, dy, g, dxo, dwo)
             return dxo, dwo
 
-        choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None),
+        choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None, is_nhwc(x)),
                             {"ours": ours, "lib": lambda: _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)})
         if choice == "ours":
             dxo = torch.empty_like(x) if need_dx else None
@@ -1247,10 +1339,11 @@ def conv_bias_relu_bwd(dy, y, db):
     if y is None and db is None:
         return dy
     if native(dy):
-        dy = dy.contiguous()
+        nhwc = cl_ok(dy, C)
+        dy = cl_dense(dy, nhwc)
         dz = torch.empty_like(dy) if y is not None else None
         ws = torch.empty(ext().bn_ws(N, C, HW), device=dy.device, dtype=torch.float32)
-        ext().channel_sum(dy, y, dz, db, ws, N, C, HW)
+        ext().channel_sum(dy, cl_dense(y, nhwc) if y is not None else None, dz, db, ws, N, C, HW, nhwc)
         return dz if dz is not None else dy
     dz = dy * (y > 0) if y is not None else dy
     if db is not None:

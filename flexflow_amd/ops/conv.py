@@ -1,4 +1,5 @@
-"""Conv2D and Pool2D (NCHW), reference src/ops/conv_2d.cc, src/ops/pool_2d.cc (cuDNN).
+"""Conv2D and Pool2D (NCHW logical shapes; channel-last memory on the device, kernels.CHANNELS_LAST),
+reference src/ops/conv_2d.cc, src/ops/pool_2d.cc (cuDNN).
 
 Parallel axes: N (sample), C_out (parameter; conv only), H and W (attribute parallelism: each part
 computes an output row/col block and reads its input block plus a halo of the receptive field,
@@ -147,9 +148,11 @@ class Conv2D(_Spatial):
             b = None
         kh, kw, sh, sw, ph, pw = self._kp()
         xc, pad = self._local_input(ctx, x)
+        groups = self.attrs.get("groups", 1)
+        xc = K.cl_dense(xc, K.cl_ok(xc, xc.shape[1] // groups))  # the layout the kernels take (saved as such)
         act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
         relu = act == ActiMode.AC_MODE_RELU
-        z = K.conv2d_fwd(xc, w, b, (sh, sw), pad, self.attrs.get("groups", 1), relu)
+        z = K.conv2d_fwd(xc, w, b, (sh, sw), pad, groups, relu)
         y = z if act in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU) else K.act_ref(z, act.value)
         if ctx.training:
             ctx.saved.update(xc=xc, w=w, z=z, y=y, pad=pad, x_shape=x.shape, has_b=b is not None)
@@ -234,9 +237,10 @@ class Pool2D(_Spatial):
         if not fused:
             return self._forward_torch(ctx, x)
         xc, pads, crop = self._local_block(ctx, x)
-        y, idx = K.pool2d_fwd(xc.contiguous(), kh, kw, sh, sw, pads, is_max, include_pad, relu, ctx.training)
+        xc = K.act_dense(xc)
+        y, idx = K.pool2d_fwd(xc, kh, kw, sh, sw, pads, is_max, include_pad, relu, ctx.training)
         if ctx.training:
-            ctx.saved.update(xc=xc.contiguous(), y=y, idx=idx, pads=pads, crop=crop, x_shape=x.shape)
+            ctx.saved.update(xc=xc, y=y, idx=idx, pads=pads, crop=crop, x_shape=x.shape)
         return [y]
 
     def backward(self, ctx, douts):

@@ -116,7 +116,7 @@ class BatchNorm(OpImpl):
         """Batch statistics in training (running statistics updated, momentum 0.1), running
         statistics in inference; fused ReLU per the reference's batch_norm(relu=True) default.
         HIP kernels: csrc/kernels/cnn.hip (split Welford statistics + normalize pass)."""
-        x = xs[0].contiguous()
+        x = K.act_dense(xs[0])  # channel-last on the device (kernels.CHANNELS_LAST)
         c = x.shape[1]
         rm = ctx.extra.setdefault("running_mean", torch.zeros(c, device=x.device))
         rv = ctx.extra.setdefault("running_var", torch.ones(c, device=x.device))

@@ -217,7 +217,7 @@ class Split(OpImpl):
         return [tuple(range(n)) for _ in self.layer.outputs]
 
     def forward(self, ctx, xs, ws):
-        return [t.contiguous() for t in torch.split(xs[0], self.attrs["sizes"], self.attrs["axis"])]
+        return [K.dense(t) for t in torch.split(xs[0], self.attrs["sizes"], self.attrs["axis"])]
 
     def backward(self, ctx, douts):
         like = [d for d in douts if d is not None][0]

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Our implicit-GEMM convolution vs MIOpen (torch) on CNN-zoo layer shapes, bf16, forward and
-backward (data + filter). Usage: python scripts/conv_probe.py"""
+backward (data + filter), in the layout the framework runs (channel-last unless
+FF_CHANNELS_LAST=0). Usage: python scripts/conv_probe.py"""
 import os
 import sys
 
@@ -18,6 +19,11 @@ SHAPES = [  # name, N, C, H, W, K, (kh, kw), (sh, sw), (ph, pw), groups
     ("resnet.c4_3x3", 64, 256, 14, 14, 256, (3, 3), (1, 1), (1, 1), 1),
     ("resnet.c5_1x1", 64, 2048, 7, 7, 512, (1, 1), (1, 1), (0, 0), 1),
     ("inception.1x7", 32, 128, 17, 17, 128, (1, 7), (1, 1), (0, 3), 1),
+    ("inception.A1x1", 64, 192, 35, 35, 64, (1, 1), (1, 1), (0, 0), 1),
+    ("inception.A5x5", 64, 48, 35, 35, 64, (5, 5), (1, 1), (2, 2), 1),
+    ("inception.A3x3", 64, 64, 35, 35, 96, (3, 3), (1, 1), (1, 1), 1),
+    ("inception.stem3", 64, 32, 147, 147, 64, (3, 3), (1, 1), (1, 1), 1),
+    ("inception.E1x1", 64, 1280, 8, 8, 320, (1, 1), (1, 1), (0, 0), 1),
     ("resnext.g32", 32, 256, 28, 28, 256, (3, 3), (1, 1), (1, 1), 32),
 ]
 
@@ -36,13 +42,16 @@ def timed(fn, reps=10):
 
 for name, N, C, H, W, Ko, k, st, pad, G in SHAPES:
     x = torch.randn(N, C, H, W, device="cuda").bfloat16()
+    x = K.cl_dense(x, K.cl_ok(x, C // G))
     w = (torch.randn(Ko, C // G, *k, device="cuda") * 0.05).bfloat16()
     b = torch.zeros(Ko, device="cuda").bfloat16()
     g = K.conv_geometry(x, w, st, pad, G)
     fl = 2.0 * N * Ko * g[5] * g[6] * (C // G) * k[0] * k[1]
-    f_o = timed(lambda: K._conv_ours_fwd(x, w, b, g, True))
+    y_cl = K.cl_ok(x, Ko // G)
+    f_o = timed(lambda: K._conv_ours_fwd(x, w, b, g, True, y_cl))
     f_l = timed(lambda: K._conv_lib_fwd(x, w, b, g, True))
     dy = torch.randn(N, Ko, g[5], g[6], device="cuda").bfloat16()
+    dy = K.cl_dense(dy, y_cl)
     dx = torch.empty_like(x)
     dw = torch.zeros(w.shape, device="cuda")
     b_o = timed(lambda: K._conv_ours_bwd(x, w, dy, g, dx, dw))

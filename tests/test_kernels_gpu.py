@@ -501,13 +501,16 @@ def test_hipblaslt_splitk_and_tuned_choice(ffC):
     assert _rel(C, ref) < 2e-3
 
 
+@pytest.mark.parametrize("cl", [True, False])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape,relu", [((8, 64, 14, 14), True), ((3, 5, 7, 9), False), ((3, 3, 1, 1), True),
-                                        ((64, 16, 32, 32), False)])
-def test_batchnorm(shape, relu, dtype):
+                                        ((64, 16, 32, 32), False), ((4, 200, 9, 9), True), ((2, 512, 7, 7), False)])
+def test_batchnorm(shape, relu, dtype, cl, monkeypatch):
     """HIP batch norm (split Welford statistics, fused ReLU) against torch's fp32 batch_norm:
-    output, running statistics, and dx / dgamma / dbeta."""
+    output, running statistics, and dx / dgamma / dbeta. cl: bf16 tensors with C % 8 == 0 take the
+    channel-last kernels (column reductions over [N*H*W][C])."""
     from flexflow_amd import kernels as K
+    monkeypatch.setattr(K, "CHANNELS_LAST", cl)
     torch.manual_seed(21)
     N, C = shape[:2]
     x = (torch.randn(shape, device=DEV) * 2 + 3).to(dtype)  # offset mean: Welford, not sum-of-squares
@@ -515,6 +518,7 @@ def test_batchnorm(shape, relu, dtype):
     b = torch.randn(C, device=DEV).to(dtype)
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     y, mean, rstd = K.batchnorm_fwd(x, g, b, rm, rv, True, relu)
+    assert K.is_nhwc(y) == (K.cl_ok(x, C) or K.is_nhwc(x))
     xr, gr, br = (t.float().requires_grad_() for t in (x, g, b))
     rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     ref = torch.nn.functional.batch_norm(xr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5)
@@ -555,15 +559,18 @@ def test_pool2d(k, s, p, is_max, inc, relu, dtype):
     assert _rel(dx, xr.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
 
 
+@pytest.mark.parametrize("cl", [True, False])
 @pytest.mark.parametrize("shape,k,s,p,is_max", [((8, 32, 35, 35), 3, 1, 1, False),   # Inception A/C/E pools
                                                  ((4, 16, 147, 147), 3, 2, 0, True),  # Inception stem
                                                  ((2, 3, 64, 48), 3, 3, 1, True),
                                                  ((1, 2, 260, 260), 2, 1, 0, False),  # plane past LDS: fallback
                                                  ((1, 2, 260, 260), 2, 1, 0, True)])
-def test_pool2d_planes(shape, k, s, p, is_max):
+def test_pool2d_planes(shape, k, s, p, is_max, cl, monkeypatch):
     """Large-plane pooling: the LDS plane-staged backward (several planes per workgroup) and the
-    memory-gather fallback for planes too large for LDS, against torch fp32."""
+    memory-gather fallback for planes too large for LDS (NCHW), or the channel-last kernels (cl,
+    C % 8 == 0), against torch fp32."""
     from flexflow_amd import kernels as K
+    monkeypatch.setattr(K, "CHANNELS_LAST", cl)
     torch.manual_seed(24)
     x = torch.randn(*shape, device=DEV).bfloat16()
     y, idx = K.pool2d_fwd(x, k, k, s, s, (p, p, p, p), is_max, True, False, True)
@@ -592,6 +599,7 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     assert _rel(K.pool2d_bwd(x, y, dy, idx, 3, 3, 2, 2, pads, is_max, inc, False), xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
 @pytest.mark.parametrize("geo", [
     # N, C, H, W, K, (kh, kw), (sh, sw), (ph, pw), groups
     (2, 3, 32, 32, 16, (3, 3), (1, 1), (1, 1), 1),
@@ -604,17 +612,23 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     (2, 192, 35, 35, 64, (1, 1), (1, 1), (0, 0), 1),   # Inception A 1x1: 3 channel tiles, odd HW
     (2, 64, 16, 16, 64, (3, 3), (1, 1), (1, 1), 32),   # ResNeXt grouped 3x3: Cp = 8 per group
 ])
-def test_conv2d_implicit_gemm(geo):
+def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     """Our implicit-GEMM MFMA convolution (forward with bias + ReLU, backward data, backward filter
-    through float atomics) against fp32 torch autograd on the same bf16 inputs."""
+    through float atomics) against fp32 torch autograd on the same bf16 inputs; nhwc: channel-last
+    activations read in place (channels per group % 8 == 0, else staged) and channel-last outputs
+    through the LDS epilogue (output channels per group % 8 == 0)."""
     from flexflow_amd import kernels as K
+    monkeypatch.setattr(K, "CHANNELS_LAST", layout == "nhwc")
     torch.manual_seed(31)
     N, C, H, W, Ko, (kh, kw), st, pad, G = geo
     x = torch.randn(N, C, H, W, device=DEV).bfloat16()
+    x = K.cl_dense(x, K.cl_ok(x, C // G))
     w = (torch.randn(Ko, C // G, kh, kw, device=DEV) / math.sqrt(C // G * kh * kw)).bfloat16()
     b = torch.randn(Ko, device=DEV).bfloat16()
     g = K.conv_geometry(x, w, st, pad, G)
-    y = K._conv_ours_fwd(x, w, b, g, True)
+    y_nhwc = K.cl_ok(x, Ko // G)
+    y = K._conv_ours_fwd(x, w, b, g, True, y_nhwc)
+    assert K.is_nhwc(y) == y_nhwc or y.is_contiguous()
     xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
     ref = torch.relu(torch.nn.functional.conv2d(xr, wr, br, st, pad, 1, G))
     assert y.shape == ref.shape
@@ -622,6 +636,7 @@ def test_conv2d_implicit_gemm(geo):
     dy = torch.randn_like(ref).bfloat16()
     ref.backward(dy.float())
     dz = K.conv_bias_relu_bwd(dy, y, None)
+    dz = K.cl_dense(dz, K.cl_ok(dz, Ko // G))
     dx = torch.empty_like(x)
     dw = torch.zeros(w.shape, device=DEV)
     K._conv_ours_bwd(x, w, dz, g, dx, dw)
@@ -653,11 +668,15 @@ def test_rmsnorm(rows, d, dtype):
     assert _rel(dw, wr.grad) < 1e-3
 
 
-@pytest.mark.parametrize("shape", [(3, 5, 7, 9), (64, 32, 35, 35), (2, 3, 1, 1), (16, 48, 17, 17), (1, 7, 64, 64)])
-def test_chan_sum_relu_mask(shape):
+@pytest.mark.parametrize("cl", [True, False])
+@pytest.mark.parametrize("shape", [(3, 5, 7, 9), (64, 32, 35, 35), (2, 3, 1, 1), (16, 48, 17, 17), (1, 7, 64, 64),
+                                   (8, 768, 17, 17)])
+def test_chan_sum_relu_mask(shape, cl, monkeypatch):
     """Per-channel bias gradient with the ReLU mask (chan_sum_kernel: 4 loads in flight per lane,
-    incremental (image, pixel) indexing across odd planes and the tail) against torch."""
+    incremental (image, pixel) indexing across odd planes and the tail; cl: the channel-last
+    column reduction) against torch."""
     from flexflow_amd import kernels as K
+    monkeypatch.setattr(K, "CHANNELS_LAST", cl)
     torch.manual_seed(43)
     dy = torch.randn(*shape, device=DEV).bfloat16()
     y = torch.randn(*shape, device=DEV).bfloat16()
@@ -666,3 +685,51 @@ def test_chan_sum_relu_mask(shape):
     ref = dy.float() * (y.float() > 0)
     assert torch.equal(dz.float(), ref.bfloat16().float())
     assert _rel(db, 0.5 + ref.sum((0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("k,s,p,is_max,inc,relu", [(3, 2, 1, True, True, False), (2, 2, 0, True, True, True),
+                                                   (3, 1, 1, False, True, False), (3, 2, 1, False, False, True),
+                                                   (5, 3, 2, False, False, False), (8, 8, 0, False, True, False)])
+def test_pool2d_channel_last(k, s, p, is_max, inc, relu):
+    """Channel-last pooling (one thread per pixel x 8 channels, winner bytes in NHWC order) forward
+    and backward against torch fp32, on channel-last bf16 inputs."""
+    from flexflow_amd import kernels as K
+    if not K.CHANNELS_LAST:
+        pytest.skip("FF_CHANNELS_LAST=0")
+    torch.manual_seed(25)
+    x = torch.randn(4, 48, 17, 15, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    y, idx = K.pool2d_fwd(x, k, k, s, s, (p, p, p, p), is_max, inc, relu, True)
+    assert K.is_nhwc(y)
+    # reference in NCHW: torch's channel-last avg_pool2d backward disagreed with both its own NCHW
+    # result and our two kernels on this image (seen on MI355X, torch 2.10 ROCm)
+    xr = x.float().contiguous().requires_grad_()
+    ref = K._pool_ref(xr, k, k, s, s, (p, p, p, p), is_max, inc, relu)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()  # NCHW: the wrapper re-lays it out
+    ref.backward(dy.float())
+    dx = K.pool2d_bwd(x, y, dy, idx, k, k, s, s, (p, p, p, p), is_max, inc, relu)
+    assert K.is_nhwc(dx)
+    # (avg + ReLU: the mask of outputs within rounding of 0 can differ from the fp32 reference's)
+    assert _rel(dx, xr.grad) < 2e-2
+
+
+def test_elementwise_channel_last():
+    """Unary / binary elementwise kernels index channel-last operands flat and keep the layout;
+    mixed layouts are re-laid out to the first operand's."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(26)
+    a = torch.randn(4, 24, 9, 7, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    b = torch.randn(4, 24, 9, 7, device=DEV).bfloat16()
+    y = K.unary_fwd("relu", a)
+    assert K.is_nhwc(y) and torch.equal(y.float(), torch.relu(a.float()))
+    dx = K.unary_bwd("relu", a, y, b)
+    assert torch.equal(dx.float(), (b.float() * (a.float() > 0)))
+    c = K.binary_fwd("add", a, b)
+    assert K.is_nhwc(c) and _rel(c, a.float() + b.float()) < 1e-2
+    ar, br = a.float().requires_grad_(), b.float().requires_grad_()
+    (ar * br).backward(b.float())
+    da, db = K.binary_bwd("mul", a, b, b.contiguous(memory_format=torch.channels_last))
+    assert _rel(da, ar.grad) < 1e-2 and _rel(db, br.grad) < 1e-2
+    # a channel slice of a channel-last tensor (a concat's backward split) stays channel-last
+    part = K.dense(a[:, 8:16])
+    assert K.is_nhwc(part) and torch.equal(part, a[:, 8:16])
