@@ -290,7 +290,9 @@ __device__ __forceinline__ void st8(bf16_t* p, const float* v) {
 }
 
 // STATS: a = x -> Welford (n, mean, M2); BWD: a = x, b = dy -> (sum d, sum d * xhat) with the ReLU
-// mask recomputed; SUM: a = dy, b = y (optional ReLU mask) -> sum dz, dz written when requested
+// mask recomputed; SUM: a = dy, b = y (optional ReLU mask) -> sum dz, dz written when requested,
+// the per-workgroup channel sums added straight into the fp32 bias gradient (part) by atomics: no
+// finalize launch (its latency-bound fold over ~1k splits cost as much as the reduction)
 template <int MODE>
 __global__ void __launch_bounds__(256) nhwc_colred_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
                                                           bf16_t* __restrict__ dz, const float* __restrict__ mean,
@@ -390,60 +392,53 @@ __global__ void __launch_bounds__(256) nhwc_colred_kernel(const bf16_t* __restri
           if (NV == 2) f[1] += p[1];
         }
       }
-      float* o = part + ((int64_t)s * q.C + c) * NV;
+      if (MODE == CR_SUM) {
+        if (part) atomicAdd(part + c, f[0]);  // SUM: part is the fp32 bias gradient itself
+      } else {
+        float* o = part + ((int64_t)s * q.C + c) * NV;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) o[v] = f[v];
+        for (int v = 0; v < NV; ++v) o[v] = f[v];
+      }
     }
   }
 }
 
-// finalize of the NHWC partials part[S][C][NV]: a workgroup owns 32 channels, its 8 thread groups
-// fold strided subsets of the S splits (independent loads, 4 in flight) and merge through LDS
+// finalize of the NHWC partials part[S][C][NV] (STATS, BWD): a workgroup owns 8 channels, its 32
+// thread groups fold strided subsets of the S splits (independent loads, 4 in flight: the partials
+// sit in other XCDs' L2 or in HBM, so the fold is latency-bound) and merge through LDS
 template <int MODE>
 __global__ void __launch_bounds__(256) nhwc_finalize_kernel(const float* __restrict__ part, int C, int S, float eps,
                                                             float momentum, float* __restrict__ out0,
                                                             float* __restrict__ out1, float* __restrict__ run_mean,
                                                             float* __restrict__ run_var, float* __restrict__ dg,
                                                             float* __restrict__ db) {
-  constexpr int NV = MODE == CR_STATS ? 3 : MODE == CR_BWD ? 2 : 1;
-  __shared__ float sh[8][32][NV];
-  const int cl = threadIdx.x & 31, sg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
+  constexpr int NV = MODE == CR_STATS ? 3 : 2, CPB = 8, NG = 256 / CPB;
+  __shared__ float sh[NG][CPB][NV];
+  const int cl = threadIdx.x % CPB, sg = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + cl;
   float f[3] = {0.f, 0.f, 0.f};
+  auto merge = [&](const float* v) {
+    if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], v[0], v[1], v[2]);
+    else { f[0] += v[0]; f[1] += v[1]; }
+  };
   if (c < C) {
     int s = sg;
-    for (; s + 24 < S; s += 32) {
+    for (; s + 3 * NG < S; s += 4 * NG) {
       float v[4][NV];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int k = 0; k < NV; ++k) v[u][k] = part[((int64_t)(s + 8 * u) * C + c) * NV + k];
+        for (int k = 0; k < NV; ++k) v[u][k] = part[((int64_t)(s + NG * u) * C + c) * NV + k];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], v[u][0], v[u][1], v[u][2]);
-        else
-#pragma unroll
-          for (int k = 0; k < NV; ++k) f[k] += v[u][k];
-      }
+      for (int u = 0; u < 4; ++u) merge(v[u]);
     }
-    for (; s < S; s += 8) {
-      const float* p = part + ((int64_t)s * C + c) * NV;
-      if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], p[0], p[1], p[2]);
-      else
-#pragma unroll
-        for (int k = 0; k < NV; ++k) f[k] += p[k];
-    }
+    for (; s < S; s += NG) merge(part + ((int64_t)s * C + c) * NV);
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) sh[sg][cl][k] = f[k];
   __syncthreads();
   if (sg != 0 || c >= C) return;
-  for (int g = 1; g < 8; ++g) {
-    if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], sh[g][cl][0], sh[g][cl][1], sh[g][cl][2]);
-    else
-#pragma unroll
-      for (int k = 0; k < NV; ++k) f[k] += sh[g][cl][k];
-  }
+  for (int gi = 1; gi < NG; ++gi) merge(sh[gi][cl]);
   if (MODE == CR_STATS) {
     const float n = f[0], mean = f[1], m2 = f[2];
     const float var = n > 0.f ? m2 / n : 0.f;
@@ -451,12 +446,10 @@ __global__ void __launch_bounds__(256) nhwc_finalize_kernel(const float* __restr
     out1[c] = rsqrtf(var + eps);
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (n > 1.f ? m2 / (n - 1.f) : var);
-  } else if (MODE == CR_BWD) {
+  } else {
     out0[2 * c] = f[0];
     out0[2 * c + 1] = f[1];
     if (dg) dg[c] += f[1];
-    if (db) db[c] += f[0];
-  } else {
     if (db) db[c] += f[0];
   }
 }
@@ -547,7 +540,7 @@ void batchnorm_fwd(int dt, const void* x, void* y, const void* g, const void* b,
     if (training) {
       hipLaunchKernelGGL(nhwc_colred_kernel<CR_STATS>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)x,
                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
-      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_STATS>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, eps,
+      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_STATS>, dim3((C + 7) / 8), dim3(256), 0, st, ws, C, q.S, eps,
                          momentum, mean, rstd, run_mean, run_var, nullptr, nullptr);
     } else {
       hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps, mean,
@@ -586,7 +579,7 @@ void batchnorm_bwd(int dt, const void* x, const void* dy, const void* g, const v
     float* sums = ws + (int64_t)C * q.S * 3;
     hipLaunchKernelGGL(nhwc_colred_kernel<CR_BWD>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)x,
                        (const bf16_t*)dy, nullptr, mean, rstd, (const bf16_t*)g, (const bf16_t*)b, ws, q, relu);
-    hipLaunchKernelGGL(nhwc_finalize_kernel<CR_BWD>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f, sums,
+    hipLaunchKernelGGL(nhwc_finalize_kernel<CR_BWD>, dim3((C + 7) / 8), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f, sums,
                        nullptr, nullptr, nullptr, dg, db);
     const uint32_t n8 = (uint32_t)(total / 8);
     hipLaunchKernelGGL(bn_bwd_dx_nhwc_kernel, dim3(ew_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)x,
@@ -616,10 +609,7 @@ void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, flo
   if (nhwc) {
     const ColGeom q = nhwc_geom((int64_t)N * HW, C);
     hipLaunchKernelGGL(nhwc_colred_kernel<CR_SUM>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
-    if (db)
-      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_SUM>, dim3((C + 31) / 32), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f,
-                         nullptr, nullptr, nullptr, nullptr, nullptr, db);
+                       (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, db, q, 0);
     return;
   }
   const int S = bn_splits(C, (int64_t)N * HW);

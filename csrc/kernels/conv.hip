@@ -17,11 +17,11 @@
 //     4 waves x (2 x 2) MFMA tiles, bias + ReLU fused into the store: NCHW straight from the
 //     accumulators, channel-last through an LDS [pixel][channel] image so that each pixel's
 //     channels leave as whole 16-B chunks.
-//   * backward-filter (conv_wgrad_kernel): rows = output channels, columns = input channels of
-//     one (kh, kw), reduction = output pixels, split over workgroups. Both operands arrive as
-//     [pixel][channel] images (the channel-last copies) and are read transposed with
-//     ds_read_b64_tr_b16 — the attention dV^T = dO^T . P operand path — and each workgroup adds its
-//     fp32 32x32 tiles into the fp32 weight gradient with float atomics.
+//   * backward-filter (conv_wgrad_kernel): rows = output channels, columns = the flattened
+//     (kh, kw, input channel) axis, reduction = output pixels, split over workgroups. Both
+//     operands arrive as [pixel][channel] images and are read transposed with ds_read_b64_tr_b16 —
+//     the attention dV^T = dO^T . P operand path; the splits' fp32 tiles go to slabs that one
+//     reduce pass adds into the weight gradient (no atomics).
 #include "common.h"
 #include "ops.h"
 
@@ -118,9 +118,10 @@ struct IGemmArgs {
   int out_nhwc;      // channel-last output (M % 8 == 0)
 };
 
-template <bool BWD, int BN>
+template <bool BWD, int BM, int BN>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
-  constexpr int BM = 128, BK = 32, NB = BN / 64;  // NB: pixel rows per thread / MFMA columns per wave
+  // MI / NB: MFMA row / column tiles per wave (BM / 2 rows x BN / 2 pixels per wave)
+  constexpr int BK = 32, MI = BM / 64, NB = BN / 64;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;
   constexpr int RS = BM * 2 + 16;  // channel-last epilogue: [pixel][BM channels] rows, 16-B pad
   constexpr int SMEM = 2 * (TA + TB) > BN * RS ? 2 * (TA + TB) : BN * RS;
@@ -135,13 +136,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
   const bf16_t* Ag = a.A + (int64_t)g * a.M * a.Kp;
   // this thread's staging slots: rows r and r + 64 of both tiles, 16-B chunk c
   const int sr = tid >> 2, sc = tid & 3;
-  const bf16_t* arow[2];
-  bool aok[2];
+  const bf16_t* arow[MI];
+  bool aok[MI];
   int64_t pbase[NB];
   int prow[NB], pcol[NB];
   bool pok[NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MI; ++i) {
     const int m = m0 + sr + 64 * i;
     aok[i] = m < a.M;
     arow[i] = Ag + (int64_t)(aok[i] ? m : 0) * a.Kp + sc * 8;
@@ -159,10 +160,10 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
   }
   // reduction chunk of this thread at K-step 0: chunk index sc -> (kh, kw, c8)
   int c8 = sc % C8, kw = (sc / C8) % a.KW, kh = sc / C8 / a.KW;
-  uint4 ra[2], rb[NB];
+  uint4 ra[MI], rb[NB];
   auto load = [&](int ks) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
       ra[i] = aok[i] ? *reinterpret_cast<const uint4*>(arow[i] + ks * BK) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -193,13 +194,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     char* la = smem + buf * (TA + TB);
     char* lb = la + TA;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(la + off32(sr + 64 * i, sc)) = ra[i];
+    for (int i = 0; i < MI; ++i) *reinterpret_cast<uint4*>(la + off32(sr + 64 * i, sc)) = ra[i];
 #pragma unroll
     for (int i = 0; i < NB; ++i) *reinterpret_cast<uint4*>(lb + off32(sr + 64 * i, sc)) = rb[i];
   };
-  f32x16 acc[2][NB];
+  f32x16 acc[MI][NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
   const int nks = a.Kp / BK;
@@ -213,15 +214,15 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     if (ks + 1 < nks) load(ks + 1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2], bfr[NB];
+      bf16x8 af[MI], bfr[NB];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(la + off32(64 * wm + 32 * i + (lane & 31), 2 * kk + h));
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(la + off32((BM / 2) * wm + 32 * i + (lane & 31), 2 * kk + h));
 #pragma unroll
       for (int j = 0; j < NB; ++j)
         bfr[j] = *reinterpret_cast<const bf16x8*>(lb + off32((BN / 2) * wn + 32 * j + (lane & 31), 2 * kk + h));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
@@ -237,10 +238,10 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     for (int j = 0; j < NB; ++j) {
       const int px = (BN / 2) * wn + 32 * j + (lane & 31);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int ml = 64 * wm + 32 * i + 8 * q + 4 * h;
+          const int ml = (BM / 2) * wm + 32 * i + 8 * q + 4 * h;
           uint16_t e[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -277,10 +278,10 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     const int64_t n = p / HoWo, pp = p - n * HoWo;
     bf16_t* ob = a.out + (n * a.G + g) * (int64_t)a.M * HoWo + pp;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + (BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m >= a.M) continue;
         float v = acc[i][j][r];
         if (a.bias) v += bf2f(a.bias[g * a.M + m]);
@@ -292,12 +293,20 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------- bwd-filter
+// dW as an implicit GEMM: rows = output channels (TM per workgroup), columns = the flattened
+// (kh, kw, input channel) reduction axis of the forward (128 per workgroup, so 1x1 and k x k
+// convolutions both fill whole tiles), reduction = output pixels in steps of 64, split over S
+// workgroups per tile. Both operands are [pixel][channel] images (dy rows; x rows gathered at the
+// pixel shifted by each column's (kh, kw)) read transposed from LDS with ds_read_b64_tr_b16. Each
+// split writes its fp32 tile to a slab and wgrad_reduce_kernel adds the S slabs into dW (no
+// atomics), re-indexing (kh, kw, c) columns to the [K][C][KH][KW] weight layout.
 struct WGradArgs {
-  const bf16_t* dyt;  // [N][OH][OW][G][Kgp]
-  const bf16_t* xt;   // [N][H][W][G][Cp]
-  float* dw;          // [G*Kg][Cg][KH][KW] fp32, accumulated
-  int N, G, Kg, Kgp, Cg, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw;
-  int splits;         // workgroups over the output pixels per output tile
+  const bf16_t* dy;   // [N][OH][OW][G][Kgs]
+  const bf16_t* x;    // [N][H][W][G][Cp]
+  float* ws;          // [G][S][Kg][NC] fp32 partial tiles
+  int N, G, Kg, Kgs, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw;
+  int NC;             // KH * KW * Cp columns
+  int S;              // pixel splits per tile
 };
 
 // [rows][TC] bf16 image (TC = 64 or 128 channels per row): the attention kernels' swizzles,
@@ -309,74 +318,83 @@ __device__ __forceinline__ int offc(int row, int col) {
   return row * (TC * 2) + ((((col >> 3) ^ sw)) << 4) + ((col & 7) << 1);
 }
 
-// TC output channels x TC input channels of one (kh, kw) per workgroup, 64 output pixels per
-// step; 4 waves in 2 x 2, each (TC/2)^2 = (TC/64)^2 MFMA tiles of 32 x 32
-template <int TC>
+// TM output channels x 128 columns per workgroup; 4 waves in 2 x 2, each (TM/2) x 64 as
+// (TM/64) x 2 MFMA tiles of 32 x 32
+template <int TM>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WGradArgs a) {
-  constexpr int BP = 64, TI = BP * TC * 2, NCH = TC / 8, LPT = BP * NCH / 256, MT = TC / 64;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TI];
+  constexpr int TN = 128, BP = 64;
+  constexpr int TIA = BP * TM * 2, TIB = BP * TN * 2;
+  constexpr int CA = TM / 8, CB = TN / 8;                   // 16-B chunks per pixel row
+  constexpr int LA = BP * CA / 256, LB = BP * CB / 256;     // chunks per thread per step
+  constexpr int MTM = TM / 64, MTN = TN / 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (TIA + TIB)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int co0 = blockIdx.x * TC;
-  const int ncb = (a.Cg + TC - 1) / TC;
-  const int kpos = blockIdx.y / ncb, ci0 = (blockIdx.y % ncb) * TC;
-  const int kh = kpos / a.KW, kw = kpos % a.KW;
-  const int g = blockIdx.z / a.splits, split = blockIdx.z % a.splits;
+  const int co0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  const int g = blockIdx.z / a.S, split = blockIdx.z % a.S;
   const int64_t P = (int64_t)a.N * a.OH * a.OW;
   const int64_t nsteps = (P + BP - 1) / BP;
-  const int64_t s0 = nsteps * split / a.splits, s1 = nsteps * (split + 1) / a.splits;
-  // this thread's LPT staging slots: pixel row, 16-B channel chunk; the pixel (n, oh, ow) of each
-  // slot advances by 64 every step
-  int srow[LPT], sch[LPT], on[LPT], ooh[LPT], oow[LPT];
+  const int64_t s0 = nsteps * split / a.S, s1 = nsteps * (split + 1) / a.S;
+  // A (dy) slots: rows tid / CA + (256 / CA) i, chunk tid % CA (fixed)
+  const int ach = tid % CA;
+  const bool aok = co0 + ach * 8 < a.Kgs;
+  const bf16_t* abase = a.dy + (int64_t)g * a.Kgs + co0 + ach * 8;
+  const int64_t astride = (int64_t)a.G * a.Kgs;
+  // B (x) slots: rows tid / CB + 16 i, column chunk tid % CB (fixed): its (kh, kw, c)
+  const int bch = tid % CB;
+  const int col = n0 + bch * 8;
+  const bool bok = col < a.NC;
+  const int kpos = bok ? col / a.Cp : 0, bc = col - kpos * a.Cp;
+  const int kh = kpos / a.KW, kw = kpos - kh * a.KW;
+  const bf16_t* bbase = a.x + (int64_t)g * a.Cp + bc;
+  int bn[LB], boh[LB], bow[LB];
+  const int dq = BP / a.OW, dr = BP - dq * a.OW;
 #pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int id = tid + 256 * i;
-    srow[i] = id / NCH;
-    sch[i] = id % NCH;
-    const int64_t p = s0 * BP + srow[i];
-    on[i] = (int)(p / ((int64_t)a.OH * a.OW));
-    const int rem = (int)(p - (int64_t)on[i] * a.OH * a.OW);
-    ooh[i] = rem / a.OW;
-    oow[i] = rem - ooh[i] * a.OW;
+  for (int i = 0; i < LB; ++i) {
+    const int64_t p = s0 * BP + tid / CB + (256 / CB) * i;
+    bn[i] = (int)(p / ((int64_t)a.OH * a.OW));
+    const int rem = (int)(p - (int64_t)bn[i] * a.OH * a.OW);
+    boh[i] = rem / a.OW;
+    bow[i] = rem - boh[i] * a.OW;
   }
-  uint4 ry[LPT], rx[LPT];
+  uint4 ra[LA], rb[LB];
+  int64_t st_cur = s0;
   auto load = [&]() {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      uint4 vy = make_uint4(0, 0, 0, 0), vx = make_uint4(0, 0, 0, 0);
-      if (on[i] < a.N) {
-        const int64_t p = ((int64_t)on[i] * a.OH + ooh[i]) * a.OW + oow[i];
-        const int c = sch[i] * 8;
-        if (co0 + c < a.Kgp) vy = *reinterpret_cast<const uint4*>(a.dyt + (p * a.G + g) * a.Kgp + co0 + c);
-        const int ih = ooh[i] * a.sh - a.ph + kh, iw = oow[i] * a.sw - a.pw + kw;
-        if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W && ci0 + c < a.Cp)
-          vx = *reinterpret_cast<const uint4*>(a.xt + ((((int64_t)on[i] * a.H + ih) * a.W + iw) * a.G + g) * a.Cp +
-                                               ci0 + c);
-      }
-      ry[i] = vy;
-      rx[i] = vx;
-      // next step: 64 pixels on
-      oow[i] += BP;
-      while (oow[i] >= a.OW) {
-        oow[i] -= a.OW;
-        if (++ooh[i] == a.OH) { ooh[i] = 0; ++on[i]; }
-      }
+    for (int i = 0; i < LA; ++i) {
+      const int64_t p = st_cur * BP + tid / CA + (256 / CA) * i;
+      ra[i] = (aok && p < P) ? *reinterpret_cast<const uint4*>(abase + p * astride) : make_uint4(0, 0, 0, 0);
     }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int ih = boh[i] * a.sh - a.ph + kh, iw = bow[i] * a.sw - a.pw + kw;
+      if (bok && bn[i] < a.N && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        v = *reinterpret_cast<const uint4*>(bbase + ((((int64_t)bn[i] * a.H + ih) * a.W + iw) * a.G) * a.Cp);
+      rb[i] = v;
+      // next step: 64 pixels on
+      bow[i] += dr;
+      boh[i] += dq;
+      if (bow[i] >= a.OW) { bow[i] -= a.OW; ++boh[i]; }
+      if (boh[i] >= a.OH) { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
+    }
+    ++st_cur;
   };
   auto stash = [&](int buf) {
-    char* ly = smem + buf * 2 * TI;
-    char* lx = ly + TI;
+    char* la = smem + buf * (TIA + TIB);
+    char* lb = la + TIA;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      *reinterpret_cast<uint4*>(ly + offc<TC>(srow[i], sch[i] * 8)) = ry[i];
-      *reinterpret_cast<uint4*>(lx + offc<TC>(srow[i], sch[i] * 8)) = rx[i];
-    }
+    for (int i = 0; i < LA; ++i)
+      *reinterpret_cast<uint4*>(la + offc<TM>(tid / CA + (256 / CA) * i, ach * 8)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < LB; ++i)
+      *reinterpret_cast<uint4*>(lb + offc<TN>(tid / CB + (256 / CB) * i, bch * 8)) = rb[i];
   };
-  f32x16 acc[MT][MT];
+  f32x16 acc[MTM][MTN];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MTM; ++i)
 #pragma unroll
-    for (int j = 0; j < MT; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < MTN; ++j) acc[i][j] = f32x16{};
   const int G4 = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
   if (s0 < s1) {
     load();
@@ -385,73 +403,127 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WGradArgs a) {
   __syncthreads();
   for (int64_t st = s0; st < s1; ++st) {
     const int buf = (int)((st - s0) & 1);
-    const char* ly = smem + buf * 2 * TI;
-    const char* lx = ly + TI;
+    const char* la = smem + buf * (TIA + TIB);
+    const char* lb = la + TIA;
     const bool more = st + 1 < s1;
     if (more) load();
 #pragma unroll
     for (int ks = 0; ks < BP / 16; ++ks) {
       const int r0 = 16 * ks + 4 * h + qi;
-      bf16x8 fa[MT], fb[MT];
+      bf16x8 fa[MTM], fb[MTN];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int col = (TC / 2) * wm + 32 * i + 16 * (G4 & 1) + 4 * pi;
-        fa[i] = cat(trr(ly, offc<TC>(r0, col)), trr(ly, offc<TC>(r0 + 8, col)));
+      for (int i = 0; i < MTM; ++i) {
+        const int c = (TM / 2) * wm + 32 * i + 16 * (G4 & 1) + 4 * pi;
+        fa[i] = cat(trr(la, offc<TM>(r0, c)), trr(la, offc<TM>(r0 + 8, c)));
       }
 #pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int col = (TC / 2) * wn + 32 * j + 16 * (G4 & 1) + 4 * pi;
-        fb[j] = cat(trr(lx, offc<TC>(r0, col)), trr(lx, offc<TC>(r0 + 8, col)));
+      for (int j = 0; j < MTN; ++j) {
+        const int c = (TN / 2) * wn + 32 * j + 16 * (G4 & 1) + 4 * pi;
+        fb[j] = cat(trr(lb, offc<TN>(r0, c)), trr(lb, offc<TN>(r0 + 8, c)));
       }
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MTM; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < MTN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     if (more) stash(buf ^ 1);
     __syncthreads();
   }
-  if (s0 >= s1) return;
-  // acc[i][j]: row = output channel, column = input channel (lane & 31)
+  // acc[i][j]: row = output channel, column = lane & 31; every split writes its whole slab tile
+  // (zeros for an empty split) so that the reduce reads defined values
+  float* slab = a.ws + ((int64_t)(g * a.S + split) * a.Kg) * a.NC;
 #pragma unroll
-  for (int j = 0; j < MT; ++j) {
-    const int ci = ci0 + (TC / 2) * wn + 32 * j + (lane & 31);
-    if (ci >= a.Cg) continue;
+  for (int j = 0; j < MTN; ++j) {
+    const int cc = n0 + (TN / 2) * wn + 32 * j + (lane & 31);
+    if (cc >= a.NC) continue;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MTM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = co0 + (TC / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co < a.Kg)
-          atomicAdd(a.dw + ((((int64_t)(g * a.Kg + co) * a.Cg + ci) * a.KH + kh) * a.KW + kw), acc[i][j][r]);
+        const int co = co0 + (TM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co < a.Kg) slab[(int64_t)co * a.NC + cc] = acc[i][j][r];
       }
     }
   }
+}
+
+// dW[g*Kg + m][c][kh][kw] += sum over the S slabs of column (kh*KW + kw)*Cp + c (c < Cg). A
+// workgroup owns 16 consecutive slab elements and folds their S partials in 16 strided groups (a
+// thread per element looping over S serially was latency-bound: ~0.5 us per 4 loads, S ~ 300)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, int G,
+                                                           int S, int Kg, int NC, int Cg, int Cp, int KK) {
+  __shared__ float sh[16][17];
+  const int64_t total = (int64_t)G * Kg * NC, slab = (int64_t)Kg * NC;
+  const int el = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + el;
+  float v = 0.f;
+  int g = 0;
+  int64_t rem = 0;
+  if (i < total) {
+    g = (int)(i / slab);
+    rem = i - (int64_t)g * slab;
+    const float* p = ws + (int64_t)g * S * slab + rem;
+    int s = sg;
+    for (; s + 48 < S; s += 64) v += (p[s * slab] + p[(s + 16) * slab]) + (p[(s + 32) * slab] + p[(s + 48) * slab]);
+    for (; s < S; s += 16) v += p[s * slab];
+  }
+  sh[sg][el] = v;
+  __syncthreads();
+  if (sg != 0 || i >= total) return;
+  for (int k = 1; k < 16; ++k) v += sh[k][el];
+  const int m = (int)(rem / NC), colx = (int)(rem - (int64_t)m * NC);
+  const int kp = colx / Cp, c = colx - kp * Cp;
+  if (c < Cg) dw[((int64_t)(g * Kg + m) * Cg + c) * KK + kp] += v;
 }
 
 // ------------------------------------------------------------------------------- host
 static int round8(int v) { return (v + 7) / 8 * 8; }
 static int kpad(int KH, int KW, int redp) { return (KH * KW * redp + 31) / 32 * 32; }
 
-// 128 x 128 tiles while they give at least two workgroups per CU, else 128 x 64 (twice the
-// workgroups for the same work: the K loop is latency-bound at one workgroup per CU)
+// 128-row tiles, or 64 when the GEMM has at most 64 rows (narrow layers: half the MFMA work of a
+// 128-row tile would be padding); 128 pixels per tile while that gives at least two workgroups per
+// CU, else 64 (twice the workgroups for the same work: the K loop is latency-bound at one
+// workgroup per CU)
+template <bool BWD, int BM>
+static void launch_igemm_bm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_t st) {
+  const int64_t t128 = ((P + 127) / 128) * ((M + BM - 1) / BM) * G;
+  if (t128 >= 512)
+    hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 128>), dim3((unsigned)((P + 127) / 128), (M + BM - 1) / BM, G),
+                       dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 64>), dim3((unsigned)((P + 63) / 64), (M + BM - 1) / BM, G),
+                       dim3(256), 0, st, a);
+}
 template <bool BWD>
 static void launch_igemm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_t st) {
-  const int64_t t128 = ((P + 127) / 128) * ((M + 127) / 128) * G;
-  if (t128 >= 512)
-    hipLaunchKernelGGL((conv_igemm_kernel<BWD, 128>), dim3((unsigned)((P + 127) / 128), (M + 127) / 128, G), dim3(256),
-                       0, st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BWD, 64>), dim3((unsigned)((P + 63) / 64), (M + 127) / 128, G), dim3(256), 0,
-                       st, a);
+  if (M <= 64) launch_igemm_bm<BWD, 64>(a, P, M, G, st);
+  else launch_igemm_bm<BWD, 128>(a, P, M, G, st);
 }
+
+// backward-filter tiling: 64-row tiles for narrow outputs, else 128. Pixel splits: about as many
+// workgroups as fit the CUs at once (3 per CU at 64 rows, 2 at 128: LDS), each over at least 4
+// steps of 64 pixels; slabs capped at 64 MB
+static int wgrad_tm(int Kg) { return Kg <= 64 ? 64 : 128; }
+static int wgrad_splits(int64_t P, int G, int Kg, int NC) {
+  const int TM = wgrad_tm(Kg);
+  const int64_t tiles = (int64_t)G * ((Kg + TM - 1) / TM) * ((NC + 127) / 128);
+  const int64_t nsteps = (P + 63) / 64, slots = TM == 64 ? 768 : 512;
+  int64_t S = std::min<int64_t>(nsteps / 4, (slots + tiles - 1) / tiles);
+  S = std::min<int64_t>(S, (int64_t)(16 << 20) / std::max<int64_t>(1, (int64_t)G * Kg * NC));
+  return (int)std::max<int64_t>(1, S);
+}
+
+static int64_t align8(int64_t v) { return (v + 7) / 8 * 8; }
 
 int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH, int KW, int G) {
   // bf16 elements: channel-last input + channel-last output gradient + packed weights (fwd / bwd)
+  // + the backward-filter fp32 slabs (2 bf16 elements each)
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
-  const int64_t xt = (int64_t)N * H * W * G * Cp, yt = (int64_t)N * OH * OW * G * Kgp;
+  const int64_t xt = align8((int64_t)N * H * W * G * Cp), yt = align8((int64_t)N * OH * OW * G * Kgp);
   const int64_t wf = (int64_t)G * Kg * kpad(KH, KW, Cp), wb = (int64_t)G * Cg * kpad(KH, KW, Kgp);
-  return xt + yt + std::max(wf, wb) + 64;
+  const int NC = KH * KW * Cp;
+  const int64_t slabs = (int64_t)wgrad_splits((int64_t)N * OH * OW, G, Kg, NC) * G * Kg * NC;
+  return xt + yt + align8(std::max(wf, wb)) + 2 * slabs + 64;
 }
 
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
@@ -460,7 +532,7 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg);
   bf16_t* xt = (bf16_t*)ws;
-  bf16_t* wp = xt + (int64_t)N * H * W * G * Cp + (int64_t)N * OH * OW * G * round8(Kg);
+  bf16_t* wp = xt + align8((int64_t)N * H * W * G * Cp) + align8((int64_t)N * OH * OW * G * round8(Kg));
   const int Kp = kpad(KH, KW, Cp);
   // a channel-last input (Cg % 8 == 0, so Cp == Cg) is the implicit GEMM's B operand as it is
   const bf16_t* src = (const bf16_t*)x;
@@ -481,8 +553,9 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
   bf16_t* xt = (bf16_t*)ws;
-  bf16_t* yt = xt + (int64_t)N * H * W * G * Cp;
-  bf16_t* wp = yt + (int64_t)N * OH * OW * G * Kgp;
+  bf16_t* yt = xt + align8((int64_t)N * H * W * G * Cp);
+  bf16_t* wp = yt + align8((int64_t)N * OH * OW * G * Kgp);
+  float* slabs = (float*)(wp + align8(std::max((int64_t)G * Kg * kpad(KH, KW, Cp), (int64_t)G * Cg * kpad(KH, KW, Kgp))));
   const bf16_t* ysrc = (const bf16_t*)dy;
   if (!dy_nhwc) {
     launch_nhwc((const bf16_t*)dy, yt, N, G, Kg, OH * OW, Kgp, st);
@@ -503,17 +576,15 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
       launch_nhwc((const bf16_t*)x, xt, N, G, Cg, H * W, Cp, st);
       xsrc = xt;
     }
-    // 64-channel tiles (the 128-channel variant measured no faster); split the pixels so that
-    // about 1k workgroups run, each over at least 16 steps of 64 pixels (2k workgroups of 8+
-    // steps measured slower: more atomics, more prologues; scripts/conv_probe.py)
-    const int TC = 64;
-    const int tiles = ((Kg + TC - 1) / TC) * ((Cg + TC - 1) / TC) * KH * KW * G;
-    const int64_t nsteps = ((int64_t)N * OH * OW + 63) / 64;
-    const int splits = (int)std::max<int64_t>(1, std::min<int64_t>((nsteps + 15) / 16, (1024 + tiles - 1) / tiles));
-    WGradArgs b{ysrc, xsrc, dw, N, G, Kg, Kgp, Cg, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, splits};
-    const dim3 grid((Kg + TC - 1) / TC, ((Cg + TC - 1) / TC) * KH * KW, G * splits);
-    if (TC == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
+    const int NC = KH * KW * Cp, TM = wgrad_tm(Kg);
+    const int64_t P = (int64_t)N * OH * OW;
+    const int S = wgrad_splits(P, G, Kg, NC);
+    WGradArgs b{ysrc, xsrc, slabs, N, G, Kg, Kgp, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, NC, S};
+    const dim3 grid((Kg + TM - 1) / TM, (NC + 127) / 128, G * S);
+    if (TM == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
     else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(256), 0, st, b);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)G * Kg * NC + 15) / 16)), dim3(256), 0, st, slabs,
+                       dw, G, S, Kg, NC, Cg, Cp, KH * KW);
   }
 }
 
