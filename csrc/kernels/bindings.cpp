@@ -521,7 +521,7 @@ void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, 
                   cur_stream());
 }
 void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Tensor> dw, Tensor ws,
-                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc) {
+                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc, bool accum_dx) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv2d: bf16 tensors");
@@ -535,7 +535,7 @@ void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Ten
               "conv2d_bwd: dw must be fp32 like w");
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_bwd: workspace too small");
   ffk::conv2d_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), ptr(dx), ptr<float>(dw), ws.data_ptr(), gi.data(),
-                  dx.has_value(), x_nhwc, dy_nhwc, cur_stream());
+                  dx.has_value(), x_nhwc, dy_nhwc, accum_dx && dx.has_value(), cur_stream());
 }
 
 }  // namespace

@@ -290,9 +290,9 @@ __device__ __forceinline__ void st8(bf16_t* p, const float* v) {
 }
 
 // STATS: a = x -> Welford (n, mean, M2); BWD: a = x, b = dy -> (sum d, sum d * xhat) with the ReLU
-// mask recomputed; SUM: a = dy, b = y (optional ReLU mask) -> sum dz, dz written when requested,
-// the per-workgroup channel sums added straight into the fp32 bias gradient (part) by atomics: no
-// finalize launch (its latency-bound fold over ~1k splits cost as much as the reduction)
+// mask recomputed; SUM: a = dy, b = y (optional ReLU mask) -> sum dz, dz written when requested.
+// (Adding the SUM partials straight into the bias gradient by float atomics was slower: ~600
+// splits' same-address atomics serialize, and capping the splits starves the reduction.)
 template <int MODE>
 __global__ void __launch_bounds__(256) nhwc_colred_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
                                                           bf16_t* __restrict__ dz, const float* __restrict__ mean,
@@ -392,18 +392,14 @@ __global__ void __launch_bounds__(256) nhwc_colred_kernel(const bf16_t* __restri
           if (NV == 2) f[1] += p[1];
         }
       }
-      if (MODE == CR_SUM) {
-        if (part) atomicAdd(part + c, f[0]);  // SUM: part is the fp32 bias gradient itself
-      } else {
-        float* o = part + ((int64_t)s * q.C + c) * NV;
+      float* o = part + ((int64_t)s * q.C + c) * NV;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) o[v] = f[v];
-      }
+      for (int v = 0; v < NV; ++v) o[v] = f[v];
     }
   }
 }
 
-// finalize of the NHWC partials part[S][C][NV] (STATS, BWD): a workgroup owns 8 channels, its 32
+// finalize of the NHWC partials part[S][C][NV]: a workgroup owns 8 channels, its 32
 // thread groups fold strided subsets of the S splits (independent loads, 4 in flight: the partials
 // sit in other XCDs' L2 or in HBM, so the fold is latency-bound) and merge through LDS
 template <int MODE>
@@ -412,14 +408,16 @@ __global__ void __launch_bounds__(256) nhwc_finalize_kernel(const float* __restr
                                                             float* __restrict__ out1, float* __restrict__ run_mean,
                                                             float* __restrict__ run_var, float* __restrict__ dg,
                                                             float* __restrict__ db) {
-  constexpr int NV = MODE == CR_STATS ? 3 : 2, CPB = 8, NG = 256 / CPB;
+  constexpr int NV = MODE == CR_STATS ? 3 : MODE == CR_BWD ? 2 : 1, CPB = 8, NG = 256 / CPB;
   __shared__ float sh[NG][CPB][NV];
   const int cl = threadIdx.x % CPB, sg = threadIdx.x / CPB;
   const int c = blockIdx.x * CPB + cl;
   float f[3] = {0.f, 0.f, 0.f};
   auto merge = [&](const float* v) {
     if (MODE == CR_STATS) wf_merge(f[0], f[1], f[2], v[0], v[1], v[2]);
-    else { f[0] += v[0]; f[1] += v[1]; }
+    else
+#pragma unroll
+      for (int k = 0; k < NV; ++k) f[k] += v[k];
   };
   if (c < C) {
     int s = sg;
@@ -446,11 +444,13 @@ __global__ void __launch_bounds__(256) nhwc_finalize_kernel(const float* __restr
     out1[c] = rsqrtf(var + eps);
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (n > 1.f ? m2 / (n - 1.f) : var);
-  } else {
+  } else if (MODE == CR_BWD) {
     out0[2 * c] = f[0];
     out0[2 * c + 1] = f[1];
     if (dg) dg[c] += f[1];
     if (db) db[c] += f[0];
+  } else {
+    db[c] += f[0];
   }
 }
 
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(256) bn_bwd_dx_nhwc_kernel(const bf16_t* __res
 
 // splits of the NHWC column reduction: ~1k workgroups over (channel blocks x splits), each split
 // at least one full trip of U x R rows
-static ColGeom nhwc_geom(int64_t M, int C) {
+static ColGeom nhwc_geom(int64_t M, int C, int max_splits = 1024) {
   ColGeom q;
   q.M = M;
   q.C = C;
@@ -508,7 +508,7 @@ static ColGeom nhwc_geom(int64_t M, int C) {
   q.R = 256 / q.L;
   const int ncb = (q.C8 + 31) / 32;
   const int64_t trips = (M + 4LL * q.R - 1) / (4LL * q.R);
-  q.S = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(1024 + ncb - 1) / ncb, trips, 1024}));
+  q.S = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(1024 + ncb - 1) / ncb, trips, (int64_t)max_splits}));
   return q;
 }
 
@@ -609,7 +609,10 @@ void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, flo
   if (nhwc) {
     const ColGeom q = nhwc_geom((int64_t)N * HW, C);
     hipLaunchKernelGGL(nhwc_colred_kernel<CR_SUM>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, db, q, 0);
+                       (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
+    if (db)
+      hipLaunchKernelGGL(nhwc_finalize_kernel<CR_SUM>, dim3((C + 7) / 8), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f, nullptr,
+                         nullptr, nullptr, nullptr, nullptr, db);
     return;
   }
   const int S = bn_splits(C, (int64_t)N * HW);

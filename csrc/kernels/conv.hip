@@ -116,6 +116,7 @@ struct IGemmArgs {
   int KH, KW, sh, sw, ph, pw;
   int relu;
   int out_nhwc;      // channel-last output (M % 8 == 0)
+  int accum;         // add into the existing output (a gradient summed over several consumers)
 };
 
 template <bool BWD, int BM, int BN>
@@ -264,9 +265,22 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
       const int px = k / (BM / 8), c = k % (BM / 8);
       const int64_t p = p0 + px;
       const int m = m0 + c * 8;
-      if (p < P && m < a.M)
-        *reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m) =
-            *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
+      if (p < P && m < a.M) {
+        uint4* dst = reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m);
+        uint4 v = *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
+        if (a.accum) {  // fp32 sum of the staged value and the existing gradient, one rounding
+          const uint4 o = *dst;
+          const uint32_t* ow = reinterpret_cast<const uint32_t*>(&o);
+          uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float lo = bf2f((bf16_t)(vw[k] & 0xffff)) + bf2f((bf16_t)(ow[k] & 0xffff));
+            const float hi = bf2f((bf16_t)(vw[k] >> 16)) + bf2f((bf16_t)(ow[k] >> 16));
+            vw[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+        }
+        *dst = v;
+      }
     }
     return;
   }
@@ -286,6 +300,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
         float v = acc[i][j][r];
         if (a.bias) v += bf2f(a.bias[g * a.M + m]);
         if (a.relu) v = fmaxf(v, 0.f);
+        if (a.accum) v += bf2f(ob[(int64_t)m * HoWo]);
         ob[(int64_t)m * HoWo] = f2bf(v);
       }
     }
@@ -321,7 +336,7 @@ __device__ __forceinline__ int offc(int row, int col) {
 // TM output channels x 128 columns per workgroup; 4 waves in 2 x 2, each (TM/2) x 64 as
 // (TM/64) x 2 MFMA tiles of 32 x 32
 template <int TM>
-__global__ void __launch_bounds__(256) conv_wgrad_kernel(WGradArgs a) {
+__global__ void __launch_bounds__(256, 2) conv_wgrad_kernel(WGradArgs a) {  // 2 waves / SIMD: <= 256 registers
   constexpr int TN = 128, BP = 64;
   constexpr int TIA = BP * TM * 2, TIB = BP * TN * 2;
   constexpr int CA = TM / 8, CB = TN / 8;                   // 16-B chunks per pixel row
@@ -543,12 +558,12 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Kg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                      wp, G, Kg, Cg, KH, KW, Kp, 0);
   IGemmArgs a{wp, src, (bf16_t*)y, (const bf16_t*)bias, N, G, Kg, Kp, H, W, Cp, OH, OW, KH, KW, sh, sw, ph, pw, relu,
-              y_nhwc};
+              y_nhwc, 0};
   launch_igemm<false>(a, (int64_t)N * OH * OW, Kg, G, st);
 }
 
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, int x_nhwc, int dy_nhwc, hipStream_t st) {
+                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
@@ -565,7 +580,8 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
     const int Kp = kpad(KH, KW, Kgp);
     hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                        wp, G, Kg, Cg, KH, KW, Kp, 1);
-    IGemmArgs a{wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc};
+    IGemmArgs a{wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc,
+                accum_dx};
     launch_igemm<true>(a, (int64_t)N * H * W, Cg, G, st);
   }
   if (dw) {

@@ -139,6 +139,6 @@ int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH,
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
                 int x_nhwc, int y_nhwc, hipStream_t st);
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, int x_nhwc, int dy_nhwc, hipStream_t st);
+                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st);  // accum_dx: dx +=
 
 }  // namespace ffk

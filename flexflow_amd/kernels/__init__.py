@@ -1254,9 +1254,10 @@ def _nhwc_flag(t, c):
     return cl_ok(t, c) and is_nhwc(t)
 
 
-def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out):
+def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False):
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
-    ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g, _nhwc_flag(x, g[1] // g[13]), _nhwc_flag(dy, g[4] // g[13]))
+    ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g, _nhwc_flag(x, g[1] // g[13]), _nhwc_flag(dy, g[4] // g[13]),
+                     accum_dx)
 
 
 def _conv_pick(kind, key, cands):
@@ -1266,7 +1267,7 @@ def _conv_pick(kind, key, cands):
     if choice is None:
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             return "ours"
-        times = {k: _time(f, reps=3) for k, f in cands.items()}
+        times = _time_all(cands, rounds=2)  # interleaved, best of 2 rounds: single passes flipped choices
         choice = min(times, key=lambda k: times[k])
         TUNE_LOG.append({"op": f"conv2d_{kind}", "geom": list(key), "times_ms": {k: round(v, 4) for k, v in
                                                                                times.items()}, "choice": choice})
@@ -1298,9 +1299,13 @@ def conv2d_fwd(x, w, b, stride, pad, groups, relu):
     return _conv_lib_fwd(x, w, b, g, relu)
 
 
-def conv2d_bwd(x, w, dy, g, dw, need_dx):
+def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None):
     """Backward of conv2d_fwd for geometry g (conv_geometry): returns dx (or None) and adds the
-    weight gradient into dw (fp32, shaped like w, may be None)."""
+    weight gradient into dw (fp32, shaped like w, may be None). dx_acc: an existing gradient of x
+    that dx is added into (and returned): our dgrad kernel accumulates in its epilogue when dx_acc
+    has x's memory layout, otherwise a separate add."""
+    if not need_dx:
+        dx_acc = None
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16:
         x = cl_dense(x, cl_ok(x, g[1] // g[13]))
         dy = cl_dense(dy, cl_ok(dy, g[4] // g[13]))
@@ -1315,18 +1320,26 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx):
         choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None, is_nhwc(x)),
                             {"ours": ours, "lib": lambda: _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)})
         if choice == "ours":
-            dxo = torch.empty_like(x) if need_dx else None
+            acc_in = dx_acc is not None and dx_acc.dtype == x.dtype and is_nhwc(dx_acc) == is_nhwc(x) and \
+                (dx_acc.is_contiguous() or is_nhwc(dx_acc))
+            dxo = dx_acc if acc_in else (torch.empty_like(x) if need_dx else None)
             if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.shape == w.shape:
-                _conv_ours_bwd(x, w, dy, g, dxo, dw)  # atomics accumulate straight into the gradient
+                _conv_ours_bwd(x, w, dy, g, dxo, dw, acc_in)  # the slab reduce adds into the gradient
             else:
                 dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
-                _conv_ours_bwd(x, w, dy, g, dxo, dwo)
+                _conv_ours_bwd(x, w, dy, g, dxo, dwo, acc_in)
                 if dw is not None:
                     dw.add_(dwo.view_as(dw))
+            if dx_acc is not None and not acc_in:
+                dx_acc.add_(dxo)
+                return dx_acc
             return dxo
     dxo, dwo = _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)
     if dw is not None:
         dw.add_(dwo.float().view_as(dw))
+    if dx_acc is not None:
+        dx_acc.add_(dxo)
+        return dx_acc
     return dxo
 
 

@@ -163,6 +163,11 @@ class OpImpl:
         input gradient into that tensor (same shape/dtype) and returns it for that slot."""
         return False
 
+    def accum_target_ok(self, t) -> bool:
+        """May t (an existing input gradient) be this op's dx_accum target? Default: row-major
+        contiguous (GEMM outputs are written through a 2-D view)."""
+        return t.is_contiguous()
+
     def accum_may_alias_douts(self) -> bool:
         """True if every read of the output gradients is issued before the first write into a
         dx_accum target, so that target may share storage with an output gradient."""

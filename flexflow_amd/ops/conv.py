@@ -170,7 +170,10 @@ class Conv2D(_Spatial):
         kh, kw, sh, sw, ph, pw = self._kp()
         g = K.conv_geometry(xc, w, (sh, sw), pad, self.attrs.get("groups", 1))
         dw = ctx.wgrads[0] if ctx.wgrads else None
-        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True))
+        acc = (ctx.extra.get("dx_accum") or {}).get(0)
+        if acc is not None and tuple(xc.shape) != tuple(x_shape):
+            acc = None  # attribute-parallel crop: dx is scattered into a fresh block below
+        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True), dx_acc=acc)
         if dx is None:  # the input needs no gradient (the data, or a frozen producer)
             return [None]
         if tuple(dx.shape) != tuple(x_shape):  # attribute-parallel: scatter crop back into halo'd block
@@ -196,6 +199,12 @@ class Conv2D(_Spatial):
         (a2, b2, l2), (a3, b3, l3) = sl
         full[:, :, a2:b2, a3:b3] += dxc[:, :, l2:l2 + (b2 - a2), l3:l3 + (b3 - a3)]
         return full
+
+    def accumulates_dx(self):
+        return True  # the dgrad kernel adds into an existing input gradient (kernels.conv2d_bwd)
+
+    def accum_target_ok(self, t):
+        return t.is_contiguous() or K.is_nhwc(t)
 
     def flops(self, in_shapes, out_shapes, w_shapes):
         w = w_shapes[0]

@@ -850,7 +850,7 @@ class Executor:
             if any(g is not None and g.untyped_storage().data_ptr() == sp for k, g in grads.items() if k != t.guid) \
                     or (not L.impl.accum_may_alias_douts()
                         and any(d is not None and d.untyped_storage().data_ptr() == sp for d in douts)) \
-                    or not prev.is_contiguous():
+                    or not L.impl.accum_target_ok(prev):
                 continue
             out[j] = prev
         return out or None

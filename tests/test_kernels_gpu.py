@@ -642,6 +642,11 @@ def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     K._conv_ours_bwd(x, w, dz, g, dx, dw)
     assert _rel(dx, xr.grad) < 1.5e-2
     assert _rel(dw, wr.grad) < 1e-2
+    # dgrad accumulating into an existing gradient (a tensor with several consumers)
+    acc0 = torch.randn_like(x)
+    acc = acc0.clone()
+    K._conv_ours_bwd(x, w, dz, g, acc, None, True)
+    assert _rel(acc, acc0.float() + xr.grad) < 1.5e-2
     db = torch.zeros(Ko, device=DEV)
     K.conv_bias_relu_bwd(dy, y, db)
     assert _rel(db, br.grad) < 1e-3
