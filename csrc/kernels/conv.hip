@@ -119,6 +119,103 @@ struct IGemmArgs {
   int accum;         // add into the existing output (a gradient summed over several consumers)
 };
 
+// Epilogue of the implicit GEMMs: acc[i][j] row = channel (r&3) + 8(r>>2) + 4h of the wave's
+// (BM/2)-row block, column = pixel lane & 31 of its (BN/2)-pixel block; bias, ReLU, accumulate.
+// smem: >= BN * (2 BM + 16) bytes, free (every wave past its last read of the K loop's images).
+template <int BM, int BN>
+__device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)[BM / 64][BN / 64], char* smem,
+                                               int m0, int64_t p0, int64_t P, int g) {
+  constexpr int MI = BM / 64, NB = BN / 64, RS = BM * 2 + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  if (a.out_nhwc) {
+    // stage the tile as [pixel][channel] in LDS (the K loop's buffers are free after its last
+    // barrier), then store whole 16-B channel chunks: a pixel's BM channels are one contiguous run
+    // of the channel-last output, consecutive lanes on consecutive chunks. The lane's bias values
+    // (4 consecutive channels per (i, q); M % 8 == 0 here) are loaded once, 8 B at a time.
+    float bv[MI][4][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + (BM / 2) * wm + 32 * i + 8 * q + 4 * h;
+        uint2 raw = make_uint2(0, 0);
+        if (a.bias && m < a.M) raw = *reinterpret_cast<const uint2*>(a.bias + g * a.M + m);
+        bv[i][q][0] = bf2f((bf16_t)(raw.x & 0xffff));
+        bv[i][q][1] = bf2f((bf16_t)(raw.x >> 16));
+        bv[i][q][2] = bf2f((bf16_t)(raw.y & 0xffff));
+        bv[i][q][3] = bf2f((bf16_t)(raw.y >> 16));
+      }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int px = (BN / 2) * wn + 32 * j + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ml = (BM / 2) * wm + 32 * i + 8 * q + 4 * h;
+          uint16_t e[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float v = acc[i][j][4 * q + k] + bv[i][q][k];
+            if (a.relu) v = fmaxf(v, 0.f);
+            e[k] = f2bf(v);
+          }
+          uint2 pk;
+          pk.x = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
+          pk.y = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+          *reinterpret_cast<uint2*>(smem + px * RS + ml * 2) = pk;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t ldo = (int64_t)a.G * a.M;
+    for (int k = tid; k < BN * (BM / 8); k += 256) {
+      const int px = k / (BM / 8), c = k % (BM / 8);
+      const int64_t p = p0 + px;
+      const int m = m0 + c * 8;
+      if (p < P && m < a.M) {
+        uint4* dst = reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m);
+        uint4 v = *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
+        if (a.accum) {  // fp32 sum of the staged value and the existing gradient, one rounding
+          const uint4 o = *dst;
+          const uint32_t* ow = reinterpret_cast<const uint32_t*>(&o);
+          uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float lo = bf2f((bf16_t)(vw[k] & 0xffff)) + bf2f((bf16_t)(ow[k] & 0xffff));
+            const float hi = bf2f((bf16_t)(vw[k] >> 16)) + bf2f((bf16_t)(ow[k] >> 16));
+            vw[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+        }
+        *dst = v;
+      }
+    }
+    return;
+  }
+  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int64_t p = p0 + (BN / 2) * wn + 32 * j + (lane & 31);
+    if (p >= P) continue;
+    const int64_t n = p / HoWo, pp = p - n * HoWo;
+    bf16_t* ob = a.out + (n * a.G + g) * (int64_t)a.M * HoWo + pp;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= a.M) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v += bf2f(a.bias[g * a.M + m]);
+        if (a.relu) v = fmaxf(v, 0.f);
+        if (a.accum) v += bf2f(ob[(int64_t)m * HoWo]);
+        ob[(int64_t)m * HoWo] = f2bf(v);
+      }
+    }
+  }
+}
+
 template <bool BWD, int BM, int BN>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
   // MI / NB: MFMA row / column tiles per wave (BM / 2 rows x BN / 2 pixels per wave)
@@ -230,81 +327,124 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
     if (ks + 1 < nks) stash(buf ^ 1);
     __syncthreads();
   }
-  // epilogue: acc[i][j] row = channel (r&3) + 8(r>>2) + 4h, column = pixel lane & 31
-  if (a.out_nhwc) {
-    // stage the tile as [pixel][channel] in LDS (the K loop's buffers are free after its last
-    // barrier), then store whole 16-B channel chunks: a pixel's BM channels are one contiguous run
-    // of the channel-last output, consecutive lanes on consecutive chunks
+  igemm_epilogue<BM, BN>(a, acc, smem, m0, p0, P, g);
+}
+
+// ------------------------------------------------------------------------------- fwd / bwd-data (LDS-DMA)
+// The same implicit GEMM with K steps of 64 (one barrier per 64-deep step: at 32 the barrier and the
+// fragment-read restart dominated) and operand tiles written straight into LDS by buffer_load ...
+// lds (no staging registers). Each wave instruction fills one 1-KiB piece = 8 rows of 128 B, lane
+// l landing at row l / 8, slot l % 8; the XOR swizzle (chunk c of row r at slot c ^ (r & 7)) is
+// applied on the global side, so lane l always fetches chunk (l & 7) ^ (l >> 3) of its rows and
+// keeps ONE (kh, kw, c8) reduction cursor. Padding taps, rows past M and pixels past P read an
+// offset beyond the buffer's range, which returns zeros. Two LDS buffers: the DMA for step k + 1
+// is issued right after the barrier that retires step k and runs under step k's MFMAs.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ int off64(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+template <bool BWD, int BM, int BN>
+__global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
+  constexpr int BK = 64, MI = BM / 64, NB = BN / 64;
+  constexpr int TA = BM * BK * 2, TB = BN * BK * 2;
+  constexpr int WA = TA / 1024 / 4, WB = TB / 1024 / 4;  // 1-KiB pieces per wave per step
+  constexpr int RS = BM * 2 + 16;
+  constexpr int SMEM = 2 * (TA + TB) > BN * RS ? 2 * (TA + TB) : BN * RS;
+  constexpr int BAD = 0x7ffffff0;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = blockIdx.z;
+  const int m0 = blockIdx.y * BM;
+  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+  const int64_t p0 = (int64_t)blockIdx.x * BN;
+  const int C8 = a.Cs / 8;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.A + (int64_t)g * a.M * a.Kp), (short)0, a.M * a.Kp * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.B, (short)0, (int)((int64_t)a.N * a.Hs * a.Ws * a.G * a.Cs * 2), 0x00020000);
+  const int ch = (lane & 7) ^ (lane >> 3);  // this lane's 16-B chunk of every 128-B row it loads
+  int aoff[WA];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int px = (BN / 2) * wn + 32 * j + (lane & 31);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ml = (BM / 2) * wm + 32 * i + 8 * q + 4 * h;
-          uint16_t e[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int m = m0 + ml + k;
-            float v = acc[i][j][4 * q + k];
-            if (a.bias && m < a.M) v += bf2f(a.bias[g * a.M + m]);
-            if (a.relu) v = fmaxf(v, 0.f);
-            e[k] = f2bf(v);
-          }
-          uint2 pk;
-          pk.x = (uint32_t)e[0] | ((uint32_t)e[1] << 16);
-          pk.y = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
-          *reinterpret_cast<uint2*>(smem + px * RS + ml * 2) = pk;
-        }
-      }
-    }
-    __syncthreads();
-    const int64_t ldo = (int64_t)a.G * a.M;
-    for (int k = tid; k < BN * (BM / 8); k += 256) {
-      const int px = k / (BM / 8), c = k % (BM / 8);
-      const int64_t p = p0 + px;
-      const int m = m0 + c * 8;
-      if (p < P && m < a.M) {
-        uint4* dst = reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m);
-        uint4 v = *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
-        if (a.accum) {  // fp32 sum of the staged value and the existing gradient, one rounding
-          const uint4 o = *dst;
-          const uint32_t* ow = reinterpret_cast<const uint32_t*>(&o);
-          uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float lo = bf2f((bf16_t)(vw[k] & 0xffff)) + bf2f((bf16_t)(ow[k] & 0xffff));
-            const float hi = bf2f((bf16_t)(vw[k] >> 16)) + bf2f((bf16_t)(ow[k] >> 16));
-            vw[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-          }
-        }
-        *dst = v;
-      }
-    }
-    return;
+  for (int i = 0; i < WA; ++i) {
+    const int m = m0 + (i * 4 + wave) * 8 + (lane >> 3);
+    aoff[i] = m < a.M ? (m * a.Kp + ch * 8) * 2 : BAD;
   }
-  const int64_t HoWo = (int64_t)a.Ho * a.Wo;
+  int pbase[WB], prow[WB], pcol[WB];
+  bool pok[WB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int64_t p = p0 + (BN / 2) * wn + 32 * j + (lane & 31);
-    if (p >= P) continue;
-    const int64_t n = p / HoWo, pp = p - n * HoWo;
-    bf16_t* ob = a.out + (n * a.G + g) * (int64_t)a.M * HoWo + pp;
+  for (int i = 0; i < WB; ++i) {
+    const int64_t p = p0 + (i * 4 + wave) * 8 + (lane >> 3);
+    pok[i] = p < P;
+    const int64_t pp = pok[i] ? p : 0;
+    const int n = (int)(pp / ((int64_t)a.Ho * a.Wo));
+    const int rem = (int)(pp - (int64_t)n * a.Ho * a.Wo);
+    prow[i] = rem / a.Wo;
+    pcol[i] = rem - prow[i] * a.Wo;
+    pbase[i] = n * a.Hs * a.Ws;
+  }
+  // reduction cursor of this lane's chunk: K index ks * 8 + ch -> (kh, kw, c8)
+  int c8 = ch % C8, kw = (ch / C8) % a.KW, kh = ch / C8 / a.KW;
+  auto issue = [&](int buf, int ks) {
+    char* la = smem + buf * (TA + TB);
+    char* lb = la + TA;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
+    for (int i = 0; i < WA; ++i) {
+      const int off = aoff[i] == BAD ? BAD : aoff[i] + ks * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(la + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+    }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (BM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= a.M) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v += bf2f(a.bias[g * a.M + m]);
-        if (a.relu) v = fmaxf(v, 0.f);
-        if (a.accum) v += bf2f(ob[(int64_t)m * HoWo]);
-        ob[(int64_t)m * HoWo] = f2bf(v);
+    for (int i = 0; i < WB; ++i) {
+      bool ok = pok[i] && kh < a.KH;
+      int sy, sx;
+      if (!BWD) {
+        sy = prow[i] * a.sh - a.ph + kh;
+        sx = pcol[i] * a.sw - a.pw + kw;
+      } else {  // source (output-gradient) pixel whose window at (kh, kw) covers this input pixel
+        const int ny = prow[i] + a.ph - kh, nx = pcol[i] + a.pw - kw;
+        ok = ok && ny >= 0 && nx >= 0 && ny % a.sh == 0 && nx % a.sw == 0;
+        sy = ny / a.sh;
+        sx = nx / a.sw;
       }
+      ok = ok && sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws;
+      const int off = ok ? (((pbase[i] + sy * a.Ws + sx) * a.G + g) * a.Cs + c8 * 8) * 2 : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+    }
+    c8 += 8;  // next step: 8 chunks on
+    while (c8 >= C8) {
+      c8 -= C8;
+      if (++kw == a.KW) { kw = 0; ++kh; }
+    }
+  };
+  f32x16 acc[MI][NB];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
+  const int nks = a.Kp / BK;
+  issue(0, 0);
+  for (int ks = 0; ks < nks; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // step ks visible to all waves; every wave is done reading the other buffer
+    if (ks + 1 < nks) issue((ks + 1) & 1, ks + 1);
+    const char* la = smem + (ks & 1) * (TA + TB);
+    const char* lb = la + TA;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      bf16x8 af[MI], bfr[NB];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(la + off64((BM / 2) * wm + 32 * i + (lane & 31), 2 * kk + h));
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + off64((BN / 2) * wn + 32 * j + (lane & 31), 2 * kk + h));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
+  __syncthreads();  // the epilogue reuses the images
+  igemm_epilogue<BM, BN>(a, acc, smem, m0, p0, P, g);
 }
 
 // ------------------------------------------------------------------------------- bwd-filter
@@ -493,21 +633,26 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 
 // ------------------------------------------------------------------------------- host
 static int round8(int v) { return (v + 7) / 8 * 8; }
-static int kpad(int KH, int KW, int redp) { return (KH * KW * redp + 31) / 32 * 32; }
+static int kpad(int KH, int KW, int redp) { return (KH * KW * redp + 63) / 64 * 64; }  // whole 64-deep K steps
 
 // 128-row tiles, or 64 when the GEMM has at most 64 rows (narrow layers: half the MFMA work of a
 // 128-row tile would be padding); 128 pixels per tile while that gives at least two workgroups per
 // CU, else 64 (twice the workgroups for the same work: the K loop is latency-bound at one
 // workgroup per CU)
+// The LDS-DMA kernel needs both operands addressable by 31-bit byte offsets (buffer range); the
+// register-staged kernel takes the rest.
 template <bool BWD, int BM>
 static void launch_igemm_bm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_t st) {
   const int64_t t128 = ((P + 127) / 128) * ((M + BM - 1) / BM) * G;
-  if (t128 >= 512)
-    hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 128>), dim3((unsigned)((P + 127) / 128), (M + BM - 1) / BM, G),
-                       dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 64>), dim3((unsigned)((P + 63) / 64), (M + BM - 1) / BM, G),
-                       dim3(256), 0, st, a);
+  const bool dma = (int64_t)a.N * a.Hs * a.Ws * a.G * a.Cs * 2 < 0x7fff0000LL && (int64_t)a.M * a.Kp * 2 < 0x7fff0000LL;
+  const dim3 g128((unsigned)((P + 127) / 128), (M + BM - 1) / BM, G), g64((unsigned)((P + 63) / 64), (M + BM - 1) / BM, G);
+  if (t128 >= 512) {
+    if (dma) hipLaunchKernelGGL((conv_igemm_dma_kernel<BWD, BM, 128>), g128, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 128>), g128, dim3(256), 0, st, a);
+  } else {
+    if (dma) hipLaunchKernelGGL((conv_igemm_dma_kernel<BWD, BM, 64>), g64, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BWD, BM, 64>), g64, dim3(256), 0, st, a);
+  }
 }
 template <bool BWD>
 static void launch_igemm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_t st) {
