@@ -602,6 +602,135 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_kernel(WGradArgs a) {  // 2
   }
 }
 
+// The same backward-filter GEMM with both [64 pixel][channel] images written by LDS-DMA. A piece
+// is 1 KiB of whole image rows (TC = 128: 4 rows of 256 B; 64: 8 rows of 128 B); lane l lands at
+// row l / (TC / 8), slot l % (TC / 8) and fetches the chunk slot ^ swizzle(row) of offc<TC>, so a
+// lane's column chunk is fixed per piece for the whole kernel: the x gather keeps one (kh, kw, c)
+// per piece and only advances the pixels. Out-of-range pixels / channels / padding taps read
+// beyond the buffer range (zeros).
+template <int TC>
+__device__ __forceinline__ int offc_swz(int row) {
+  return TC == 64 ? ((((row >> 1) & 1) << 2) | ((row >> 3) & 1) | (((row >> 4) & 1) << 1))
+                  : (((row & 3) << 2) | ((row >> 2) & 3));
+}
+
+template <int TM>
+__global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
+  constexpr int TN = 128, BP = 64;
+  constexpr int TIA = BP * TM * 2, TIB = BP * TN * 2;
+  constexpr int WA = TIA / 1024 / 4, WB = TIB / 1024 / 4;  // pieces per wave per step
+  constexpr int RA = 1024 / (TM * 2), RB = 1024 / (TN * 2);  // image rows per piece
+  constexpr int MTM = TM / 64, MTN = TN / 64;
+  constexpr int BAD = 0x7ffffff0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (TIA + TIB)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int co0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  const int g = blockIdx.z / a.S, split = blockIdx.z % a.S;
+  const int64_t P = (int64_t)a.N * a.OH * a.OW;
+  const int64_t nsteps = (P + BP - 1) / BP;
+  const int64_t s0 = nsteps * split / a.S, s1 = nsteps * (split + 1) / a.S;
+  const __amdgpu_buffer_rsrc_t rdy =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, (int)(P * a.G * a.Kgs * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)((int64_t)a.N * a.H * a.W * a.G * a.Cp * 2), 0x00020000);
+  // A (dy) pieces: fixed channel chunk per piece, pixel = step * 64 + row
+  int arow[WA], acol[WA];
+#pragma unroll
+  for (int i = 0; i < WA; ++i) {
+    const int row = (i * 4 + wave) * RA + lane / (TM / 8);
+    const int c = (lane % (TM / 8)) ^ offc_swz<TM>(row);
+    arow[i] = row;
+    acol[i] = co0 + c * 8 < a.Kgs ? (g * a.Kgs + co0 + c * 8) : -1;
+  }
+  // B (x) pieces: fixed column chunk (kh, kw, c) per piece, tracked pixel (n, oh, ow)
+  int bkh[WB], bkw[WB], bcol[WB], bn[WB], boh[WB], bow[WB];
+  const int dq = BP / a.OW, dr = BP - dq * a.OW;
+#pragma unroll
+  for (int i = 0; i < WB; ++i) {
+    const int row = (i * 4 + wave) * RB + lane / (TN / 8);
+    const int c = (lane % (TN / 8)) ^ offc_swz<TN>(row);
+    const int col = n0 + c * 8;
+    const int kpos = col / a.Cp, cc = col - kpos * a.Cp;
+    bkh[i] = col < a.NC ? kpos / a.KW : 1 << 20;  // past the image: always a padding tap
+    bkw[i] = kpos % a.KW;
+    bcol[i] = g * a.Cp + cc;
+    const int64_t p = s0 * BP + row;
+    bn[i] = (int)(p / ((int64_t)a.OH * a.OW));
+    const int rem = (int)(p - (int64_t)bn[i] * a.OH * a.OW);
+    boh[i] = rem / a.OW;
+    bow[i] = rem - boh[i] * a.OW;
+  }
+  auto issue = [&](int buf, int64_t st) {
+    char* la = smem + buf * (TIA + TIB);
+    char* lb = la + TIA;
+#pragma unroll
+    for (int i = 0; i < WA; ++i) {
+      const int64_t p = st * BP + arow[i];
+      const int off = (acol[i] >= 0 && p < P) ? (int)((p * a.G * a.Kgs + acol[i]) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy, (lds_ptr_t)(la + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < WB; ++i) {
+      const int ih = boh[i] * a.sh - a.ph + bkh[i], iw = bow[i] * a.sw - a.pw + bkw[i];
+      const bool ok = bn[i] < a.N && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      const int off = ok ? (int)(((((int64_t)bn[i] * a.H + ih) * a.W + iw) * a.G * a.Cp + bcol[i]) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+      bow[i] += dr;  // next step: 64 pixels on
+      boh[i] += dq;
+      if (bow[i] >= a.OW) { bow[i] -= a.OW; ++boh[i]; }
+      if (boh[i] >= a.OH) { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
+    }
+  };
+  f32x16 acc[MTM][MTN];
+#pragma unroll
+  for (int i = 0; i < MTM; ++i)
+#pragma unroll
+    for (int j = 0; j < MTN; ++j) acc[i][j] = f32x16{};
+  const int G4 = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  if (s0 < s1) issue(0, s0);
+  for (int64_t st = s0; st < s1; ++st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // step st visible to all waves; every wave is done reading the other buffer
+    if (st + 1 < s1) issue((int)((st + 1 - s0) & 1), st + 1);
+    const char* la = smem + (int)((st - s0) & 1) * (TIA + TIB);
+    const char* lb = la + TIA;
+#pragma unroll
+    for (int ks = 0; ks < BP / 16; ++ks) {
+      const int r0 = 16 * ks + 4 * h + qi;
+      bf16x8 fa[MTM], fb[MTN];
+#pragma unroll
+      for (int i = 0; i < MTM; ++i) {
+        const int c = (TM / 2) * wm + 32 * i + 16 * (G4 & 1) + 4 * pi;
+        fa[i] = cat(trr(la, offc<TM>(r0, c)), trr(la, offc<TM>(r0 + 8, c)));
+      }
+#pragma unroll
+      for (int j = 0; j < MTN; ++j) {
+        const int c = (TN / 2) * wn + 32 * j + 16 * (G4 & 1) + 4 * pi;
+        fb[j] = cat(trr(lb, offc<TN>(r0, c)), trr(lb, offc<TN>(r0 + 8, c)));
+      }
+#pragma unroll
+      for (int i = 0; i < MTM; ++i)
+#pragma unroll
+        for (int j = 0; j < MTN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* slab = a.ws + ((int64_t)(g * a.S + split) * a.Kg) * a.NC;
+#pragma unroll
+  for (int j = 0; j < MTN; ++j) {
+    const int cc = n0 + (TN / 2) * wn + 32 * j + (lane & 31);
+    if (cc >= a.NC) continue;
+#pragma unroll
+    for (int i = 0; i < MTM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (TM / 2) * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co < a.Kg) slab[(int64_t)co * a.NC + cc] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // dW[g*Kg + m][c][kh][kw] += sum over the S slabs of column (kh*KW + kw)*Cp + c (c < Cg). A
 // workgroup owns 16 consecutive slab elements and folds their S partials in 16 strided groups (a
 // thread per element looping over S serially was latency-bound: ~0.5 us per 4 loads, S ~ 300)
@@ -742,8 +871,14 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
     const int S = wgrad_splits(P, G, Kg, NC);
     WGradArgs b{ysrc, xsrc, slabs, N, G, Kg, Kgp, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, NC, S};
     const dim3 grid((Kg + TM - 1) / TM, (NC + 127) / 128, G * S);
-    if (TM == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(256), 0, st, b);
+    const bool dma = P * G * Kgp * 2 < 0x7fff0000LL && (int64_t)N * H * W * G * Cp * 2 < 0x7fff0000LL;
+    if (dma) {
+      if (TM == 128) hipLaunchKernelGGL(conv_wgrad_dma_kernel<128>, grid, dim3(256), 0, st, b);
+      else hipLaunchKernelGGL(conv_wgrad_dma_kernel<64>, grid, dim3(256), 0, st, b);
+    } else {
+      if (TM == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
+      else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(256), 0, st, b);
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)G * Kg * NC + 15) / 16)), dim3(256), 0, st, slabs,
                        dw, G, S, Kg, NC, Cg, Cp, KH * KW);
   }
