@@ -350,7 +350,9 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // tile count of the kernel that will run
   int64_t tiles;
-  if (impl == 2 && K % 32 == 0) {
+  if (impl == 3 && K % 64 == 0) {
+    tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
+  } else if (impl == 2 && K % 32 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + gemm256_bn(M, N, batch, 1) - 1) / gemm256_bn(M, N, batch, 1)) * batch;
   } else if (impl >= 1 && K % 64 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch;
@@ -370,7 +372,8 @@ int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
 
 static bool try_large(const GemmArgs& p, bool a_al, bool b_al, hipStream_t stream) {
   if (!(a_al && b_al && p.a_bytes > 0)) return false;
-  if (p.impl == 2 && gemm256_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
+  if (p.impl == 3 && gemm_w4_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
+  if (p.impl >= 2 && gemm256_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl >= 1 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   return false;
 }

@@ -27,7 +27,7 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
                                    (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
-@pytest.mark.parametrize("impl", [2, 1, 0])
+@pytest.mark.parametrize("impl", [3, 2, 1, 0])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -43,8 +43,10 @@ def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 4096, 1), (8192, 3072, 1024, 2), (1024, 4096, 8192, 4),
                                           (1000, 600, 1056, 1), (2048, 2048, 2048, 3)])
-def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk):
-    """256-row ping-pong kernel: BERT-Large shapes (both tile widths), split-K slabs, edge tiles."""
+@pytest.mark.parametrize("impl", [3, 2])
+def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
+    """256-row kernels (3: 4-wave 128x128 per wave, 2: 8-wave ping-pong): BERT-Large shapes,
+    split-K slabs, edge tiles."""
     torch.manual_seed(11)
     Am = torch.randn(M, K, device=DEV).bfloat16()
     Bn = torch.randn(N, K, device=DEV).bfloat16()
@@ -53,10 +55,10 @@ def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk):
     ref = Am.float() @ Bn.float().t()
     ws = torch.empty(M * N * splitk, device=DEV) if splitk > 1 else None
     C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    _gemm(ffC, A, B, C, M, N, K, a_k, b_k, splitk=splitk, ws=ws, impl=2)
+    _gemm(ffC, A, B, C, M, N, K, a_k, b_k, splitk=splitk, ws=ws, impl=impl)
     assert _rel(C, ref) < 1e-2
     C32 = torch.ones(M, N, device=DEV)
-    _gemm(ffC, A, B, C32, M, N, K, a_k, b_k, beta=1.0, splitk=splitk, ws=ws, impl=2)
+    _gemm(ffC, A, B, C32, M, N, K, a_k, b_k, beta=1.0, splitk=splitk, ws=ws, impl=impl)
     assert _rel(C32, ref + 1.0) < 1e-3
 
 
