@@ -25,7 +25,7 @@ struct GemmArgs {
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
-  int impl = 2;  // 3: 4-wave 256x256 kernel (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
+  int impl = 2;  // 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
   // Backward-activation epilogue (gemm256 only, see gemm_dact_bf16): C = (alpha*A.B) * act'(zin),
   // zin the producer's bf16 pre-activation in C's layout; colpart (optional) receives per-128-row
   // fp32 column sums of that product, [2 * ceil(M / 256)][N], for the producer's bias gradient.
@@ -39,7 +39,7 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk);
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl = 2);
 bool gemm_big_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 bool gemm256_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
-// 4-wave 256x256 kernel, 128x128 outputs per wave (gemm_w4.hip); needs K % 64 == 0
+// 4-wave 256x256x64 kernel, 128x128 outputs per wave, two-slot LDS-DMA ring (gemm_w4.hip); K % 128 == 0
 bool gemm_w4_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 int gemm256_bn(int M, int N, int batch, int splitk);
 // dgrad GEMM of a consumer Linear fused with the producer Linear's activation backward:

@@ -23,6 +23,7 @@
 //  src/ops/batch_matmul.cu).
 #include "common.h"
 #include "gemm.h"
+#include "ops.h"
 
 namespace ffk {
 
@@ -350,7 +351,7 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // tile count of the kernel that will run
   int64_t tiles;
-  if (impl == 3 && K % 64 == 0) {
+  if (impl == 3 && K % 128 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
   } else if (impl == 2 && K % 32 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + gemm256_bn(M, N, batch, 1) - 1) / gemm256_bn(M, N, batch, 1)) * batch;
@@ -363,7 +364,7 @@ int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // minimise (waves of 256 CUs) / split, with a small charge per split for the fp32 slab reduce
   int best = 1;
   double best_cost = 1e30;
-  for (int s = 1; s <= 8 && K / s >= 512; ++s) {
+  for (int s = 1; s <= 16 && K / s >= 512; ++s) {
     const double cost = (double)((tiles * s + 255) / 256) / s + 0.03 * s;
     if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
   }
@@ -403,6 +404,11 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
     dim3 grid(tm * tn, p.batch * p.splitk);
     if (!try_large(p, a_al, b_al, stream)) dispatch_layout<2>(p, grid, stream, a_al, b_al);
     const int64_t total = (int64_t)p.M * p.N * p.batch;
+    if (p.out_f32 && p.batch == 1 && p.ldc == p.N && !p.bias && !p.Z && p.act == ACT_NONE && total % 4 == 0 &&
+        aligned16(p.C) && aligned16(p.ws)) {
+      slab_sum(p.ws, reinterpret_cast<float*>(p.C), total, p.splitk, p.beta, stream);  // float4 slab reduce
+      return;
+    }
     if (p.out_f32) hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
     else hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(ew_grid(total, 256)), dim3(256), 0, stream, p);
     return;

@@ -117,6 +117,15 @@ __device__ __forceinline__ void wait_tiles(int tiles_after) {
 
 __device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Orders every accumulator against neighbouring asm statements (see the 4-wave kernels).
+template <int NF>
+__device__ __forceinline__ void pin_acc(f32x4 (&acc)[8][NF]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) asm volatile("" : "+a"(acc[i][j]));
+}
+
 // Epilogue of a 256-row tile whose waves each own 128 rows x WN columns (acc[i][j]: rows
 // wr*128 + 16 i + (lane & 15), columns wc*WN + 16 j + 4 (lane >> 4) + r; the MFMA operands are
 // swapped so that a lane holds 4 consecutive columns). Shared by gemm256.hip (8 waves, WN = BN/4)

@@ -72,7 +72,7 @@ import os as _os
 
 _TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
 # our kernels: 256-row ping-pong (csrc/kernels/gemm256.hip), 256x128 LDS-DMA (gemm_big.hip), 128x128
-IMPLS = {"k256": 2, "big": 1, "128": 0}
+IMPLS = {"w4": 3, "k256": 2, "big": 1, "128": 0}
 IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []
@@ -368,6 +368,11 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             else:
                 scratch = torch.zeros_like(C)
                 cands = {k: (lambda i=i: ours(i, scratch)) for k, i in IMPLS.items()}
+                if C.dtype == torch.float32 and batch == 1 and K >= 8192 and splitk is None:
+                    # weight gradients: the 4-wave kernel's split-K factor is tuned like the library's
+                    for S in (2, 4, 8, 16):
+                        if K % (S * 128) == 0:
+                            cands[f"w4_sk{S}"] = (lambda S=S: ours(IMPLS["w4"], scratch, S))
                 if plain:
                     cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
                                                      bias, batch, sA, sB, sC)
@@ -396,6 +401,8 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             _tuned[key] = choice
         if isinstance(choice, tuple):
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
+        elif isinstance(choice, str) and choice.startswith("w4_sk"):
+            ours(IMPLS["w4"], sk=int(choice[5:]))
         elif isinstance(choice, str) and choice.startswith("lib_sk"):
             _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, int(choice[6:]))
         elif choice == "lib":

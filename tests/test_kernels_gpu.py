@@ -45,7 +45,7 @@ def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
                                           (1000, 600, 1056, 1), (2048, 2048, 2048, 3)])
 @pytest.mark.parametrize("impl", [3, 2])
 def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
-    """256-row kernels (3: 4-wave 128x128 per wave, 2: 8-wave ping-pong): BERT-Large shapes,
+    """256-row kernels (3: 4-wave 256x256x64, 128x128 per wave; 2: 8-wave ping-pong): BERT-Large shapes,
     split-K slabs, edge tiles."""
     torch.manual_seed(11)
     Am = torch.randn(M, K, device=DEV).bfloat16()
