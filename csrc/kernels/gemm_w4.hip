@@ -9,7 +9,8 @@
 // covers 16 rows x 64 B, half of each 128-B line it touches, and a 256x256x32 build of this kernel
 // ran 5-9 % slower on the BERT-Large forward shapes (profiles/gemm_bert_probe_r3_w4_v2.txt);
 // ablating it (profiles/gemm_w4_ablation_r3.txt) priced the DMA issue at ~20 % of the main loop and
-// the fragment reads at ~3-10 %.
+// the fragment reads at ~3-10 %. Spreading the DMA over both halves (A in three 32-KiB slots, B in
+// two: 160 KiB) measured 1-4 % slower than this two-slot ring (profiles/gemm_bert_probe_r3_w4_v3.txt).
 //
 // Per K-tile t (slot t % 2), per wave:
 //   half 0: 64 MFMAs on the kk = 0 fragments of tile t (registers, read during the previous
@@ -35,8 +36,9 @@ constexpr int A_PIECES = A_BYTES / 1024, PIECES = STAGE / 1024, PW = PIECES / 4;
 
 template <int N>
 __device__ __forceinline__ void vmcnt() {
-  static_assert(N == 0 || N == 16, "add the immediate");
+  static_assert(N == 0 || N == 8 || N == 16, "add the immediate");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
 

@@ -14,6 +14,9 @@ GPU work is long (>= config.graph_min_step_ms, e.g. BERT-Large: 55 ms) keeps run
 measured on MI355X, replaying its ~800-node graph took 58.7 ms/step against 55.1 ms eager (the
 graph's per-node dispatch costs more than the host's launch stream, which runs far ahead of the
 GPU) — while short steps (DLRM, small CNNs), where host launch latency dominates, are captured.
+Steps in between (config.graph_min_step_ms <= eager < config.graph_trial_max_ms, e.g. Inception-v3
+with ~1k kernels per step) are captured on trial: two replays are timed and the graph is kept only
+if it beats the eager step, else dropped for good.
 """
 from __future__ import annotations
 
@@ -29,7 +32,9 @@ class StepGraph:
         self.warm = 0
         self.failed = False
         self.eager_ms = []  # timed eager warm-up steps ("auto" policy)
-        self.decision = None
+        self.graph_ms = []  # timed replays of a trial capture
+        self.trial = 0
+        self.decision = None  # True: replay, False: eager, "trial": replay while timing it
 
     def enabled(self) -> bool:
         m = self.model
@@ -77,7 +82,13 @@ class StepGraph:
                 en.synchronize()
                 ms = st.elapsed_time(en)
                 self.eager_ms.append(ms)
-                self.decision = min(self.eager_ms) < float(m.config.graph_min_step_ms)
+                best = min(self.eager_ms)
+                if best < float(m.config.graph_min_step_ms):
+                    self.decision = True
+                elif best < float(getattr(m.config, "graph_trial_max_ms", 30.0)):
+                    self.decision = "trial"
+                else:
+                    self.decision = False
             return
         if self.graph is None:
             torch.cuda.synchronize()
@@ -97,8 +108,24 @@ class StepGraph:
                 ex.update(m.optimizer)
                 return
             self.graph = g
+        timed = self.decision == "trial" and self.trial >= 1  # the first replay pays first-use costs
+        if timed:
+            torch.cuda.synchronize()
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
         self.graph.replay()
         ex.update(m.optimizer)
+        if self.decision == "trial":
+            self.trial += 1
+            if timed:
+                en.record()
+                en.synchronize()
+                self.graph_ms.append(st.elapsed_time(en))
+            if len(self.graph_ms) >= 2:
+                keep = min(self.graph_ms) < 0.98 * min(self.eager_ms)
+                self.decision = keep
+                if not keep:
+                    self.graph = None  # releases the graph's memory pool
 
 
 def run_train_step(model):

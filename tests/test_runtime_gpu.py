@@ -119,3 +119,37 @@ def test_sparse_embedding_sgd_matches_dense_gpu(monkeypatch):
     assert n1 > 0 and n0 == 0
     for k, (x, y) in enumerate(zip(a, b)):
         np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-6, err_msg=str(k))
+
+
+def test_graph_trial_policy_matches_eager():
+    """'auto' hipGraph policy for mid-length steps: capture on trial, time two replays, keep the
+    graph only if it beats the eager step. Whatever it decides, the weights after 8 steps match an
+    eager run, and the trial ends in a definite decision."""
+    from flexflow_amd.core import FFConfig, FFModel, SGDOptimizer
+    from flexflow_amd.models import build
+
+    def run(flags, trial):
+        cfg = FFConfig(["--dtype", "bf16"] + flags)
+        if trial:
+            cfg.graph_min_step_ms, cfg.graph_trial_max_ms = 0.0, 1e9  # every step length is a trial
+        cfg.batch_size = 64
+        ff = FFModel(cfg)
+        inputs, out, loss, mets, make_batch = build("dlrm", ff, 64, small=True)
+        ff.optimizer = SGDOptimizer(ff, 0.05)
+        ff.compile(loss_type=loss, metrics=mets)
+        rng = np.random.default_rng(0)
+        for _ in range(8):
+            arrs, lab = make_batch(rng)
+            for t, a in zip(inputs, arrs):
+                t.set_tensor(ff, a)
+            ff.label_tensor.set_tensor(ff, lab)
+            ff.train_step()
+        return ff, [np.asarray(w.get_weights(ff)) for L in ff.layers for w in L.weights]
+
+    ff, a = run([], True)
+    sg = ff._step_graph
+    assert sg.decision in (True, False) and len(sg.graph_ms) == 2, (sg.decision, sg.graph_ms)
+    assert (sg.graph is not None) == sg.decision
+    _, b = run(["--no-hip-graphs"], False)
+    for k, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5, err_msg=str(k))
