@@ -189,6 +189,8 @@ def main():
                         "parallelism": describe(ff, world), "search": (ff.search_report or {}).get("algo"),
                         "optimizer": args.optimizer, "params": info["params"]}, **info["extra"]),
     }
+    sg = getattr(ff, "_step_graph", None)
+    res["hip_graph"] = bool(sg is not None and sg.graph is not None)  # step replayed from a hipGraph
     if info["flops_per_sample"]:
         res["model_tflops_per_gpu"] = round(info["flops_per_sample"] * sps / world / 1e12, 2)
     rep = ff.search_report or {}

@@ -359,9 +359,20 @@ __global__ void col_reduce_add_kernel(const float* __restrict__ part, Outs3 o, i
   const int rl = threadIdx.x >> 6;
   const int per = (R + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
-  float s = 0.f;
-  if (c < C)
-    for (int r = r0 + rl; r < r1; r += 4) s += p[(int64_t)r * C + c];
+  // four independent partial sums: the row loads of an unrolled iteration are all in flight
+  // together (one dependent load per iteration left the ~100 launches per BERT step latency-bound)
+  float s = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < C) {
+    int r = r0 + rl;
+    for (; r + 12 < r1; r += 16) {
+      s += p[(int64_t)r * C + c];
+      s1 += p[(int64_t)(r + 4) * C + c];
+      s2 += p[(int64_t)(r + 8) * C + c];
+      s3 += p[(int64_t)(r + 12) * C + c];
+    }
+    for (; r < r1; r += 4) s += p[(int64_t)r * C + c];
+  }
+  s = (s + s1) + (s2 + s3);
   red[rl][threadIdx.x & 63] = s;
   __syncthreads();
   if (rl == 0 && c < C) {
