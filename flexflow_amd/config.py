@@ -92,6 +92,8 @@ class FFConfig:
         self.dist_timeout_s = 1800.0  # --dist-timeout S: torch.distributed collective timeout
         self.iter_config_seq_length = -1
         self._traces: dict = {}
+        self._trace_active = None  # begin_trace / end_trace -> hipGraphs (runtime/trace.py)
+        self._trace_state: dict = {}
 
         self._discover_machine()
         if argv is None:
@@ -281,10 +283,16 @@ class FFConfig:
         return time.perf_counter() * 1e6
 
     def begin_trace(self, trace_id: int):
+        """Start of a traced iteration body: repeated bodies are captured into a hipGraph and
+        replayed (runtime/trace.py), the counterpart of the reference's Legion tracing."""
+        from .runtime import trace
         self._traces[trace_id] = True
+        trace.begin(self, trace_id)
 
     def end_trace(self, trace_id: int):
+        from .runtime import trace
         self._traces.pop(trace_id, None)
+        trace.end(self, trace_id)
 
     def get_batch_size(self):
         return self.batch_size

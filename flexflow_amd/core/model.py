@@ -520,17 +520,31 @@ class FFModel:
     def forward(self, seq_length=None):
         if seq_length is not None:
             self.iter_config_seq_length = seq_length
-        self.executor.forward()
+        from ..runtime.trace import traced_call
+        traced_call(self, "forward", self._eager_forward)
         self._metrics_pending = True
 
     def zero_gradients(self):
-        self.executor.zero_gradients()
+        from ..runtime.trace import traced_call
+        traced_call(self, "zero_gradients", self._eager_zero_gradients)
 
     def backward(self, seq_length=None):
-        self.executor.backward()  # loss gradient + metrics of the last forward
+        from ..runtime.trace import traced_call
+        traced_call(self, "backward", self._eager_backward)  # loss gradient + metrics of the last forward
         self._metrics_pending = False
 
+    def _eager_forward(self):
+        self.executor.forward()
+
+    def _eager_zero_gradients(self):
+        self.executor.zero_gradients()
+
+    def _eager_backward(self):
+        self.executor.backward()
+
     def update(self):
+        from ..runtime.trace import note_update
+        note_update(self)
         self.executor.update(self.optimizer)
 
     def compute_metrics(self):

@@ -575,8 +575,9 @@ class Executor:
         its slice of the fused optimizer runs now on a side stream while the backward continues.
         A bucket completes only after the backward of every op using its weights was issued (the
         executor marks a weight ready after its last user), so no later backward op reads the
-        weights this overwrites. Memory-bound Adam beside compute-bound GEMMs: the ~2 ms single
-        pass of BERT-Large mostly disappears from the step."""
+        weights this overwrites. Memory-bound Adam beside compute-bound GEMMs: on BERT-Large about
+        half of the ~2.5 ms pass overlaps the backward (step profile: busy exceeds span by
+        ~1.3 ms, profiles/bert_large_b32_r3_w4_steps.txt); same-box A/B -0.2 ms/step."""
         if not self._overlap_active or b.get("sharded"):
             return
         if handle is not None and dist.get_backend(self.comm.group(b["group"])) != "nccl":

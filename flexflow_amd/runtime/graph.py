@@ -25,6 +25,19 @@ import os
 import torch
 
 
+def capturable(model) -> bool:
+    """Whether the model's iteration can be captured into a hipGraph at all (shared by the
+    train_step graph below and begin_trace / end_trace, runtime/trace.py)."""
+    ex = model.executor
+    if getattr(ex, "zero", False) or ex.hooks:
+        return False
+    if not (model.config.hip_graphs and torch.cuda.is_available() and ex.device.type == "cuda"):
+        return False
+    if ex.comm.distributed and os.environ.get("FF_GRAPH_COLLECTIVES", "0") != "1":
+        return False
+    return True
+
+
 class StepGraph:
     def __init__(self, model):
         self.model = model

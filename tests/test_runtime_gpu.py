@@ -153,3 +153,41 @@ def test_graph_trial_policy_matches_eager():
     _, b = run(["--no-hip-graphs"], False)
     for k, (x, y) in enumerate(zip(a, b)):
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5, err_msg=str(k))
+
+
+def test_begin_end_trace_replays_hipgraph():
+    """FFConfig.begin_trace / end_trace (reference: Legion tracing): from the third iteration the
+    recorded forward / zero_gradients / backward sequence replays as one hipGraph; weights after 6
+    iterations match an untraced eager run."""
+    from flexflow_amd.core import FFConfig, FFModel, SGDOptimizer
+    from flexflow_amd.models import build
+
+    def run(trace):
+        cfg = FFConfig(["--dtype", "bf16"] + ([] if trace else ["--no-hip-graphs"]))
+        cfg.batch_size = 64
+        ff = FFModel(cfg)
+        inputs, out, loss, mets, make_batch = build("dlrm", ff, 64, small=True)
+        ff.optimizer = SGDOptimizer(ff, 0.05)
+        ff.compile(loss_type=loss, metrics=mets)
+        rng = np.random.default_rng(0)
+        for _ in range(6):
+            arrs, lab = make_batch(rng)
+            for t, a in zip(inputs, arrs):
+                t.set_tensor(ff, a)
+            ff.label_tensor.set_tensor(ff, lab)
+            if trace:
+                cfg.begin_trace(111)
+            ff.forward()
+            ff.zero_gradients()
+            ff.backward()
+            ff.update()
+            if trace:
+                cfg.end_trace(111)
+        return cfg, [np.asarray(w.get_weights(ff)) for L in ff.layers for w in L.weights]
+
+    cfg, a = run(True)
+    st = cfg._trace_state[111]
+    assert st.graph is not None and not st.off and st.seq == ["forward", "zero_gradients", "backward"]
+    _, b = run(False)
+    for k, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5, err_msg=str(k))
