@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one GEMM configuration repeatedly (for rocprofv3 --pmc / kernel-trace of a single kernel).
 
-usage: gemm_probe.py M N K a_k b_k [impl=k256|big|128|lib] [reps=20] [out=bf16|f32]
+usage: gemm_probe.py M N K a_k b_k [impl=w4|k256|big|128|lib] [reps=20] [out=bf16|f32]
 """
 import sys
 import torch
@@ -21,7 +21,7 @@ C = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if out == "bf16" else tor
 lda = K if a_k else M
 ldb = K if b_k else N
 X = Kn.ext()
-IMP = {"k256": 2, "big": 1, "128": 0}.get(impl, 2)
+IMP = {"w4": 3, "k256": 2, "big": 1, "128": 0}.get(impl, 2)
 splitk = X.gemm_pick_splitk(M, N, K, 1, IMP)
 ws = torch.empty(M * N * splitk, device=dev) if splitk > 1 else None
 for _ in range(reps):
