@@ -115,6 +115,14 @@ __device__ __forceinline__ float binary_f(int op, float a, float b) {
   }
 }
 
+// op | B_RELU: the consumer ReLU fused into the binary op (executor._plan_binary_relu: ResNet's
+// residual add + ReLU in one pass instead of two)
+constexpr int B_RELU = 0x100;
+__device__ __forceinline__ float binary_act(int op, float a, float b) {
+  const float r = binary_f(op & 0xff, a, b);
+  return (op & B_RELU) ? fmaxf(r, 0.f) : r;
+}
+
 // Same-shape fast path.
 template <typename T>
 __global__ void binary_same_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ c,
@@ -127,11 +135,11 @@ __global__ void binary_same_kernel(const T* __restrict__ a, const T* __restrict_
     load16(a + i * V, av);
     load16(b + i * V, bv);
 #pragma unroll
-    for (int j = 0; j < V; ++j) av[j] = binary_f(op, av[j], bv[j]);
+    for (int j = 0; j < V; ++j) av[j] = binary_act(op, av[j], bv[j]);
     store16(c + i * V, av);
   }
   for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    c[i] = Cvt<T>::from_f(binary_f(op, Cvt<T>::to_f(a[i]), Cvt<T>::to_f(b[i])));
+    c[i] = Cvt<T>::from_f(binary_act(op, Cvt<T>::to_f(a[i]), Cvt<T>::to_f(b[i])));
 }
 
 // General broadcast path: output shape `shape` (ndim <= 6), strides of a/b in elements
@@ -154,7 +162,7 @@ __global__ void binary_bcast_kernel(const T* __restrict__ a, const T* __restrict
       oa += idx * d.sa[k];
       ob += idx * d.sb[k];
     }
-    c[i] = Cvt<T>::from_f(binary_f(op, Cvt<T>::to_f(a[oa]), Cvt<T>::to_f(b[ob])));
+    c[i] = Cvt<T>::from_f(binary_act(op, Cvt<T>::to_f(a[oa]), Cvt<T>::to_f(b[ob])));
   }
 }
 

@@ -451,6 +451,7 @@ class FFModel:
         self.executor.init_weights(cfg.seed)
         if os.environ.get("FF_NO_INPLACE") != "1":
             self.executor._plan_inplace()
+            self.executor._plan_binary_relu()
         self.executor._plan_bias_grad_fusion()
         self.executor._plan_dact_fusion()
         if self.optimizer is not None and training:

@@ -844,7 +844,8 @@ def _bcast_desc(a, b, out_shape):
     return list(out_shape), strides(a), strides(b)
 
 
-def binary_fwd(name, a, b):
+def binary_fwd(name, a, b, relu=False):
+    """c = a (op) b, optionally followed by ReLU in the same pass (relu=True)."""
     out_shape = torch.broadcast_shapes(a.shape, b.shape)
     if native(a) and a.dtype in (torch.bfloat16, torch.float32) and len(out_shape) <= 6:
         if b.dtype != a.dtype:
@@ -857,11 +858,13 @@ def binary_fwd(name, a, b):
         else:
             c = torch.empty(out_shape, device=a.device, dtype=a.dtype)
         shp, sa, sb = _bcast_desc(a, b, out_shape)
-        ext().binary_fwd(a, b, c, B[name], shp, sa, sb, same)
+        ext().binary_fwd(a, b, c, B[name] | (0x100 if relu else 0), shp, sa, sb, same)
         return c
     af, bf = a.float(), b.float()
     r = {"add": af + bf, "sub": af - bf, "mul": af * bf, "div": af / bf, "max": torch.maximum(af, bf),
          "min": torch.minimum(af, bf)}[name]
+    if relu:
+        r = torch.relu(r)
     return r.to(a.dtype)
 
 

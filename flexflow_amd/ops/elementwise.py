@@ -46,6 +46,13 @@ class ElementUnary(OpImpl):
         x = xs[0]
         if self.fn == "identity":
             return [x]
+        if ctx.extra.get("fused_into_producer"):
+            # the producing binary op already applied this ReLU (executor._plan_binary_relu); the
+            # gradient needs the output only
+            if ctx.training:
+                ctx.saved["x"] = x
+                ctx.saved["y"] = x
+            return [x]
         if ctx.extra.get("inplace") and x.is_contiguous():
             y = K.unary_fwd(self.fn, x, self.scalar, out=x)
             if ctx.training:
@@ -105,7 +112,7 @@ class ElementBinary(OpImpl):
 
     def forward(self, ctx, xs, ws):
         a, b = xs
-        c = K.binary_fwd(self.fn, a, b)
+        c = K.binary_fwd(self.fn, a, b, relu=bool(ctx.extra.get("fused_relu")))
         if ctx.training:
             ctx.saved["a"], ctx.saved["b"] = a, b
         return [c]

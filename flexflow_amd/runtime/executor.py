@@ -29,6 +29,9 @@ from ..parallel.comm import Communicator, GradBucketer, Transfer
 from ..parallel.layout import Layout, rel_slices
 from ..pcg.strategy import OpConfig, op_layouts
 from ..type import DataType, LossType, MetricsType, OperatorType
+from ..ops.elementwise import BINARY as _BINARY
+
+BINARY_OPS = frozenset(_BINARY.keys())
 
 
 class WeightArena:
@@ -744,6 +747,29 @@ class Executor:
             if self.fwd_tx[(L.name, 0)].kind != "identity" or t.data_type != L.outputs[0].data_type:
                 continue
             self.ctx[L.name].extra["inplace"] = True
+            n += 1
+        return n
+
+    def _plan_binary_relu(self):
+        """A ReLU whose input is the output of an element-wise binary op (ResNet's residual add)
+        and nothing else reads (the in-place conditions of _plan_inplace) is applied inside that
+        op's kernel: one pass over the activation instead of two. The ReLU's backward is unchanged
+        (it needs only the output)."""
+        if os.environ.get("FF_NO_BINARY_RELU") == "1":
+            return 0
+        prod = {}
+        for L in self.layers:
+            for o in L.outputs:
+                prod[o.guid] = L
+        n = 0
+        for L in self.layers:
+            if L.op_type != OperatorType.OP_RELU or not self.ctx[L.name].extra.get("inplace"):
+                continue
+            P = prod.get(L.inputs[0].guid)
+            if P is None or P.op_type not in BINARY_OPS or not self.local.get(P.name):
+                continue
+            self.ctx[P.name].extra["fused_relu"] = True
+            self.ctx[L.name].extra["fused_into_producer"] = True
             n += 1
         return n
 
