@@ -20,6 +20,7 @@ CASES = [
                                      "--num_layers", "2", "--iterations", "2", "--train"]),
     ("native/print_layers.py", []),
     ("native/alexnet.py", ["-b", "4", "--iterations", "1", "--small"]),
+    ("native/resnet.py", ["-b", "4", "--iterations", "2", "--small"]),
     ("native/dlrm.py", ["-b", "16", "--iterations", "2", "--small"]),
     ("native/transformer.py", ["-b", "2", "--iterations", "1", "--small"]),
     ("native/mixture_of_experts.py", ["-b", "16", "--iterations", "2", "--small"]),
