@@ -25,6 +25,11 @@ CASES = [
     ("native/transformer.py", ["-b", "2", "--iterations", "1", "--small"]),
     ("native/mixture_of_experts.py", ["-b", "16", "--iterations", "2", "--small"]),
     ("native/nmt.py", ["-b", "8", "--iterations", "2", "--small"]),
+    ("native/inception.py", ["-b", "2", "--iterations", "1", "--small"]),
+    ("native/resnext50.py", ["-b", "2", "--iterations", "1", "--small"]),
+    ("native/xdl.py", ["-b", "16", "--iterations", "2", "--small"]),
+    ("native/candle_uno.py", ["-b", "8", "--iterations", "2", "--small"]),
+    ("native/mlp_unify.py", ["-b", "16", "--iterations", "2", "--small"]),
     ("native/tensor_attach.py", []),
     ("native/print_input.py", ["-b", "4"]),
     ("native/print_weight.py", ["-b", "16"]),
