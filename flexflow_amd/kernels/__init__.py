@@ -77,6 +77,63 @@ IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []
 
+# Persistent autotune cache (FF_TUNE_CACHE=<file.json>): the GEMM and convolution choices of a run
+# are written at exit (rank 0, atomic rename, merged with what the file held) and read back by the
+# next run, whose first step then skips the timing. Only named choices persist; the direct
+# hipBLASLt plans ("lt" tuples) hold process-local handles and are re-timed.
+_TUNE_CACHE = _os.environ.get("FF_TUNE_CACHE", "")
+_cached: dict = {"gemm": {}, "conv": {}}
+
+
+def _ckey(key) -> str:
+    return repr(tuple(str(k) if isinstance(k, torch.dtype) else k for k in key))
+
+
+def tune_cache_load(path: str) -> int:
+    """Read a tune cache file; returns the number of choices loaded (0 if the file is absent)."""
+    import json
+    if not path or not _os.path.exists(path):
+        return 0
+    with open(path) as f:
+        d = json.load(f)
+    n = 0
+    for kind in ("gemm", "conv"):
+        for k, v in d.get(kind, {}).items():
+            if isinstance(v, str):
+                _cached[kind][k] = v
+                n += 1
+    return n
+
+
+def tune_cache_save(path: str) -> int:
+    """Write the named choices tuned so far (plus those already cached) to `path`."""
+    import json
+    out = {"gemm": dict(_cached["gemm"]), "conv": dict(_cached["conv"])}
+    for k, v in _tuned.items():
+        if isinstance(v, str):
+            out["gemm"][_ckey(k)] = v
+    for k, v in _conv_tuned.items():
+        if isinstance(v, str):
+            out["conv"][_ckey(k)] = v
+    tmp = f"{path}.tmp{_os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    _os.replace(tmp, path)
+    return len(out["gemm"]) + len(out["conv"])
+
+
+def _tune_cache_lookup(kind, key):
+    if not _TUNE_CACHE:
+        return None
+    return _cached[kind].get(_ckey(key))
+
+
+if _TUNE_CACHE:
+    import atexit as _atexit
+    tune_cache_load(_TUNE_CACHE)
+    if _os.environ.get("RANK", "0") == "0":
+        _atexit.register(lambda: (_tuned or _conv_tuned) and tune_cache_save(_TUNE_CACHE))
+
 
 def _views(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, batch, sA, sB, sC):
     Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)
@@ -362,6 +419,10 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                beta != 0.0, splitk)
         choice = _tuned.get(key)
         if choice is None:
+            choice = _tune_cache_lookup("gemm", key)
+            if choice is not None:
+                _tuned[key] = choice
+        if choice is None:
             plain = act == ACT_NONE and Z is None and sC in (0, M * N) and ldc == N
             if not _TUNE or torch.cuda.is_current_stream_capturing():
                 choice = IMPL_DEFAULT
@@ -454,6 +515,10 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
 
     key = ("dact", M, N, K, a_k, b_k, lda, ldb, ldc, act, db is not None)
     choice = _tuned.get(key)
+    if choice is None:
+        choice = _tune_cache_lookup("gemm", key)
+        if choice is not None:
+            _tuned[key] = choice
     if choice is None:
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             choice = "fused"
@@ -1274,6 +1339,10 @@ def _conv_pick(kind, key, cands):
     if _CONV_IMPL in ("ours", "lib"):
         return _CONV_IMPL
     choice = _conv_tuned.get((kind, key))
+    if choice is None:
+        choice = _tune_cache_lookup("conv", (kind, key))
+        if choice is not None:
+            _conv_tuned[(kind, key)] = choice
     if choice is None:
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             return "ours"

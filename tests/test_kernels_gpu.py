@@ -740,3 +740,28 @@ def test_elementwise_channel_last():
     # a channel slice of a channel-last tensor (a concat's backward split) stays channel-last
     part = K.dense(a[:, 8:16])
     assert K.is_nhwc(part) and torch.equal(part, a[:, 8:16])
+
+
+def test_tune_cache_skips_timing(tmp_path, monkeypatch):
+    """A GEMM call site tuned in one run is dispatched from FF_TUNE_CACHE in the next, without timing."""
+    from flexflow_amd import kernels as K
+    path = str(tmp_path / "tune.json")
+    M, N, Kd = 512, 768, 1024
+    A = torch.randn(M, Kd, device=DEV).bfloat16()
+    B = torch.randn(N, Kd, device=DEV).bfloat16()
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    monkeypatch.setattr(K, "_tuned", {})
+    monkeypatch.setattr(K, "_cached", {"gemm": {}, "conv": {}})
+    K.gemm(A, B, C, M, N, Kd, True, True, Kd, Kd, N)
+    first = next(iter(K._tuned.values()))
+    n_log = len(K.TUNE_LOG)
+    K.tune_cache_save(path)
+    monkeypatch.setattr(K, "_tuned", {})
+    monkeypatch.setattr(K, "_TUNE_CACHE", path)
+    K.tune_cache_load(path)
+    C2 = torch.empty_like(C)
+    K.gemm(A, B, C2, M, N, Kd, True, True, Kd, Kd, N)
+    torch.cuda.synchronize()
+    if isinstance(first, str):  # a named choice persists: the second run takes it without timing
+        assert len(K.TUNE_LOG) == n_log and next(iter(K._tuned.values())) == first
+    assert _rel(C2, A.float() @ B.float().t()) < 1e-2
