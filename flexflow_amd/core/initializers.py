@@ -82,3 +82,22 @@ def default_initializer(weight_name: str, seed: int) -> Initializer:
     if weight_name in ("gamma", "scale"):
         return ConstantInitializer(1.0)
     return GlorotUniformInitializer(seed)
+
+
+class BlockInitializer(Initializer):
+    """Initializer of a weight that a graph rewrite built by stacking other weights along axis 0
+    (pcg/joint.py MergeSiblings). Each row block is filled exactly as its original weight would
+    have been (its own initializer, fans and seed), so a rewritten graph starts from the same
+    values as the graph the user wrote. `parts` = [(original Parameter, first row, rows)];
+    `resolve(param) -> Initializer` supplies the default initializer of an original weight."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+        self.resolve = None
+
+    def fill_full(self, t, shape):
+        for w, start, size in self.parts:
+            init = self.resolve(w) if self.resolve is not None else w.initializer
+            blk = torch.empty(tuple(w.dims), dtype=t.dtype, device=t.device)
+            init.fill_full(blk, tuple(w.dims))
+            t[start:start + size].copy_(blk)

@@ -465,6 +465,10 @@ class FFModel:
             for guid, v in self._pending_weights.items():
                 if guid in by_guid:
                     self.executor.set_weight(by_guid[guid], v)
+                else:  # a weight a graph rewrite stacked into a larger one
+                    tgt = self._resolve_weight_alias(guid)
+                    if tgt is not None:
+                        self._set_weight_block(tgt, v)
         for L in self.layers:
             for t in L.outputs:
                 if t._attached is not None:
@@ -696,16 +700,45 @@ class FFModel:
 
     def _get_tensor_grad(self, t):
         if isinstance(t, Parameter):
+            tgt = self._resolve_weight_alias(t.guid)
+            if tgt is not None:
+                lw, start, rows = tgt
+                return self.executor.get_weight_grad(lw).detach().cpu().numpy()[start:start + rows].copy()
             return self.executor.get_weight_grad(t).detach().cpu().numpy().copy()
         raise NotImplementedError("activation gradients are not retained")
+
+    def _resolve_weight_alias(self, guid):
+        """(live weight, first row, rows) holding the original weight `guid` after graph rewrites
+        that stacked it into a larger weight (pcg/joint.py MergeSiblings), or None."""
+        alias = getattr(self, "_weight_alias", None) or {}
+        if guid not in alias:
+            return None
+        w, start, rows = alias[guid]
+        while w.guid in alias:  # merged again: offset into the outer stack
+            w2, s2, _ = alias[w.guid]
+            w, start = w2, s2 + start
+        return w, start, rows
+
+    def _set_weight_block(self, tgt, arr):
+        w, start, rows = tgt
+        full = self.executor.get_weight(w).float().detach().cpu().numpy().copy()
+        full[start:start + rows] = np.asarray(arr, dtype=np.float32).reshape(full[start:start + rows].shape)
+        self.executor.set_weight(w, full)
 
     def _set_weight_value(self, w, arr):
         if not self._compiled:
             self._pending_weights[w.guid] = np.asarray(arr)
             return
+        tgt = self._resolve_weight_alias(w.guid)
+        if tgt is not None:
+            return self._set_weight_block(tgt, arr)
         self.executor.set_weight(w, np.asarray(arr))
 
     def _get_weight_value(self, w):
+        tgt = self._resolve_weight_alias(w.guid)
+        if tgt is not None:
+            lw, start, rows = tgt
+            return self.executor.get_weight(lw).float().detach().cpu().numpy()[start:start + rows].copy()
         return self.executor.get_weight(w).float().detach().cpu().numpy().copy()
 
     @property

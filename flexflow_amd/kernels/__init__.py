@@ -83,6 +83,28 @@ TUNE_LOG: list = []
 # hipBLASLt plans ("lt" tuples) hold process-local handles and are re-timed.
 _TUNE_CACHE = _os.environ.get("FF_TUNE_CACHE", "")
 _cached: dict = {"gemm": {}, "conv": {}}
+# call sites whose choice came from a timing (or from the cache): only these are persisted. A choice
+# made without timing (FF_GEMM_TUNE=0, first call inside graph capture) is a default, and saving
+# it would stop every later run from timing that call site.
+_timed: set = set()
+
+
+def tune_cache_stamp() -> dict:
+    """What a cache file is valid for: the device and the kernel build. A file written on another
+    GPU model or by another build of _C.so is ignored (its timings do not transfer)."""
+    dev = "cpu"
+    if torch.cuda.is_available():
+        pr = torch.cuda.get_device_properties(0)
+        dev = f"{pr.name}|{getattr(pr, 'gcnArchName', '')}|{pr.multi_processor_count}"
+    so = _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "flexflow_amd", "_C.so")
+    build = "none"
+    if _os.path.exists(so):
+        import hashlib
+        h = hashlib.sha1()
+        with open(so, "rb") as f:
+            h.update(f.read())
+        build = h.hexdigest()[:16]
+    return {"device": dev, "build": build}
 
 
 def _ckey(key) -> str:
@@ -96,6 +118,9 @@ def tune_cache_load(path: str) -> int:
         return 0
     with open(path) as f:
         d = json.load(f)
+    stamp = d.get("stamp")
+    if stamp is not None and stamp != tune_cache_stamp():
+        return 0  # another device or kernel build: re-time everything
     n = 0
     for kind in ("gemm", "conv"):
         for k, v in d.get(kind, {}).items():
@@ -108,9 +133,9 @@ def tune_cache_load(path: str) -> int:
 def tune_cache_save(path: str) -> int:
     """Write the named choices tuned so far (plus those already cached) to `path`."""
     import json
-    out = {"gemm": dict(_cached["gemm"]), "conv": dict(_cached["conv"])}
+    out = {"gemm": dict(_cached["gemm"]), "conv": dict(_cached["conv"]), "stamp": tune_cache_stamp()}
     for k, v in _tuned.items():
-        if isinstance(v, str):
+        if isinstance(v, str) and k in _timed:
             out["gemm"][_ckey(k)] = v
     for k, v in _conv_tuned.items():
         if isinstance(v, str):
@@ -422,6 +447,7 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             choice = _tune_cache_lookup("gemm", key)
             if choice is not None:
                 _tuned[key] = choice
+                _timed.add(key)
         if choice is None:
             plain = act == ACT_NONE and Z is None and sC in (0, M * N) and ldc == N
             if not _TUNE or torch.cuda.is_current_stream_capturing():
@@ -459,6 +485,7 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                 choice = min(times, key=lambda k: times[k])
                 TUNE_LOG.append({"M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "batch": batch, "act": act,
                                  "times_ms": {str(k): round(v, 4) for k, v in times.items()}, "choice": str(choice)})
+                _timed.add(key)
             _tuned[key] = choice
         if isinstance(choice, tuple):
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
@@ -519,6 +546,7 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
         choice = _tune_cache_lookup("gemm", key)
         if choice is not None:
             _tuned[key] = choice
+            _timed.add(key)
     if choice is None:
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             choice = "fused"
@@ -533,6 +561,7 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
                 choice = min(times, key=lambda k: times[k])
                 TUNE_LOG.append({"op": "gemm_dact", "M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "act": act,
                                  "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
+                _timed.add(key)
         _tuned[key] = choice
     if choice == "fused" and fused():
         return C

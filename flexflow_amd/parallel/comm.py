@@ -1,4 +1,5 @@
-"""Explicit data movement between sharded layouts over RCCL (torch.distributed 'nccl') or gloo.
+"""Explicit data movement between sharded layouts over RCCL (torch.distributed 'nccl'; the CPU
+multi-rank tests run the same calls on gloo — no backend-specific branches).
 
 This replaces the reference's implicit Legion/Realm DMA between logical-region partitions and its
 parallel-op kernels (src/parallel_ops/{partition,combine,replicate,reduction}.cc,
@@ -129,6 +130,8 @@ def _a2a_dims(S: Layout, D: Layout):
         return None
     a, b = a[0], b[0]
     k = S.degrees[a]
+    if S.shape[a] % k or S.shape[b] % k:  # equal chunks only (chunk + stack in _all_to_all)
+        return None
     for blk in S.blocks():
         if blk[a] != 0:
             continue
@@ -347,14 +350,9 @@ class Transfer:
         out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
         g = comm.group(grp)
         nb = self.bytes_moved(x.element_size())
-        if comm.is_nccl:
-            h = dist.reduce_scatter_tensor(out, inp, group=g, async_op=True)
-            return Pending([h], lambda: out.movedim(0, d).contiguous(), kind="reduce_scatter", nbytes=nb)
-        # gloo: no reduce_scatter; all_reduce then keep own chunk
-        tmp = inp.clone()
-        h = dist.all_reduce(tmp, group=g, async_op=True)
-        return Pending([h], lambda: tmp.chunk(k, 0)[grp.index(r)].movedim(0, d).contiguous(), kind="reduce_scatter",
-                       nbytes=nb)
+        # one code path for every backend: RCCL on the GPU, gloo in the CPU multi-rank tests
+        h = dist.reduce_scatter_tensor(out, inp, group=g, async_op=True)
+        return Pending([h], lambda: out.movedim(0, d).contiguous(), kind="reduce_scatter", nbytes=nb)
 
     def _all_gather(self, comm, x):
         S, D, d, r = self.src, self.dst, self.dim, self.rank
@@ -369,13 +367,9 @@ class Transfer:
         xm = x.movedim(d, 0).contiguous()
         g = comm.group(grp)
         nb = self.bytes_moved(x.element_size())
-        if comm.is_nccl:
-            out = torch.empty((k * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
-            h = dist.all_gather_into_tensor(out, xm, group=g, async_op=True)
-            chunks = list(out.chunk(k, 0))
-        else:
-            chunks = [torch.empty_like(xm) for _ in range(k)]
-            h = dist.all_gather(chunks, xm, group=g, async_op=True)
+        out = torch.empty((k * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
+        h = dist.all_gather_into_tensor(out, xm, group=g, async_op=True)
+        chunks = list(out.chunk(k, 0))
 
         def finish():
             # chunks[i] came from group-rank i == device grp[i]; reorder to dim order

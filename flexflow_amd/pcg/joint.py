@@ -37,11 +37,22 @@ from ..type import ActiMode, OperatorType
 # ----------------------------------------------------------------------------- graph states
 def snapshot(model):
     return (list(model.layers), {id(L): list(L.inputs) for L in model.layers}, model._output,
-            dict(getattr(model, "_tensor_remap", {})), set(getattr(model, "_names", set())))
+            dict(getattr(model, "_tensor_remap", {})), set(getattr(model, "_names", set())),
+            dict(getattr(model, "_weight_alias", {})))
+
+
+def stamp_init_slots(model):
+    """Record each weight's (layer position, slot) in the graph as written: the seed of its default
+    initializer. Rewrites move layers, and a rewritten graph must initialise like the original."""
+    for li, L in enumerate(model.layers):
+        for i, w in enumerate(L.weights):
+            if getattr(w, "_init_slot", None) is None:
+                w._init_slot = (li, i)
 
 
 def restore(model, snap):
-    layers, inputs, out, remap, names = snap
+    layers, inputs, out, remap, names, alias = snap
+    model._weight_alias = dict(alias)
     model.layers = list(layers)
     for L in model.layers:
         L.inputs = list(inputs[id(L)])
@@ -134,22 +145,36 @@ class MergeSiblings:
         if a is None or b is None or not self._ok(a, _users(model), None) or not self._ok(b, _users(model), None) \
                 or a is b or not a.inputs or not b.inputs or a.inputs[0] is not b.inputs[0]:
             return False
+        from ..core.initializers import BlockInitializer
         oa, ob = self._out_attr(), None
         attrs = dict(a.attrs)
         attrs[oa] = int(a.attrs[oa]) + int(b.attrs[oa])
-        if a.attrs.get("kernel_init") is not b.attrs.get("kernel_init"):
-            attrs["kernel_init"] = None
-        if a.attrs.get("bias_init") is not b.attrs.get("bias_init"):
-            attrs["bias_init"] = None
         name = f"{a.name}&{b.name}"
         M = Layer(model, self.op_type, name, [a.inputs[0]], attrs)
         M.__class__ = op_class(self.op_type)
+        if len(M.weights) != len(a.weights) or len(M.weights) != len(b.weights):
+            return False
+        # every weight of the merged op is the row-stack of the two originals: each block keeps its
+        # original initializer / seed, and values set on the original Parameters (before or after
+        # compile) are redirected into the block (FFModel._weight_alias)
+        na, nb = int(a.attrs[oa]), int(b.attrs[oa])
+        for wm, wa, wb in zip(M.weights, a.weights, b.weights):
+            if wm.dims[0] != na + nb or tuple(wa.dims[1:]) != tuple(wm.dims[1:]) \
+                    or tuple(wb.dims[1:]) != tuple(wm.dims[1:]):
+                return False
+            wm.initializer = BlockInitializer([(wa, 0, na), (wb, na, nb)])
         axis = -1 if self.op_type == OperatorType.OP_LINEAR else 1
         S = Layer(model, OperatorType.OP_SPLIT, f"split[{name}]", [M.outputs[0]],
                   {"sizes": [int(a.attrs[oa]), int(b.attrs[oa])], "axis": axis})
         S.__class__ = op_class(OperatorType.OP_SPLIT)
         if tuple(S.outputs[0].dims) != tuple(a.outputs[0].dims) or tuple(S.outputs[1].dims) != tuple(b.outputs[0].dims):
             return False
+        alias = getattr(model, "_weight_alias", None)
+        if alias is None:
+            alias = model._weight_alias = {}
+        for wm, wa, wb in zip(M.weights, a.weights, b.weights):
+            alias[wa.guid] = (wm, 0, na)
+            alias[wb.guid] = (wm, na, nb)
         _replace(model, [a, b], [M, S], {a.outputs[0].guid: S.outputs[0], b.outputs[0].guid: S.outputs[1]})
         return True
 
@@ -286,6 +311,7 @@ def joint_search(model, algo: str = "unity", budget: Optional[int] = None, alpha
     alpha = alpha if alpha is not None else max(1.0, float(cfg.search_alpha or 1.0))
     xfers = build_xfers(model)
     t0 = time.perf_counter()
+    stamp_init_slots(model)
     base = snapshot(model)
     strat0, rep0 = param_search(model, algo)
     best = [rep0["predicted_ms"], [], strat0, rep0]
@@ -343,4 +369,5 @@ def replay_broadcast(model, seq):
     if model._output is None:
         model._output = model.output_tensor()
     xfers = build_xfers(model)
+    stamp_init_slots(model)
     return replay(model, xfers, [(n, _tuple(m)) for n, m in seq])

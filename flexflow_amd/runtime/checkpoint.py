@@ -101,15 +101,29 @@ def load_checkpoint(model, path: str, strict: bool = True):
     with safe_open(fn, framework="pt") as f:
         md = f.metadata() or {}
     if "arenas" not in md:
-        raise ValueError(f"{fn} has no per-entry arena layout (written by an older version); "
-                         "it cannot be mapped onto this job's arenas safely")
+        # written before per-entry layouts were stored: the old whole-arena copy is safe only when
+        # this job's arenas have exactly the sizes the shard holds (same placement and layout)
+        arenas = _arenas(ex)
+        if not all(f"arena{i}.master" in tensors and tensors[f"arena{i}.master"].numel() == ar.size
+                   for i, ar in arenas):
+            raise ValueError(f"{fn} has no per-entry arena layout (written by an older version) and its "
+                             "arena sizes differ from this job's; it cannot be mapped safely")
+        for i, ar in arenas:
+            ar.master.copy_(tensors[f"arena{i}.master"].to(ar.master.device))
+            st = getattr(opt, "state", {}).get(id(ar))
+            for j, t in enumerate(list(st) if isinstance(st, (tuple, list)) else ([st] if st is not None else [])):
+                if f"arena{i}.opt{j}" in tensors:
+                    t.copy_(tensors[f"arena{i}.opt{j}"].to(t.device))
+            if ar.lowp is not None:
+                ar.lowp.copy_(ar.master.to(ar.lowp.dtype))
+        md = None
     # saved weight key -> (arena index, offset, numel, shape)
     saved = {}
-    for a in json.loads(md["arenas"]):
+    for a in (json.loads(md["arenas"]) if md is not None else []):
         for key, off, n, shape in a["entries"]:
             saved[key] = (a["arena"], int(off), int(n), tuple(shape))
     wkeys = _weight_keys(model)
-    for i, ar in _arenas(ex):
+    for i, ar in (_arenas(ex) if md is not None else []):
         ar.master.zero_()
         st = getattr(opt, "state", {}).get(id(ar))
         st = list(st) if isinstance(st, (tuple, list)) else ([st] if st is not None else [])

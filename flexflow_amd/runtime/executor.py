@@ -294,7 +294,19 @@ class Executor:
     def init_weights(self, seed_base: int, only=None):
         """Deterministic global init, each rank keeping its shard (only: re-initialise just these
         layers, the reference's Op.init)."""
-        from ..core.initializers import default_initializer
+        from ..core.initializers import BlockInitializer, default_initializer
+
+        def resolve(w, li=None, i=None):
+            # model-local seed (layer position, weight slot): identical in every process and
+            # independent of how many models were built before. Graph rewrites stamp the slot of
+            # the graph as written (w._init_slot) so that rewritten graphs initialise identically.
+            slot = getattr(w, "_init_slot", None) or (li, i)
+            init = w.initializer or default_initializer(getattr(w, "short_name", w.name),
+                                                        seed_base + 1009 * slot[0] + slot[1])
+            if isinstance(init, BlockInitializer):
+                init.resolve = resolve
+            return init
+
         done = set()
         for li, L in enumerate(self.layers):
             if only is not None and L not in only:
@@ -305,10 +317,7 @@ class Executor:
                 done.add(w.guid)
                 ar, idx = self.weight_loc[w.guid]
                 m, _, c = ar.views(idx)
-                # model-local seed (layer position, weight slot): identical in every process and
-                # independent of how many models were built before
-                init = w.initializer or default_initializer(getattr(w, "short_name", w.name),
-                                                            seed_base + 1009 * li + i)
+                init = resolve(w, li, i)
                 full = torch.empty(w.dims, dtype=torch.float32, device=self.device)
                 init.fill_full(full, w.dims)
                 wl = self.weight_layout[w.guid]

@@ -4,10 +4,12 @@
 A BERT-Large step is ~1.5k kernel launches; eager Python dispatch would dominate the GPU time.
 After three eager warm-up steps (so every buffer of the torch caching allocator exists), the
 zero-grad + forward + backward of one step is captured once into a hipGraph and replayed; the
-optimizer update (one fused kernel per arena, with host-side bias-corrected scalars) and the
-bucket all-reduces that belong to it run after the replay. Multi-rank steps with in-step
-collectives are captured too when FF_GRAPH_COLLECTIVES=1 (RCCL supports stream capture);
-otherwise they run eagerly with backward-overlapped bucketed all-reduce.
+optimizer update (one fused kernel per arena, with host-side bias-corrected scalars) runs after
+the replay. Multi-rank steps are captured too (RCCL supports stream capture): the activation
+collectives and the bucketed gradient all-reduces are part of the graph, joined back into the
+captured stream before it ends; the timing decision below is agreed over all ranks.
+FF_GRAPH_COLLECTIVES=0 keeps multi-rank steps eager (backward-overlapped bucketed all-reduce),
+and a capture error falls back to eager loudly.
 
 Policy (config.hip_graphs = "auto", the default): the eager warm-up steps are timed; a step whose
 GPU work is long (>= config.graph_min_step_ms, e.g. BERT-Large: 55 ms) keeps running eagerly —
@@ -25,17 +27,39 @@ import os
 import torch
 
 
+def _collectives_capturable(ex, default: str) -> bool:
+    """Multi-rank steps: RCCL collectives can be captured (RCCL supports stream capture); gloo
+    (the CPU multi-rank tests) cannot. FF_GRAPH_COLLECTIVES=0 keeps every multi-rank step eager."""
+    if not ex.comm.distributed:
+        return True
+    if os.environ.get("FF_GRAPH_COLLECTIVES", default) != "1":
+        return False
+    return ex.comm.is_nccl
+
+
 def capturable(model) -> bool:
     """Whether the model's iteration can be captured into a hipGraph at all (shared by the
-    train_step graph below and begin_trace / end_trace, runtime/trace.py)."""
+    train_step graph below and begin_trace / end_trace, runtime/trace.py). A trace body ends at a
+    backward() whose bucket all-reduces are waited for by the later update(): at N > 1 it is
+    captured only on request (FF_GRAPH_COLLECTIVES=1); the train_step graph joins them itself."""
     ex = model.executor
     if getattr(ex, "zero", False) or ex.hooks:
         return False
     if not (model.config.hip_graphs and torch.cuda.is_available() and ex.device.type == "cuda"):
         return False
-    if ex.comm.distributed and os.environ.get("FF_GRAPH_COLLECTIVES", "0") != "1":
-        return False
-    return True
+    return _collectives_capturable(ex, "0")
+
+
+def _agree(ex, value: float, op) -> float:
+    """Every rank takes the same graph decision: the timings are reduced over the world (a rank
+    capturing while another runs its collectives eagerly would leave the two out of step)."""
+    if not ex.comm.distributed:
+        return value
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=ex.device if ex.comm.is_nccl else "cpu")
+    dist.all_reduce(t, op=op)
+    return float(t.item())
 
 
 class StepGraph:
@@ -62,9 +86,9 @@ class StepGraph:
             return False
         if self.failed or ex.hooks:  # per-op hooks time / inspect individual ops: run eagerly
             return False
-        if ex.comm.distributed and os.environ.get("FF_GRAPH_COLLECTIVES", "0") != "1":
-            return False
-        return True
+        # multi-rank: captured by default over RCCL (the bucket all-reduces are joined inside the
+        # graph, see step()); the 'auto' timing decision is agreed over all ranks
+        return _collectives_capturable(ex, "1")
 
     def step(self):
         m = self.model
@@ -93,7 +117,8 @@ class StepGraph:
             if auto and self.warm >= 2:
                 en.record()
                 en.synchronize()
-                ms = st.elapsed_time(en)
+                import torch.distributed as dist
+                ms = _agree(ex, st.elapsed_time(en), dist.ReduceOp.MAX)
                 self.eager_ms.append(ms)
                 best = min(self.eager_ms)
                 if best < float(m.config.graph_min_step_ms):
@@ -111,6 +136,10 @@ class StepGraph:
                     ex.zero_gradients()
                     ex.forward()
                     ex.backward()
+                    if ex.comm.distributed:
+                        # every bucket all-reduce is issued and joined back into the captured
+                        # stream, so update() after a replay finds final gradients and no handle
+                        ex.bucketer.flush()
             except Exception as e:  # fall back to eager, loudly
                 self.failed = True
                 print(f"[flexflow_amd] hipGraph capture failed ({e}); running eagerly", flush=True)
@@ -135,7 +164,8 @@ class StepGraph:
                 en.synchronize()
                 self.graph_ms.append(st.elapsed_time(en))
             if len(self.graph_ms) >= 2:
-                keep = min(self.graph_ms) < 0.98 * min(self.eager_ms)
+                import torch.distributed as dist
+                keep = _agree(ex, float(min(self.graph_ms) < 0.98 * min(self.eager_ms)), dist.ReduceOp.MIN) > 0.5
                 self.decision = keep
                 if not keep:
                     self.graph = None  # releases the graph's memory pool

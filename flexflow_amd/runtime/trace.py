@@ -8,9 +8,11 @@ third captures that sequence (up to the first update(), whose bias-corrected sca
 values) into one hipGraph; from then on the first recorded call of an iteration replays the whole
 graph and the following recorded calls return at once. update(), and any call that departs from
 the recorded sequence, runs eagerly. A trace whose iterations do not repeat, or a model that
-cannot be captured (CPU, ZeRO, per-op hooks, multi-rank without FF_GRAPH_COLLECTIVES=1), runs
-eagerly throughout — the reference's semantics: tracing only ever changes how an iteration is
-issued, not what it computes.
+cannot be captured (CPU, ZeRO, per-op hooks, more than one backward per update, a row-sparse SGD
+plan), runs eagerly throughout — the reference's semantics: tracing only ever changes how an
+iteration is issued, not what it computes. The eager iterations 2 and 3 are timed and the
+train_step graph's policy applies (runtime/graph.py): long bodies stay eager, mid-length ones are
+captured on trial and kept only when two timed replays beat the eager time.
 """
 from __future__ import annotations
 
@@ -29,6 +31,53 @@ class _Trace:
         self.graph = None
         self.pos = 0       # replay: next recorded call of this iteration
         self.off = False
+        # the train_step graph's timing policy (runtime/graph.py): eager iterations are timed, a
+        # long body stays eager, a mid-length one is captured on trial and kept only if faster
+        self.ev = None       # (start event) of the iteration being timed
+        self.eager_ms = []
+        self.graph_ms = []
+        self.decision = None  # True: keep the graph, "trial": replaying while timing it
+        self.replays = 0
+
+
+def _timing_wanted(st) -> bool:
+    return torch.cuda.is_available() and st.model.config.hip_graphs == "auto"
+
+
+def _start_timer(st):
+    torch.cuda.synchronize()
+    st.ev = torch.cuda.Event(enable_timing=True)
+    st.ev.record()
+
+
+def _stop_timer(st):
+    if st.ev is None:
+        return None
+    en = torch.cuda.Event(enable_timing=True)
+    en.record()
+    en.synchronize()
+    ms = st.ev.elapsed_time(en)
+    st.ev = None
+    return ms
+
+
+def _decide(st):
+    """True / "trial" / False from the timed eager iterations (graph.StepGraph's thresholds)."""
+    if not _timing_wanted(st) or not st.eager_ms:
+        return True
+    cfg = st.model.config
+    best = min(st.eager_ms)
+    if best < float(cfg.graph_min_step_ms):
+        return True
+    if best < float(getattr(cfg, "graph_trial_max_ms", 30.0)):
+        return "trial"
+    return False
+
+
+def _replay_bookkeeping(st):
+    """Host-side state the replayed calls would have updated eagerly."""
+    ex = st.model.executor
+    ex._bwd_since_update += sum(1 for n in st.seq if n == "backward")
 
 
 def _state(model):
@@ -52,9 +101,17 @@ def traced_call(model, name: str, run) -> None:
         return
     if st.graph is None:
         st.cur.append(name)
+        if len(st.cur) == 1 and st.iters in (1, 2) and _timing_wanted(st):
+            _start_timer(st)  # eager iterations 2 and 3 are timed (the first pays autotuning)
         if st.iters >= 2 and st.seq and len(st.cur) == 1 and name == st.seq[0]:
             from .graph import capturable
-            if capturable(model):
+            ex = model.executor
+            decision = _decide(st)
+            # one graph per update: the row-sparse SGD plan and several backward passes per update
+            # depend on host bookkeeping a replay would skip
+            if (capturable(model) and decision is not False and st.seq.count("backward") <= 1
+                    and not ex._sparse_plan(model.optimizer)):
+                st.ev = None
                 g = torch.cuda.CUDAGraph()
                 try:
                     torch.cuda.synchronize()
@@ -68,14 +125,22 @@ def traced_call(model, name: str, run) -> None:
                     run()
                     return
                 st.graph = g
+                st.decision = decision
                 g.replay()
+                _replay_bookkeeping(st)
+                st.replays = 1
                 st.pos = 1
                 return
+            st.ev = None
             st.off = True
         run()
         return
     if st.pos == 0 and name == st.seq[0]:
+        if st.decision == "trial" and st.replays >= 1:
+            _start_timer(st)  # the first replay pays first-use costs
         st.graph.replay()
+        _replay_bookkeeping(st)
+        st.replays += 1
         st.pos = 1
         return
     if 0 < st.pos < len(st.seq) and name == st.seq[st.pos]:
@@ -106,6 +171,17 @@ def end(cfg, trace_id) -> None:
     if st is None:
         return
     st.iters += 1
+    ms = _stop_timer(st)
+    if st.graph is not None and st.decision == "trial" and ms is not None:
+        st.graph_ms.append(ms)
+        if len(st.graph_ms) >= 2:
+            if min(st.graph_ms) < 0.98 * min(st.eager_ms):
+                st.decision = True
+            else:  # replay is not faster: eager for good (releases the graph's pool)
+                st.graph, st.off = None, True
+                return
+    elif st.graph is None and ms is not None:
+        st.eager_ms.append(ms)
     if st.graph is None and not st.off:
         if st.prev is not None and st.prev != st.cur:
             st.off = True  # the iteration body changes: no stable sequence to capture

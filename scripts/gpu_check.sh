@@ -23,7 +23,7 @@ for step in "$@"; do
     dtests) run dtests 600 python -u -m pytest tests/test_distributed_gpu.py -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     calib) run calib 600 python -u scripts/calibrate_sim.py bert-large 32 6 ;;
-    gemmprobe) run gemmprobe 400 python -u scripts/gemm_bert_probe.py k256,lib 3 20 ;;
+    gemmprobe) run gemmprobe 400 python -u scripts/gemm_bert_probe.py w4,lib 3 20 ;;
     bench) FF_TUNE_LOG=$OUT/tune.json run bench 600 python bench.py --steps 10 --warmup 3 ;;
     microbench) run microbench 400 python scripts/bench_kernels.py ;;
     prof) cd /tmp && export TMPDIR=/tmp && run prof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-hip-graphs; cd - >/dev/null ;;

@@ -104,6 +104,13 @@ def _strategy(case, ff, world):
         # sample-parallel producer d1; the executor starts it between d2's dgrad and wgrad GEMMs
         return {"x": cfg("x", [world]), "d1": cfg("d1", [world]), "d2": cfg("d2", [1, world]),
                 "d3": cfg("d3", [world]), "sm": cfg("sm", [world])}
+    if case == "siblings_split":
+        # resource split: the two sibling branches run data parallel on DISJOINT halves of the
+        # ranks, the rest of the graph on all of them; every edge between the two placements goes
+        # through the generic point-to-point transfer
+        h = world // 2
+        return {"x": cfg("x", [world]), "da": cfg("da", [h], range(h)), "db": cfg("db", [h], range(h, world)),
+                "sum": cfg("sum", [world]), "head": cfg("head", [world]), "sm": cfg("sm", [world])}
     if case == "mlp2d" and world == 4:
         return {"x": cfg("x", [4]), "d1": cfg("d1", [2, 2]), "d2": cfg("d2", [1, 2, 2]),
                 "d3": cfg("d3", [2, 2], [3, 2, 1, 0]), "sm": cfg("sm", [2], [2, 3])}
@@ -205,10 +212,12 @@ def test_searched_strategy_matches_single(case, world, monkeypatch):
     used = {d for v in search["strategy"].values() for d in v["devices"]}
     print(case, world, "devices used", sorted(used), "rewrites", search["rewrites"],
           {k: search["report"].get(k) for k in ("predicted_ms", "predicted_dp_ms", "graphs_costed")})
-    if case in ("dlrm_small", "inception_small"):
-        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
-    if case in ("dlrm_small", "inception_small"):
-        assert len(used) > 1, used  # the searched plan spreads these models over several ranks
+    if case == "dlrm_small":
+        # not data parallel: some weighted op is split along a non-sample axis (the embedding tables
+        # parameter-parallel), or runs on a strict subset of the ranks
+        non_dp = [k for k, v in search["strategy"].items()
+                  if any(d > 1 for d in v["degrees"][1:]) or len(set(v["devices"])) not in (1, world)]
+        assert non_dp, search["strategy"]
     if case == "siblings":
         # the accepted rewrite changed the graph the strategy is chosen for
         assert any(r["xfer"] == "merge_siblings_linear" for r in search["rewrites"]), search["rewrites"]
@@ -253,3 +262,15 @@ def test_bf16_gradient_comm_matches_single():
     par, _, _ = _run("mlp2d", 2, flags=["--only-data-parallel", "--grad-comm-dtype", "bf16"], strat_case="none")
     ref = _single("mlp2d")
     _compare(par, ref, "bf16-grad-comm", rtol=2e-2, atol=2e-3)
+
+
+def test_resource_split_strategy_matches_single():
+    """World 8: branches on disjoint device groups (the plans the non-sequence split of the DP
+    search produces), exchanged through the generic P2P transfer, match one process."""
+    from flexflow_amd.parallel.comm import Transfer
+    from flexflow_amd.parallel.layout import Layout
+    t = Transfer(Layout((8, 32), (8, 1), 1, tuple(range(8))), Layout((8, 32), (4, 1), 1, (0, 1, 2, 3)), False, 0)
+    assert t.kind == "generic"
+    par, _, _ = _run("siblings", 8, strat_case="siblings_split")
+    ref = _single("siblings")
+    _compare(par, ref, "siblings_split@8")

@@ -63,3 +63,27 @@ def test_trace_records_sequence_and_detects_changes(monkeypatch):
     cfg, _ = _loop(True, changing)
     st = cfg._trace_state[7]
     assert st.off and st.iters == 4 and st.graph is None
+
+
+def test_trace_policy_and_replay_bookkeeping():
+    """The trace graph follows the train_step graph's timing policy, and a replay does the host
+    bookkeeping its eager calls would have done (backward count for the sparse-SGD guard)."""
+    from types import SimpleNamespace
+
+    from flexflow_amd.runtime import trace as T
+    cfg = SimpleNamespace(hip_graphs="auto", graph_min_step_ms=12.0, graph_trial_max_ms=30.0)
+    ex = SimpleNamespace(_bwd_since_update=0)
+    st = T._Trace(SimpleNamespace(config=cfg, executor=ex))
+    st.seq = ["zero_gradients", "forward", "backward"]
+    T._replay_bookkeeping(st)
+    T._replay_bookkeeping(st)
+    assert ex._bwd_since_update == 2
+    if T._timing_wanted(st):  # device: the eager timings decide
+        st.eager_ms = [5.0]
+        assert T._decide(st) is True
+        st.eager_ms = [20.0]
+        assert T._decide(st) == "trial"
+        st.eager_ms = [50.0]
+        assert T._decide(st) is False
+    else:  # CPU never captures: nothing to time, the default is to capture when capturable
+        assert T._decide(st) is True
