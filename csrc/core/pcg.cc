@@ -302,6 +302,28 @@ double Simulator::edge_cost(int node, int slot, int cfg, int prod_cfg) const {
   return ms;
 }
 
+const XferCost& Simulator::edge_xfer(int node, int slot, int cfg, int prod_cfg, bool backward) const {
+  uint64_t key = mix(mix(mix(mix(mix(7ull, node), slot), cfg), prod_cfg), backward ? 1 : 0);
+  auto it = xfer_cache_.find(key);
+  if (it != xfer_cache_.end()) return it->second;
+  const Node& n = prob_.nodes[node];
+  const auto in = n.inputs[slot];
+  const Node& pn = prob_.nodes[in.first];
+  XferCost x;
+  if (!backward) {
+    const Layout& src = pn.cands[prod_cfg].out_layouts[in.second];
+    x = transfer_cost(src, n.cands[cfg].in_layouts[slot], src.partial, n.elem_bytes, prob_.machine);
+  } else {
+    Layout dst = pn.cands[prod_cfg].out_layouts[in.second];
+    Layout src = n.cands[cfg].in_layouts[slot];
+    const bool sp = src.replicas > 1 || !src.halo.empty();
+    src.partial = false;
+    dst.partial = false;
+    x = transfer_cost(src, dst, sp, n.elem_bytes, prob_.machine);
+  }
+  return xfer_cache_.emplace(key, std::move(x)).first->second;
+}
+
 double Simulator::weight_sync_ms(int node, int cfg) const {
   const OpCandidate& c = prob_.nodes[node].cands[cfg];
   double ms = 0;
@@ -360,9 +382,7 @@ SimResult Simulator::simulate(const std::vector<int>& choice) const {
     for (size_t s = 0; s < n.inputs.size(); ++s) {
       const int p = n.inputs[s].first;
       if (p < 0) continue;
-      const Node& pn = prob_.nodes[p];
-      const Layout& src = pn.cands[choice[p]].out_layouts[n.inputs[s].second];
-      XferCost x = transfer_cost(src, c.in_layouts[s], src.partial, n.elem_bytes, prob_.machine);
+      const XferCost& x = edge_xfer(i, (int)s, choice[i], choice[p], false);
       double t = fwd_end[p];
       if (x.kind != XferKind::IDENTITY && x.ms > 0) t = run(x.devices, true, t, x.ms);
       ready = std::max(ready, t);
@@ -400,13 +420,7 @@ SimResult Simulator::simulate(const std::vector<int>& choice) const {
       if (p < 0) continue;
       const bool ng = s < n.input_needs_grad.size() ? n.input_needs_grad[s] : true;
       if (!ng) continue;
-      const Node& pn = prob_.nodes[p];
-      Layout dst = pn.cands[choice[p]].out_layouts[n.inputs[s].second];
-      Layout src = c.in_layouts[s];
-      const bool sp = src.replicas > 1 || !src.halo.empty();
-      src.partial = false;
-      dst.partial = false;
-      XferCost x = transfer_cost(src, dst, sp, n.elem_bytes, prob_.machine);
+      const XferCost& x = edge_xfer(i, (int)s, choice[i], choice[p], true);
       double t = bwd_end[i];
       if (x.kind != XferKind::IDENTITY && x.ms > 0) t = run(x.devices, true, t, x.ms);
       out_grad_time[p] = std::max(out_grad_time[p], t);

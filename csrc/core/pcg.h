@@ -142,6 +142,10 @@ class Simulator {
  private:
   const Problem& prob_;
   mutable std::unordered_map<uint64_t, double> edge_cache_;
+  // simulate(): the transfer of one edge for (node, slot, config, producer config), forward and
+  // backward (MCMC re-simulates the whole graph per move; layouts never change within a Problem)
+  mutable std::unordered_map<uint64_t, XferCost> xfer_cache_;
+  const XferCost& edge_xfer(int node, int slot, int cfg, int prod_cfg, bool backward) const;
 };
 
 // One parallel-branch region examined by the non-sequence (resource-split) refinement.

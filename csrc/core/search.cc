@@ -41,22 +41,51 @@ SearchResult search_dp(const Problem& p, int beam) {
     for (auto& in : p.nodes[i].inputs)
       if (in.first >= 0) last_use[in.first] = std::max(last_use[in.first], i);
 
-  // state: ordered list of live node ids + their chosen configs
-  std::vector<int> live;  // node ids (sorted by id)
+  // per-(node, config) compute cost and dense per-(node, slot) edge-cost matrices, filled lazily:
+  // the state loop below reads them (states x candidates) times per node, so they are plain
+  // arrays instead of the simulator's hashed edge cache
+  std::vector<std::vector<double>> ncost(N);
+  std::vector<std::vector<std::vector<double>>> ecost(N);
+  for (int i = 0; i < N; ++i) {
+    const Node& n = p.nodes[i];
+    ncost[i].resize(n.cands.size());
+    for (size_t c = 0; c < n.cands.size(); ++c) {
+      const OpCandidate& oc = n.cands[c];
+      double ms = oc.fwd_ms + (n.backward ? oc.bwd_ms : 0.0);
+      if (n.backward) ms += sim.weight_sync_ms(i, (int)c) * (p.overlap_grad_sync ? 0.5 : 1.0);
+      if (oc.mem_bytes > p.machine.mem_capacity) ms += 1e6;
+      ncost[i][c] = ms;
+    }
+    ecost[i].resize(n.inputs.size());
+    for (size_t s = 0; s < n.inputs.size(); ++s)
+      if (n.inputs[s].first >= 0)
+        ecost[i][s].assign(n.cands.size() * p.nodes[n.inputs[s].first].cands.size(), -1.0);
+  }
+  auto edge = [&](int i, int s, int c, int pc) {
+    const size_t np = p.nodes[p.nodes[i].inputs[s].first].cands.size();
+    double& v = ecost[i][s][(size_t)c * np + pc];
+    if (v < 0) v = sim.edge_cost(i, s, c, pc);
+    return v;
+  };
+
+  // A state is the configs of the live nodes (those with a later consumer), kept in a flat arena
+  // (stride = live count) and indexed by an open-addressing hash table.
   struct Entry {
     double cost;
-    int back;  // index into previous step's entry list
+    int back;  // index into the previous step's entries
     int cfg;   // config chosen for the node added at this step
   };
   std::vector<std::vector<Entry>> hist;
-  std::vector<std::vector<std::vector<int>>> keys_hist;
-  std::vector<std::vector<int>> cur_keys = {{}};
+  hist.reserve(N);
+  std::vector<int> live;
+  std::vector<int> cur_keys;  // flat, stride live.size()
   std::vector<Entry> cur = {{0.0, -1, -1}};
   int64_t states = 0;
+  std::vector<int> table;
 
   for (int i = 0; i < N; ++i) {
     const Node& n = p.nodes[i];
-    // positions of this node's producers within the live list
+    const int K = (int)live.size();
     std::vector<int> prod_pos(n.inputs.size(), -1);
     for (size_t s = 0; s < n.inputs.size(); ++s) {
       const int pr = n.inputs[s].first;
@@ -64,38 +93,84 @@ SearchResult search_dp(const Problem& p, int beam) {
       auto it = std::find(live.begin(), live.end(), pr);
       prod_pos[s] = (int)(it - live.begin());
     }
-    // next live set
-    std::vector<int> nlive;
-    for (int x : live)
-      if (last_use[x] > i) nlive.push_back(x);
+    std::vector<int> nlive, keep_pos;
+    for (int k = 0; k < K; ++k)
+      if (last_use[live[k]] > i) {
+        nlive.push_back(live[k]);
+        keep_pos.push_back(k);
+      }
     const bool keep_self = last_use[i] > i;
     if (keep_self) nlive.push_back(i);
-    std::vector<int> keep_pos;
-    for (size_t k = 0; k < live.size(); ++k)
-      if (last_use[live[k]] > i) keep_pos.push_back((int)k);
-
-    std::unordered_map<std::vector<int>, int, KeyHash> index;
-    std::vector<std::vector<int>> nkeys;
+    const int K2 = (int)nlive.size();
+    const int C = (int)n.cands.size();
+    const size_t expect = std::min<size_t>((size_t)cur.size() * (keep_self ? C : 1), (size_t)1 << 22);
+    size_t cap = 64;
+    while (cap < 2 * expect) cap <<= 1;
+    table.assign(cap, -1);
     std::vector<Entry> next;
+    std::vector<int> nkeys;
+    next.reserve(expect);
+    nkeys.reserve(expect * K2);
     std::vector<int> prod_cfg(n.inputs.size(), 0);
+    std::vector<double> cc(C);
     for (size_t e = 0; e < cur.size(); ++e) {
-      const auto& key = cur_keys[e];
+      const int* key = cur_keys.data() + e * K;
+      uint64_t h0 = 1469598103934665603ull;
+      for (int kp : keep_pos) h0 = (h0 ^ (uint64_t)(key[kp] + 1)) * 1099511628211ull;
       for (size_t s = 0; s < n.inputs.size(); ++s) prod_cfg[s] = prod_pos[s] >= 0 ? key[prod_pos[s]] : 0;
-      for (int c = 0; c < (int)n.cands.size(); ++c) {
-        const double cost = cur[e].cost + sim.node_cost(i, c, prod_cfg);
-        std::vector<int> nk;
-        nk.reserve(nlive.size());
-        for (int kp : keep_pos) nk.push_back(key[kp]);
-        if (keep_self) nk.push_back(c);
-        auto it = index.find(nk);
-        if (it == index.end()) {
-          index.emplace(nk, (int)next.size());
-          nkeys.push_back(std::move(nk));
-          next.push_back({cost, (int)e, c});
-        } else if (cost < next[it->second].cost) {
-          next[it->second] = {cost, (int)e, c};
+      for (int c = 0; c < C; ++c) {
+        double cost = cur[e].cost + ncost[i][c];
+        for (size_t s = 0; s < n.inputs.size(); ++s)
+          if (n.inputs[s].first >= 0) cost += edge(i, (int)s, c, prod_cfg[s]);
+        cc[c] = cost;
+      }
+      states += C;
+      // without a later consumer this node's config does not enter the state: only the best
+      // config per predecessor state can survive
+      int c_lo = 0, c_hi = C;
+      if (!keep_self) {
+        int b = 0;
+        for (int c = 1; c < C; ++c)
+          if (cc[c] < cc[b]) b = c;
+        c_lo = b;
+        c_hi = b + 1;
+      }
+      for (int c = c_lo; c < c_hi; ++c) {
+        const uint64_t h = keep_self ? (h0 ^ (uint64_t)(c + 1)) * 1099511628211ull : h0;
+        size_t slot = (size_t)(h ^ (h >> 29)) & (cap - 1);
+        int found = -1;
+        while (table[slot] >= 0) {
+          const int* k2 = nkeys.data() + (size_t)table[slot] * K2;
+          bool eq = true;
+          for (size_t q = 0; q < keep_pos.size() && eq; ++q) eq = k2[q] == key[keep_pos[q]];
+          if (eq && keep_self) eq = k2[K2 - 1] == c;
+          if (eq) {
+            found = table[slot];
+            break;
+          }
+          slot = (slot + 1) & (cap - 1);
         }
-        ++states;
+        if (found < 0) {
+          table[slot] = (int)next.size();
+          for (int kp : keep_pos) nkeys.push_back(key[kp]);
+          if (keep_self) nkeys.push_back(c);
+          next.push_back({cc[c], (int)e, c});
+          if (next.size() * 2 > cap) {  // grow and rehash
+            cap <<= 1;
+            table.assign(cap, -1);
+            for (size_t q = 0; q < next.size(); ++q) {
+              const int* k2 = nkeys.data() + q * K2;
+              uint64_t hh = 1469598103934665603ull;
+              for (int t = 0; t < K2 - (keep_self ? 1 : 0); ++t) hh = (hh ^ (uint64_t)(k2[t] + 1)) * 1099511628211ull;
+              if (keep_self) hh = (hh ^ (uint64_t)(k2[K2 - 1] + 1)) * 1099511628211ull;
+              size_t sl = (size_t)(hh ^ (hh >> 29)) & (cap - 1);
+              while (table[sl] >= 0) sl = (sl + 1) & (cap - 1);
+              table[sl] = (int)q;
+            }
+          }
+        } else if (cc[c] < next[found].cost) {
+          next[found] = {cc[c], (int)e, c};
+        }
       }
     }
     if ((int)next.size() > beam) {  // keep the best `beam` frontier states
@@ -105,16 +180,17 @@ SearchResult search_dp(const Problem& p, int beam) {
                        [&](int a, int b) { return next[a].cost < next[b].cost; });
       ord.resize(beam);
       std::vector<Entry> n2;
-      std::vector<std::vector<int>> k2;
+      std::vector<int> k2;
+      n2.reserve(beam);
+      k2.reserve((size_t)beam * K2);
       for (int k : ord) {
         n2.push_back(next[k]);
-        k2.push_back(nkeys[k]);
+        k2.insert(k2.end(), nkeys.begin() + (size_t)k * K2, nkeys.begin() + (size_t)(k + 1) * K2);
       }
       next.swap(n2);
       nkeys.swap(k2);
     }
     hist.push_back(next);
-    keys_hist.push_back(nkeys);
     cur.swap(next);
     cur_keys.swap(nkeys);
     live.swap(nlive);

@@ -25,13 +25,14 @@ struct GemmArgs {
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
-  int impl = 2;  // 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
+  int impl = 2;  // 4: persistent 4-wave (gemm_w4p.hip, falls back to 3), 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
   // Backward-activation epilogue (gemm256 only, see gemm_dact_bf16): C = (alpha*A.B) * act'(zin),
   // zin the producer's bf16 pre-activation in C's layout; colpart (optional) receives per-128-row
   // fp32 column sums of that product, [2 * ceil(M / 256)][N], for the producer's bias gradient.
   const void* zin = nullptr;
   float* colpart = nullptr;
   bool dact = false;
+  int ablate = 0;  // measurement builds only (impl 40 / 41 in the probes): see gemm_w4p.hip
 };
 
 void gemm_bf16(GemmArgs p, hipStream_t stream);
@@ -41,6 +42,9 @@ bool gemm_big_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStrea
 bool gemm256_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 // 4-wave 256x256x64 kernel, 128x128 outputs per wave, two-slot LDS-DMA ring (gemm_w4.hip); K % 128 == 0
 bool gemm_w4_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+// the same main loop as a persistent launch (one workgroup per CU walks the tiles; the next tile's
+// first K-tiles load during this tile's epilogue), gemm_w4p.hip; batch 1, no beta / split-K / Z
+bool gemm_w4p_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 int gemm256_bn(int M, int N, int batch, int splitk);
 // dgrad GEMM of a consumer Linear fused with the producer Linear's activation backward:
 // C[M,N] bf16 = (A.B) * act'(zin), colpart as above. False when the shape / alignment does not

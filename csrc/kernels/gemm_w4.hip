@@ -24,62 +24,11 @@
 // compiler are padded explicitly (pin_acc + s_nop at both ends of the loop).
 // Fragment images, swizzles, MFMA operand order and epilogue as gemm256_tile.h. Requires
 // K % 128 == 0, 16-B aligned operand rows, operands < 2 GiB.
-#include "gemm256_tile.h"
+#include "gemm_w4_core.h"
 
 namespace ffk {
 namespace w4 {
 using namespace g256;
-
-constexpr int BN = 256, BK = 64, NTH = 256;
-constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-constexpr int A_PIECES = A_BYTES / 1024, PIECES = STAGE / 1024, PW = PIECES / 4;
-
-template <int N>
-__device__ __forceinline__ void vmcnt() {
-  static_assert(N == 0 || N == 8 || N == 16, "add the immediate");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-}
-
-template <bool KCONT>
-__device__ __forceinline__ int piece_off(int64_t ld, int mn0, int k0, int pc, int lane) {
-  int64_t elem;
-  if (KCONT) {  // 8 rows x 128 B
-    const int row = pc * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ swz_k<BK>(row);
-    elem = (int64_t)(mn0 + row) * ld + k0 + c * 8;
-  } else {  // 4 k-rows of one 128-wide half (256 B each)
-    const int half = pc / (BK / 4);
-    const int krow = (pc % (BK / 4)) * 4 + (lane >> 4);
-    const int c = (lane & 15) ^ swz_mn(krow);
-    elem = (int64_t)(k0 + krow) * ld + mn0 + half * 128 + c * 8;
-  }
-  return (int)(elem * 2);
-}
-
-// frag<KCONT, 64>(tile, r0, kk). The MN-contiguous (transposing) form is inline asm: hipcc puts an
-// s_waitcnt vmcnt(0) in front of every ds_read_b64_tr_b16 builtin while LDS-DMA is in flight (it
-// cannot tell that the read and the DMA touch different slots), which drains the ring once per
-// fragment. The asm results are consumed only after the half's lgkmcnt(0).
-template <bool KCONT>
-__device__ __forceinline__ bf16x8 frag64(const char* tile, int r0, int kk, int lane) {
-  if constexpr (KCONT) {
-    return frag<true, BK>(tile, r0, kk, lane);
-  } else {
-    const char* hl = tile + (r0 >> 7) * (BK * 256);
-    const int rr = r0 & 127;
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
-    const int chunk = (rr >> 3) + (pp >> 1);
-    const int k0 = 32 * kk + 8 * g + q, k1 = k0 + 4;
-    const unsigned a0 = (unsigned)(uintptr_t)(hl + k0 * 256 + ((chunk ^ swz_mn(k0)) << 4) + 8 * (pp & 1));
-    const unsigned a1 = (unsigned)(uintptr_t)(hl + k1 * 256 + ((chunk ^ swz_mn(k1)) << 4) + 8 * (pp & 1));
-    typedef short v4s __attribute__((ext_vector_type(4)));
-    v4s lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3" : "=&v"(lo), "=&v"(hi) : "v"(a0), "v"(a1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  }
-}
 
 template <bool A_K, bool B_K, int OUT_MODE>
 __global__ void __launch_bounds__(NTH, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))

@@ -184,7 +184,9 @@ def enumerate_configs(layer, num_devices: int, allow_kinds=("sample", "attribute
 
     rec(0, 1)
     pinned = layer.attrs.get("pin")
-    if pinned is not None:  # a pin_parallel rewrite (pcg/joint.py) fixed this op's degrees
+    if pinned is not None and math.prod(pinned) > num_devices:
+        pinned = None  # a plan for more devices replayed on fewer (e.g. a 1-process reference run)
+    if pinned is not None:  # a parallelization rewrite (pcg/joint.py) fixed this op's degrees
         out = [c for c in out if tuple(c.degrees) == tuple(pinned)] or \
             [OpConfig(tuple(pinned), tuple(range(int(math.prod(pinned)))))]
     return _cap_candidates(out, max_configs)
@@ -228,8 +230,8 @@ def data_parallel_config(layer, num_devices: int) -> OpConfig:
     pin = getattr(layer.impl, "pinned_config", None)
     if pin is not None:
         return pin(num_devices)
-    if layer.attrs.get("pin") is not None:  # pinned by a joint-search rewrite: its only layout
-        degs = tuple(layer.attrs["pin"])
+    if layer.attrs.get("pin") is not None and math.prod(layer.attrs["pin"]) <= num_devices:
+        degs = tuple(layer.attrs["pin"])  # pinned by a joint-search rewrite: its only layout
         return OpConfig(degs, tuple(range(int(math.prod(degs)))))
     sizes = layer.impl.axis_sizes()
     n = len(sizes)

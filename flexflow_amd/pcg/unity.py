@@ -92,6 +92,18 @@ def allowed_kinds(cfg):
     return tuple(k)
 
 
+_CAND_CACHE: dict = {}
+
+
+def layer_signature(L) -> tuple:
+    """Everything an op's candidate configs, layouts and costs depend on (not its name/position)."""
+    return (L.op_type.value, tuple((tuple(t.dims), t.data_type.value) for t in L.inputs),
+            tuple((tuple(w.dims), w.data_type.value) for w in L.weights),
+            tuple((tuple(o.dims), o.data_type.value) for o in L.outputs),
+            repr(sorted((k, repr(v)) for k, v in L.attrs.items() if k not in ("kernel_init", "bias_init", "name"))),
+            tuple(L.impl.needs_input_grad(j) for j in range(len(L.inputs))))
+
+
 def build_problem(model, n_devices: int, measure: bool):
     core = _core()
     cfg = model.config
@@ -114,13 +126,34 @@ def build_problem(model, n_devices: int, measure: bool):
     out_t = model.output_tensor()
     from .strategy import machine_device_sets
     dsets = machine_device_sets(n_devices, prob.machine.gpus_per_node)
+    max_cands = int(os.environ.get("FF_MAX_CANDS", "32"))
     for i, L in enumerate(layers):
-        cands = enumerate_configs(L, n_devices, kinds, max_configs=int(os.environ.get("FF_MAX_CANDS", "32")),
-                                  device_sets=dsets)
-        dp = data_parallel_config(L, n_devices)
-        if dp not in cands:
-            cands.append(dp)
-        all_cands.append(cands)
+        # candidates and their costs depend only on the op's signature: identical layers (BERT's 24
+        # encoder layers) and the unchanged layers of a rewritten graph (joint search) reuse them
+        key = (layer_signature(L), n_devices, kinds, cdt, bool(measure), prob.machine.gpus_per_node, max_cands,
+               str(device))
+        hit = _CAND_CACHE.get(key)
+        if hit is None:
+            cands = enumerate_configs(L, n_devices, kinds, max_configs=max_cands, device_sets=dsets)
+            dp = data_parallel_config(L, n_devices)
+            if dp not in cands:
+                cands.append(dp)
+            cc = []
+            for c in cands:
+                lo = op_layouts(L, c)
+                oc = core.OpCandidate()
+                oc.degrees = list(c.degrees)
+                oc.devices = list(c.devices)
+                f, b = costmodel.op_cost(L, c, cdt, measure, device)
+                oc.fwd_ms, oc.bwd_ms = f, b
+                oc.mem_bytes = costmodel.mem_bytes(L, c, cdt)
+                oc.in_layouts = [to_core_layout(x) for x in lo.inputs]
+                oc.out_layouts = [to_core_layout(x) for x in lo.outputs]
+                oc.w_layouts = [to_core_layout(x) for x in lo.weights]
+                cc.append(oc)
+            hit = _CAND_CACHE[key] = (cands, cc)
+        cands, cc = hit
+        all_cands.append(list(cands))
         node = core.Node()
         node.name = L.name
         node.op_type = L.op_type.name
@@ -129,26 +162,15 @@ def build_problem(model, n_devices: int, measure: bool):
                                  for j, t in enumerate(L.inputs)]
         node.elem_bytes = elem
         node.backward = L.op_type != OperatorType.OP_INPUT
-        cc = []
-        for c in cands:
-            lo = op_layouts(L, c)
-            oc = core.OpCandidate()
-            oc.degrees = list(c.degrees)
-            oc.devices = list(c.devices)
-            f, b = costmodel.op_cost(L, c, cdt, measure, device)
-            oc.fwd_ms, oc.bwd_ms = f, b
-            oc.mem_bytes = costmodel.mem_bytes(L, c, cdt)
-            oc.in_layouts = [to_core_layout(x) for x in lo.inputs]
-            oc.out_layouts = [to_core_layout(x) for x in lo.outputs]
-            oc.w_layouts = [to_core_layout(x) for x in lo.weights]
-            cc.append(oc)
         node.cands = cc
         nodes.append(node)
     prob.nodes = nodes
     return prob, all_cands
 
 
-def search(model, algo: str):
+def search(model, algo: str, quick: bool = False):
+    """quick: the frontier DP only (no simulator-driven MCMC, no resource-split refinement) — how
+    the joint search ranks candidate graphs before the full search of the best one."""
     cfg = model.config
     n = cfg.num_devices
     core = _core()
@@ -162,6 +184,8 @@ def search(model, algo: str):
     budget = cfg.search_budget if cfg.search_budget and cfg.search_budget > 0 else None
 
     def run_search():
+        if quick:
+            return core.search_unity(prob, 4096, 0, cfg.search_alpha, cfg.seed)
         if algo == "mcmc":
             return core.search_mcmc(prob, dp_choice, budget or cfg.mcmc_iterations, cfg.search_alpha, cfg.seed)
         return core.search_unity(prob, 4096, budget if budget is not None else 300, cfg.search_alpha, cfg.seed)
@@ -173,7 +197,7 @@ def search(model, algo: str):
         res = run_search()
     choice = list(res.choice)
     split_report = []
-    if algo != "mcmc" and n > 1 and os.environ.get("FF_NONSEQ_SPLIT", "1") != "0":
+    if algo != "mcmc" and n > 1 and not quick and os.environ.get("FF_NONSEQ_SPLIT", "1") != "0":
         # resource-split refinement: parallel branches re-searched on disjoint device groups
         sr = core.search_split(prob, choice, 4096)
         for si in sr.splits:

@@ -35,7 +35,7 @@ SHAPES = [
     ("wgrad", 1024, 4096, T, False, False, 24, True),
     ("wgrad", 30522, 1024, T, False, False, 1, True),
 ]
-IMP = {"w4": 3, "k256": 2, "big": 1, "128": 0}
+IMP = {"w4p": 4, "w4p_nostore": 40, "w4": 3, "k256": 2, "big": 1, "128": 0}
 dev = "cuda"
 X = Kn.ext()
 
