@@ -292,6 +292,137 @@ void slab_sum(Tensor slabs, Tensor out, int64_t S, double beta) {
   ffk::slab_sum(slabs.data_ptr<float>(), out.data_ptr<float>(), out.numel(), (int)S, (float)beta, cur_stream());
 }
 
+void gemm_f32(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> Z, int64_t M, int64_t N,
+              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t batch,
+              bool a_k, bool b_k, double alpha, double beta, int64_t act) {
+  check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
+  TORCH_CHECK(A.scalar_type() == at::kFloat && B.scalar_type() == at::kFloat && C.scalar_type() == at::kFloat,
+              "gemm_f32: A/B/C must be fp32");
+  auto last = [](int64_t rows, int64_t cols, int64_t ld, int64_t stride, int64_t nb) {
+    return (nb - 1) * stride + (rows - 1) * ld + cols;
+  };
+  TORCH_CHECK(last(a_k ? M : K, a_k ? K : M, lda, sA, batch) <= A.numel(), "gemm_f32: A too small");
+  TORCH_CHECK(last(b_k ? N : K, b_k ? K : N, ldb, sB, batch) <= B.numel(), "gemm_f32: B too small");
+  TORCH_CHECK(last(M, N, ldc, sC, batch) <= C.numel(), "gemm_f32: C too small");
+  ffk::GemmArgs p;
+  p.A = reinterpret_cast<const uint16_t*>(A.data_ptr());
+  p.B = reinterpret_cast<const uint16_t*>(B.data_ptr());
+  p.C = C.data_ptr();
+  if (Z.has_value() && Z->defined()) {
+    TORCH_CHECK(Z->scalar_type() == at::kFloat && Z->numel() >= last(M, N, ldc, sC, batch), "gemm_f32: Z");
+    p.Z = Z->data_ptr();
+  }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N, "gemm_f32: bias too small");
+    p.bias = bias->data_ptr();
+    p.bias_bf16 = bias->scalar_type() == at::kBFloat16;
+  }
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.sA = sA; p.sB = sB; p.sC = sC; p.batch = batch;
+  p.alpha = alpha; p.beta = beta; p.act = act;
+  p.a_kcontig = a_k; p.b_kcontig = b_k; p.out_f32 = true;
+  ffk::gemm_f32(p, cur_stream());
+}
+
+void causal_mask_f32(Tensor s, int64_t Sq, int64_t Sk) {
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.is_contiguous() && s.numel() % Sk == 0);
+  ffk::causal_mask_f32(s.data_ptr<float>(), s.numel() / Sk, (int)Sq, (int)Sk, cur_stream());
+}
+
+// ------------------------------------------------------------------ mixture of experts (moe.hip)
+std::vector<void*> ptr_list(const std::vector<optional<Tensor>>& ts, at::ScalarType dt, int64_t numel) {
+  TORCH_CHECK((int)ts.size() <= ffk::kMoeMaxExperts, "moe: at most ", ffk::kMoeMaxExperts, " experts");
+  std::vector<void*> out;
+  for (auto& t : ts) {
+    if (t.has_value() && t->defined()) {
+      check_dev(*t, "expert tensor");
+      TORCH_CHECK(t->scalar_type() == dt && t->is_contiguous() && t->numel() == numel, "moe: expert tensor shape/dtype");
+      out.push_back(t->data_ptr());
+    } else {
+      out.push_back(nullptr);
+    }
+  }
+  return out;
+}
+
+void topk_fwd(Tensor x, Tensor vals, Tensor idx, int64_t k) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && vals.is_contiguous() && idx.is_contiguous() && idx.scalar_type() == at::kInt);
+  const int64_t n = x.size(-1), rows = x.numel() / n;
+  TORCH_CHECK(k >= 1 && k <= n && vals.numel() == rows * k && idx.numel() == rows * k && vals.scalar_type() == x.scalar_type());
+  ffk::topk_fwd(dtcode(x), x.data_ptr(), vals.data_ptr(), idx.data_ptr<int>(), (int)rows, (int)n, (int)k, cur_stream());
+}
+
+void topk_bwd(Tensor dvals, Tensor idx, Tensor dx) {
+  const int64_t n = dx.size(-1), rows = dx.numel() / n, k = idx.size(-1);
+  TORCH_CHECK(dvals.is_contiguous() && idx.is_contiguous() && dx.is_contiguous() && idx.scalar_type() == at::kInt &&
+              dvals.numel() == rows * k && idx.numel() == rows * k && dvals.scalar_type() == dx.scalar_type());
+  ffk::topk_bwd(dtcode(dx), dvals.data_ptr(), idx.data_ptr<int>(), dx.data_ptr(), (int)rows, (int)n, (int)k, cur_stream());
+}
+
+int64_t moe_route_ws_ints(int64_t L, int64_t n) { return ffk::moe_route_ws_ints((int)L, (int)n); }
+
+void moe_route(Tensor assign, int64_t n, int64_t cap, Tensor expert, Tensor pos, Tensor load, Tensor ws) {
+  check_dev(assign, "assign");
+  const int64_t L = assign.numel();
+  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.is_contiguous() && expert.numel() == L && pos.numel() == L &&
+              load.numel() == n && expert.scalar_type() == at::kInt && pos.scalar_type() == at::kInt &&
+              load.scalar_type() == at::kInt && ws.scalar_type() == at::kInt &&
+              ws.numel() >= ffk::moe_route_ws_ints((int)L, (int)n) && n >= 1);
+  ffk::moe_route(assign.data_ptr<int>(), (int)L, (int)n, (int)cap, expert.data_ptr<int>(), pos.data_ptr<int>(),
+                 load.data_ptr<int>(), ws.data_ptr<int>(), cur_stream());
+}
+
+void groupby_fwd(Tensor data, Tensor expert, Tensor pos, std::vector<optional<Tensor>> outs, int64_t cap, int64_t k) {
+  check_dev(data, "data");
+  TORCH_CHECK(data.is_contiguous());
+  const int64_t B = data.size(0), D = data.numel() / B, L = expert.numel();
+  TORCH_CHECK(L == B * k && pos.numel() == L);
+  auto ptrs = ptr_list(outs, data.scalar_type(), cap * D);
+  ffk::groupby_fwd(dtcode(data), data.data_ptr(), expert.data_ptr<int>(), pos.data_ptr<int>(), ptrs.data(),
+                   (int)ptrs.size(), (int)cap, (int)L, (int)k, (int)D, cur_stream());
+}
+
+void groupby_bwd(std::vector<optional<Tensor>> douts, Tensor expert, Tensor pos, Tensor dx, int64_t cap, int64_t k) {
+  TORCH_CHECK(dx.is_contiguous());
+  const int64_t B = dx.size(0), D = dx.numel() / B;
+  TORCH_CHECK(expert.numel() == B * k && pos.numel() == B * k);
+  auto ptrs = ptr_list(douts, dx.scalar_type(), cap * D);
+  ffk::groupby_bwd(dtcode(dx), ptrs.data(), (int)ptrs.size(), expert.data_ptr<int>(), pos.data_ptr<int>(),
+                   dx.data_ptr(), (int)B, (int)k, (int)D, cur_stream());
+}
+
+void aggregate_fwd(optional<Tensor> gate, std::vector<optional<Tensor>> exps, Tensor expert, Tensor pos, Tensor out,
+                   int64_t cap, int64_t k) {
+  TORCH_CHECK(out.is_contiguous());
+  const int64_t B = out.size(0), D = out.numel() / B;
+  TORCH_CHECK(expert.numel() == B * k && pos.numel() == B * k);
+  if (gate.has_value() && gate->defined())
+    TORCH_CHECK(gate->numel() == B * k && gate->is_contiguous() && gate->scalar_type() == out.scalar_type());
+  auto ptrs = ptr_list(exps, out.scalar_type(), cap * D);
+  for (void* q : ptrs) TORCH_CHECK(q != nullptr, "aggregate: every expert prediction is needed");
+  ffk::aggregate_fwd(dtcode(out), ptr(gate), ptrs.data(), (int)ptrs.size(), expert.data_ptr<int>(),
+                     pos.data_ptr<int>(), out.data_ptr(), (int)B, (int)k, (int)D, cur_stream());
+}
+
+void aggregate_bwd(Tensor dout, optional<Tensor> gate, std::vector<optional<Tensor>> exps,
+                   std::vector<optional<Tensor>> dexps, Tensor expert, Tensor pos, optional<Tensor> assign,
+                   optional<Tensor> true_assign, Tensor load, double lambda_bal, optional<Tensor> dgate,
+                   optional<Tensor> dfull, int64_t cap, int64_t k) {
+  TORCH_CHECK(dout.is_contiguous());
+  const int64_t B = dout.size(0), D = dout.numel() / B;
+  const int64_t n = (int64_t)exps.size();
+  TORCH_CHECK(expert.numel() == B * k && pos.numel() == B * k && load.numel() == n && dexps.size() == exps.size());
+  if (dgate.has_value() && dgate->defined()) TORCH_CHECK(dgate->numel() == B * k && dgate->scalar_type() == dout.scalar_type());
+  if (dfull.has_value() && dfull->defined()) TORCH_CHECK(dfull->numel() == B * n && dfull->scalar_type() == dout.scalar_type());
+  auto pe = ptr_list(exps, dout.scalar_type(), cap * D);
+  auto pd = ptr_list(dexps, dout.scalar_type(), cap * D);
+  ffk::aggregate_bwd(dtcode(dout), dout.data_ptr(), ptr(gate), pe.data(), pd.data(), (int)n, (int)cap,
+                     expert.data_ptr<int>(), pos.data_ptr<int>(), ptr<int>(assign), ptr<int>(true_assign),
+                     load.data_ptr<int>(), (float)lambda_bal, ptr(dgate), ptr(dfull), (int)B, (int)k, (int)D,
+                     cur_stream());
+}
+
 // q/k/v/o given with explicit [b,h,s] element strides (d contiguous)
 void attn_fwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
               std::vector<int64_t> vs, Tensor o, std::vector<int64_t> os, Tensor lse, int64_t B, int64_t H,
@@ -591,6 +722,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("init_normal", &init_normal);
   m.def("fill", &fill);
   m.def("slab_sum", &slab_sum);
+  m.def("gemm_f32", &gemm_f32);
+  m.def("causal_mask_f32", &causal_mask_f32);
+  m.def("topk_fwd", &topk_fwd);
+  m.def("topk_bwd", &topk_bwd);
+  m.def("moe_route_ws_ints", &moe_route_ws_ints);
+  m.def("moe_route", &moe_route);
+  m.def("groupby_fwd", &groupby_fwd);
+  m.def("groupby_bwd", &groupby_bwd);
+  m.def("aggregate_fwd", &aggregate_fwd);
+  m.def("aggregate_bwd", &aggregate_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_ws", &attn_bwd_ws);

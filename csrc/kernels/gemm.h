@@ -46,6 +46,11 @@ bool gemm_w4_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
 // first K-tiles load during this tile's epilogue), gemm_w4p.hip; batch 1, no beta / split-K / Z
 bool gemm_w4p_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 int gemm256_bn(int M, int N, int batch, int splitk);
+// fp32 operands and output on the f32-input MFMA (gemm_f32.hip): any shape / layout, batch strides,
+// alpha / beta / bias / activation / pre-activation epilogue (A, B, C, Z reinterpreted as float)
+void gemm_f32(const GemmArgs& p, hipStream_t stream);
+// fp32 attention path: -inf above the causal diagonal of [rows][Sk] scores (rows = batch * Sq)
+void causal_mask_f32(float* s, int64_t rows, int Sq, int Sk, hipStream_t st);
 // dgrad GEMM of a consumer Linear fused with the producer Linear's activation backward:
 // C[M,N] bf16 = (A.B) * act'(zin), colpart as above. False when the shape / alignment does not
 // fit the 256-row kernel's coalesced epilogue (the caller then runs GEMM + bias_act_bwd).

@@ -43,6 +43,25 @@ void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, 
 // out_k += colsum(part[k*R:(k+1)*R]) for each non-null out_k, k < 3 (slab k at offset k*R*C)
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st);
 
+// moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
+// on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.
+constexpr int kMoeMaxExperts = 64;
+void topk_fwd(int dt, const void* x, void* vals, int* idx, int rows, int n, int k, hipStream_t st);
+void topk_bwd(int dt, const void* dvals, const int* idx, void* dx, int rows, int n, int k, hipStream_t st);
+int64_t moe_route_ws_ints(int L, int n);
+// expert[i] (clamped id), pos[i] (row in the expert's tensor, -1 = dropped) of the L = B*k
+// flattened (sample, choice) pairs in reference order; load[e] = pairs routed to e
+void moe_route(const int* assign, int L, int n, int cap, int* expert, int* pos, int* load, int* ws, hipStream_t st);
+void groupby_fwd(int dt, const void* data, const int* expert, const int* pos, void* const* outs, int n, int cap,
+                 int L, int k, int D, hipStream_t st);
+void groupby_bwd(int dt, void* const* douts, int n, const int* expert, const int* pos, void* dx, int B, int k, int D,
+                 hipStream_t st);
+void aggregate_fwd(int dt, const void* gate, void* const* exps, int n, const int* expert, const int* pos, void* out,
+                   int B, int k, int D, hipStream_t st);
+void aggregate_bwd(int dt, const void* dout, const void* gate, void* const* exps, void* const* dexps, int n,
+                   int cap, const int* expert, const int* pos, const int* assign, const int* true_assign,
+                   const int* load, float lambda_bal, void* dgate, void* dfull, int B, int k, int D, hipStream_t st);
+
 // norm.hip
 void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st);

@@ -502,7 +502,20 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
         else:
             ours(IMPLS[choice])
         return C
-    # reference / fp32 path (library GEMM on device, plain torch on CPU)
+    if native(C) and A.dtype == torch.float32 and B.dtype == torch.float32:
+        # --dtype fp32 on the device: our f32-input MFMA kernel (csrc/kernels/gemm_f32.hip)
+        out = C if C.dtype == torch.float32 else torch.empty(C.shape, device=C.device, dtype=torch.float32)
+        if out is not C and beta != 0.0:
+            out.copy_(C)
+        Zf = Z if (Z is None or Z.dtype == torch.float32) else torch.empty(Z.shape, device=Z.device,
+                                                                           dtype=torch.float32)
+        ext().gemm_f32(A, B, out, bias, Zf, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act)
+        if out is not C:
+            C.copy_(out)
+        if Zf is not Z:
+            Z.copy_(Zf)
+        return C
+    # CPU reference (plain torch)
     Af = A.as_strided((batch, M, K), (sA, lda, 1)) if a_k else A.as_strided((batch, K, M), (sA, lda, 1)).transpose(1, 2)
     Bf = B.as_strided((batch, N, K), (sB, ldb, 1)).transpose(1, 2) if b_k else B.as_strided((batch, K, N), (sB, ldb, 1))
     cdt = torch.float32
@@ -524,6 +537,10 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
     and FFN1's GELU'). Autotuned per call site between the fused 256-row MFMA kernel
     (csrc/kernels/gemm256.hip dact epilogue) and the plain GEMM followed by an in-place
     bias_act_bwd pass (what the two ops run unfused)."""
+    if native(C) and C.dtype == torch.float32:  # fp32 on the device: our GEMM, then the act' pass
+        gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc)
+        ext().bias_act_bwd(C, Zp, C, db, M, N, act)
+        return C
     if not native(C) or C.dtype != torch.bfloat16:
         r = A.float() @ B.float().t() if b_k else A.float() @ B.float()
         r = r * act_grad_ref(Zp.float(), act)
@@ -575,7 +592,7 @@ def linear_fwd(x2d, w, bias, act, save_z):
     N = w.shape[0]
     y = torch.empty(M, N, device=x2d.device, dtype=x2d.dtype)
     z = torch.empty_like(y) if (save_z and act != ACT_NONE) else None
-    if native(x2d) and x2d.dtype == torch.bfloat16:
+    if native(x2d) and x2d.dtype in (torch.bfloat16, torch.float32) and w.dtype == x2d.dtype:
         gemm(x2d, w, y, M, N, K, True, True, K, K, N, bias=bias, Z=z, act=act)
         return y, z
     r = x2d.float() @ w.float().t()
@@ -610,7 +627,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
         need_dx = False
         if on_dx is not None:
             on_dx(dx)
-    if native(dy2d) and dy2d.dtype == torch.bfloat16:
+    if native(dy2d) and dy2d.dtype in (torch.bfloat16, torch.float32) and w.dtype == dy2d.dtype \
+            and x2d.dtype == dy2d.dtype:
         if need_dx:
             if dx_out is not None:
                 dx = dx_out
@@ -662,7 +680,8 @@ def bias_act_bwd(dy2d, z, act, db):
 
 def bmm(a, b, trans_a=False, trans_b=False, out=None):
     """Batched matmul over the leading dims: a [..., M, K] (or [..., K, M] if trans_a)."""
-    if native(a) and a.dtype == torch.bfloat16 and a.is_contiguous() and b.is_contiguous():
+    if native(a) and a.dtype in (torch.bfloat16, torch.float32) and b.dtype == a.dtype and a.is_contiguous() \
+            and b.is_contiguous():
         batch = int(math.prod(a.shape[:-2]))
         M = a.shape[-1] if trans_a else a.shape[-2]
         K = a.shape[-2] if trans_a else a.shape[-1]
@@ -1501,3 +1520,85 @@ def rmsnorm_bwd(x2d, w, dy2d, rstd, dw):
     if dw is not None:
         dw.add_((dyf * xf * r).sum(0))
     return dx.to(x2d.dtype)
+
+
+# ------------------------------------------------------------------ mixture of experts (moe.hip)
+MOE_MAX_EXPERTS = 64
+
+
+def moe_on_device(t: torch.Tensor, n: int = 1) -> bool:
+    """The HIP routing kernels run for bf16 / fp32 device tensors and up to 64 experts."""
+    return native(t) and t.dtype in (torch.bfloat16, torch.float32) and n <= MOE_MAX_EXPERTS
+
+
+def topk(x: torch.Tensor, k: int):
+    """(values, int32 indices) of the k largest along the last dim, values descending (ties:
+    lowest index first) — csrc/kernels/moe.hip, one wave per row."""
+    xc = x.contiguous()
+    vals = torch.empty(tuple(x.shape[:-1]) + (k,), device=x.device, dtype=x.dtype)
+    idx = torch.empty(vals.shape, device=x.device, dtype=torch.int32)
+    ext().topk_fwd(xc, vals, idx, k)
+    return vals, idx
+
+
+def topk_bwd(dvals: torch.Tensor, idx: torch.Tensor, shape) -> torch.Tensor:
+    dx = torch.empty(shape, device=dvals.device, dtype=dvals.dtype)
+    ext().topk_bwd(dvals.contiguous(), idx.contiguous(), dx)
+    return dx
+
+
+def moe_route(assign: torch.Tensor, n: int, cap: int):
+    """Device routing of the B*k (sample, choice) pairs: (expert id, row in the expert's tensor or
+    -1 when dropped past the capacity, load per expert), in the reference's sample order."""
+    a = assign.reshape(-1).to(torch.int32).contiguous()
+    L = a.numel()
+    expert = torch.empty(L, device=a.device, dtype=torch.int32)
+    pos = torch.empty(L, device=a.device, dtype=torch.int32)
+    load = torch.empty(n, device=a.device, dtype=torch.int32)
+    ws = torch.empty(max(1, int(ext().moe_route_ws_ints(L, n))), device=a.device, dtype=torch.int32)
+    ext().moe_route(a, n, cap, expert, pos, load, ws)
+    return expert, pos, load
+
+
+# ------------------------------------------------------------------ fp32 attention (our kernels)
+def attn_f32_supported(x) -> bool:
+    return native(x) and x.dtype == torch.float32
+
+
+def attn_f32_fwd(q, qs, k, ks, v, vs, o, os_, B, H, Sq, Sk, kd, vd, scale, causal):
+    """fp32 attention on our kernels, per sample: S = Q.K^T (f32 MFMA GEMM, heads as the batch),
+    causal mask, row softmax(scale * S) (softmax.hip), O = P.V. q/k/v/o are flat views with [b, h,
+    row] element strides (qs, ks, vs, os_) and contiguous head dims. Returns P [B, H, Sq, Sk]."""
+    X = ext()
+    q, k, v, o = q.reshape(-1), k.reshape(-1), v.reshape(-1), o.reshape(-1)
+    P = torch.empty(B, H, Sq, Sk, device=q.device, dtype=torch.float32)
+    S = torch.empty(H, Sq, Sk, device=q.device, dtype=torch.float32)
+    for b in range(B):
+        X.gemm_f32(q[b * qs[0]:], k[b * ks[0]:], S, None, None, Sq, Sk, kd, qs[2], ks[2], Sk, qs[1], ks[1], Sq * Sk,
+                   H, True, True, 1.0, 0.0, ACT_NONE)
+        if causal:
+            X.causal_mask_f32(S, Sq, Sk)
+        X.softmax_fwd(S, P[b], H * Sq, Sk, scale)
+        X.gemm_f32(P[b], v[b * vs[0]:], o[b * os_[0]:], None, None, Sq, vd, Sk, Sk, vs[2], os_[2], Sq * Sk, vs[1],
+                   os_[1], H, True, False, 1.0, 0.0, ACT_NONE)
+    return P
+
+
+def attn_f32_bwd(q, qs, k, ks, v, vs, do, dos, P, dq, dk, dv, B, H, Sq, Sk, kd, vd, scale):
+    """Backward of attn_f32_fwd: dP = dO.V^T, dS = scale * P * (dP - rowsum(dP * P)), dQ = dS.K,
+    dK = dS^T.Q, dV = P^T.dO (dq / dk / dv share q / k / v's strides)."""
+    X = ext()
+    q, k, v, do = q.reshape(-1), k.reshape(-1), v.reshape(-1), do.reshape(-1)
+    dq, dk, dv = dq.reshape(-1), dk.reshape(-1), dv.reshape(-1)
+    dP = torch.empty(H, Sq, Sk, device=q.device, dtype=torch.float32)
+    dS = torch.empty_like(dP)
+    for b in range(B):
+        X.gemm_f32(do[b * dos[0]:], v[b * vs[0]:], dP, None, None, Sq, Sk, vd, dos[2], vs[2], Sk, dos[1], vs[1],
+                   Sq * Sk, H, True, True, 1.0, 0.0, ACT_NONE)
+        X.softmax_bwd(P[b], dP, dS, H * Sq, Sk, scale, False)
+        X.gemm_f32(dS, k[b * ks[0]:], dq[b * qs[0]:], None, None, Sq, kd, Sk, Sk, ks[2], qs[2], Sq * Sk, ks[1],
+                   qs[1], H, True, False, 1.0, 0.0, ACT_NONE)
+        X.gemm_f32(dS, q[b * qs[0]:], dk[b * ks[0]:], None, None, Sk, kd, Sq, Sk, qs[2], ks[2], Sq * Sk, qs[1],
+                   ks[1], H, False, False, 1.0, 0.0, ACT_NONE)
+        X.gemm_f32(P[b], do[b * dos[0]:], dv[b * vs[0]:], None, None, Sk, vd, Sq, Sk, dos[2], vs[2], Sq * Sk,
+                   dos[1], vs[1], H, False, False, 1.0, 0.0, ACT_NONE)

@@ -165,6 +165,9 @@ class MultiHeadAttention(OpImpl):
             lse = K.flash_attn_fwd(pq, pst, pk, kst, pv, kst, po, pst, B, Hl, Sq, Sk, Dp, scale, causal)
             o.copy_(po[..., :vd])
             s.update(lse=lse, pad=(Dp, pq, pk, pv, po))
+        elif K.attn_f32_supported(q_in) and os.environ.get("FF_ATTN_REF_FALLBACK") != "1":
+            # --dtype fp32 on the device: f32 MFMA GEMMs + causal mask + row softmax, our kernels
+            s["P"] = K.attn_f32_fwd(qv, qs, kv, ks, vv, vs, o.view(-1), os_, B, Hl, Sq, Sk, kd, vd, scale, causal)
         else:
             if K.native(q_in) and q_in.dtype == torch.bfloat16 and os.environ.get("FF_ATTN_REF_FALLBACK") != "1":
                 raise NotImplementedError(
@@ -227,6 +230,9 @@ class MultiHeadAttention(OpImpl):
         elif "lse" in s:
             K.flash_attn_bwd(qv, qs, kv, ks, vv, vs, o, os_, do, os_, s["lse"], dq, qs, dk, ks, dv, vs,
                              B, Hl, Sq, Sk, kd, scale, causal)
+        elif "P" in s:
+            K.attn_f32_bwd(qv, qs, kv, ks, vv, vs, do.contiguous().view(-1), os_, s["P"], dq.view(-1), dk.view(-1),
+                           dv.view(-1), B, Hl, Sq, Sk, kd, vd, scale)
         else:
             q4 = qv.as_strided((B, Hl, Sq, kd), (qs[0], qs[1], qs[2], 1)).detach().float().requires_grad_()
             k4 = kv.as_strided((B, Hl, Sk, kd), (ks[0], ks[1], ks[2], 1)).detach().float().requires_grad_()

@@ -3,8 +3,9 @@ AggregateSpec / Cache).
 
 Reference: src/ops/batch_matmul.cc, reduce.cc, mean.cc (a stub that asserts in the reference),
 topk.cc, group_by.cc, aggregate.cc, aggregate_spec.cc, cache.cc (also a stub there).
-BatchMatmul runs on the bf16 MFMA GEMM (strided batch); the MoE routing ops are index shuffles
-on small tensors and use torch indexing.
+BatchMatmul runs on the bf16 MFMA GEMM (strided batch); TopK and the MoE routing ops run on the
+HIP kernels of csrc/kernels/moe.hip on the device (no host synchronisation, so an MoE step can be
+captured into a hipGraph) and on torch indexing on the CPU.
 """
 from __future__ import annotations
 
@@ -122,16 +123,23 @@ class TopK(OpImpl):
 
     def forward(self, ctx, xs, ws):
         x = xs[0]
+        if K.moe_on_device(x):  # HIP kernel (csrc/kernels/moe.hip): values descending, ties lowest index
+            v, i = K.topk(x, self.attrs["k"])
+            ctx.saved.update(idx=i, shape=x.shape, dtype=x.dtype)
+            return [v, i]
         v, i = torch.topk(x.float(), self.attrs["k"], -1, largest=True, sorted=bool(self.attrs.get("sorted", False)))
-        ctx.saved.update(idx=i, shape=x.shape)
+        ctx.saved.update(idx=i, shape=x.shape, dtype=x.dtype)
         return [v.to(x.dtype), i.to(torch.int32)]
 
     def backward(self, ctx, douts):
-        i, shp = ctx.saved.pop("idx"), ctx.saved.pop("shape")
+        i, shp, dt = ctx.saved.pop("idx"), ctx.saved.pop("shape"), ctx.saved.pop("dtype")
+        if douts[0] is None:
+            return [torch.zeros(shp, dtype=dt, device=i.device)]
+        if K.moe_on_device(douts[0]):
+            return [K.topk_bwd(douts[0].to(dt), i.to(torch.int32), shp)]
         dx = torch.zeros(shp, dtype=torch.float32, device=i.device)
-        if douts[0] is not None:
-            dx.scatter_add_(-1, i, douts[0].float())
-        return [dx.to(douts[0].dtype if douts[0] is not None else torch.float32)]
+        dx.scatter_add_(-1, i.long(), douts[0].float())
+        return [dx.to(douts[0].dtype)]
 
 
 def _expert_slots(assign: torch.Tensor, n: int, cap: int):
@@ -171,6 +179,13 @@ class GroupBy(OpImpl):
         data, assign = xs
         n, cap = self.attrs["n"], self.attrs["cap"]
         k = assign.shape[-1]
+        if K.moe_on_device(data, n):
+            # device routing + row scatter, no host synchronisation (csrc/kernels/moe.hip)
+            e, pos, _ = K.moe_route(assign, n, cap)
+            outs = [torch.empty((cap,) + tuple(data.shape[1:]), dtype=data.dtype, device=data.device) for _ in range(n)]
+            K.ext().groupby_fwd(data.contiguous(), e, pos, outs, cap, k)
+            ctx.saved.update(dev=(e, pos), shape=data.shape, dtype=data.dtype, k=k)
+            return outs
         e, pos, valid = _expert_slots(assign, n, cap)
         src = torch.arange(e.numel(), device=data.device) // k
         outs = []
@@ -184,6 +199,13 @@ class GroupBy(OpImpl):
 
     def backward(self, ctx, douts):
         s = ctx.saved
+        if "dev" in s:
+            e, pos = s.pop("dev")
+            shp, dt, k = s.pop("shape"), s.pop("dtype"), s.pop("k")
+            dx = torch.empty(shp, dtype=dt, device=e.device)
+            K.ext().groupby_bwd([d.to(dt).contiguous() if d is not None else None for d in douts], e, pos, dx,
+                                self.attrs["cap"], k)
+            return [dx, None]
         e, pos, valid, src, shp = s.pop("e"), s.pop("pos"), s.pop("valid"), s.pop("src"), s.pop("shape")
         like = [d for d in douts if d is not None][0]
         dx = torch.zeros(shp, dtype=torch.float32, device=like.device)
@@ -223,6 +245,18 @@ class Aggregate(OpImpl):
         n = len(exps)
         cap = exps[0].shape[0]
         B, k = assign.shape
+        spec = self.layer.op_type == OperatorType.OP_AGG_SPEC
+        if K.moe_on_device(exps[0], n):
+            dt = exps[0].dtype
+            e, pos, load = K.moe_route(assign, n, cap)
+            ex = [x.to(dt).contiguous() for x in exps]
+            g = None if spec else gate.to(dt).contiguous()
+            out = torch.empty((B, ex[0].shape[-1]), dtype=dt, device=ex[0].device)
+            K.ext().aggregate_fwd(g, ex, e, pos, out, cap, k)
+            ctx.saved.update(dev=(e, pos, load), exps=ex, gate=g, spec=spec, assign=assign.to(torch.int32).contiguous(),
+                             true_assign=true_assign.to(torch.int32).contiguous(), gate_dtype=gate.dtype,
+                             full_shape=full_gate.shape, full_dtype=full_gate.dtype, k=k, cap=cap)
+            return [out]
         e, pos, valid = _expert_slots(assign, n, cap)
         stacked = torch.stack([x.float() for x in exps])  # [n, cap, D]
         rows = stacked[e.clamp(0, n - 1), pos.clamp(0, cap - 1)]  # [B*k, D]
@@ -236,6 +270,21 @@ class Aggregate(OpImpl):
 
     def backward(self, ctx, douts):
         s = ctx.saved
+        if "dev" in s:
+            e, pos, load = s["dev"]
+            ex, g, spec = s["exps"], s["gate"], s["spec"]
+            dt = ex[0].dtype
+            dout = douts[0].to(dt).contiguous()
+            B, k, n = dout.shape[0], s["k"], len(ex)
+            dexp = [torch.empty_like(x) for x in ex]
+            dgate = None if spec else torch.empty((B, k), dtype=dt, device=dout.device)
+            dfull = None if spec else torch.empty(tuple(s["full_shape"]), dtype=dt, device=dout.device)
+            K.ext().aggregate_bwd(dout, g, ex, dexp, e, pos, s["assign"], s["true_assign"], load,
+                                  float(self.attrs.get("lambda_bal", 0.0)), dgate, dfull, s["cap"], k)
+            gdt, fdt = s["gate_dtype"], s["full_dtype"]
+            ctx.saved.clear()
+            return [None if dgate is None else dgate.to(gdt), None, None,
+                    None if dfull is None else dfull.to(fdt)] + dexp
         dout = douts[0].float()
         B, k, n, cap = s["B"], s["k"], s["n"], s["cap"]
         e, pos, valid, rows, w = s["e"], s["pos"], s["valid"], s["rows"], s["w"]

@@ -1,5 +1,6 @@
 """Numerics of the hand-written HIP kernels against plain PyTorch fp32 references (GPU only)."""
 import math
+import numpy as np
 
 import pytest
 import torch
@@ -796,3 +797,74 @@ def test_tune_cache_skips_timing(tmp_path, monkeypatch):
     if isinstance(first, str):  # a named choice persists: the second run takes it without timing
         assert len(K.TUNE_LOG) == n_log and next(iter(K._tuned.values())) == first
     assert _rel(C2, A.float() @ B.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,batch", [(256, 384, 512, 1), (200, 136, 72, 3), (1000, 1001, 1030, 1), (5, 7, 9, 2)])
+def test_gemm_f32(ffC, a_k, b_k, M, N, K, batch):
+    """fp32 GEMM on the f32-input MFMA (gemm_f32.hip) against torch fp32: layouts, edges, batches,
+    alpha / beta / bias / GELU / pre-activation epilogue."""
+    torch.manual_seed(4)
+    Am = torch.randn(batch, M, K, device=DEV)
+    Bn = torch.randn(batch, N, K, device=DEV)
+    A = Am if a_k else Am.transpose(1, 2).contiguous()
+    B = Bn if b_k else Bn.transpose(1, 2).contiguous()
+    ref = torch.bmm(Am.double(), Bn.double().transpose(1, 2))
+    C = torch.empty(batch, M, N, device=DEV)
+    ffC.gemm_f32(A, B, C, None, None, M, N, K, A.shape[-1], B.shape[-1], N, A.shape[-1] * A.shape[-2],
+                 B.shape[-1] * B.shape[-2], M * N, batch, a_k, b_k, 1.0, 0.0, 10)
+    assert _rel(C, ref) < 1e-6
+    bias = torch.randn(N, device=DEV)
+    C0 = torch.randn(batch, M, N, device=DEV)
+    C2, Z = C0.clone(), torch.empty(batch, M, N, device=DEV)
+    ffC.gemm_f32(A, B, C2, bias, Z, M, N, K, A.shape[-1], B.shape[-1], N, A.shape[-1] * A.shape[-2],
+                 B.shape[-1] * B.shape[-2], M * N, batch, a_k, b_k, 0.5, 1.0, 14)
+    z = 0.5 * ref + C0.double() + bias.double()
+    assert _rel(Z, z) < 1e-6
+    assert _rel(C2, torch.nn.functional.gelu(z)) < 1e-5
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("fused", [True, False])
+def test_attention_f32_path(causal, fused):
+    """--dtype fp32 attention runs our kernels (f32 MFMA GEMMs + mask + softmax), not einsum: the op's
+    forward and input gradients against the fp32 autograd reference."""
+    from flexflow_amd.core import DataType, FFConfig, FFModel, SGDOptimizer
+    cfg = FFConfig(["--dtype", "fp32", "--no-hip-graphs"])
+    cfg.batch_size = 2
+    ff = FFModel(cfg)
+    x = ff.create_tensor([2, 24, 64], DataType.DT_FLOAT)
+    if fused:
+        y = ff.multihead_attention(x, x, x, 64, 4, causal=causal)
+    else:
+        x2 = ff.create_tensor([2, 24, 64], DataType.DT_FLOAT)
+        y = ff.multihead_attention(x, x2, x2, 64, 4, causal=causal)
+    ff.optimizer = SGDOptimizer(ff, 0.0)
+    ff.compile()
+    L = [l for l in ff.layers if l.op_type.name == "OP_MULTIHEAD_ATTENTION"][0]
+    assert L.attrs["fused_qkv"] == fused
+    rng = torch.Generator().manual_seed(0)
+    xv = torch.randn(2, 24, 64, generator=rng)
+    x.set_tensor(ff, xv.numpy())
+    if not fused:
+        x2.set_tensor(ff, xv.numpy())
+    ff.forward()
+    ex = ff.executor
+    assert "P" in ex.ctx[L.name].saved and "lse" not in ex.ctx[L.name].saved  # the fp32 kernel path ran
+    out = torch.from_numpy(ff._get_tensor_value(y))
+    # reference: the op's own weights through torch autograd in fp64
+    W = {w.short_name: torch.from_numpy(np.asarray(w.get_weights(ff))).double() for w in L.weights}
+    xr = xv.double()
+    if fused:
+        qkv = xr.reshape(48, 64) @ W["qkv_weight"].reshape(-1, 64).t() + W["qkv_bias"].reshape(-1)
+        qkv = qkv.view(2, 24, 3, 4, 16)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    else:
+        proj = lambda n: (xr.reshape(48, 64) @ W[f"{n}_weight"].reshape(-1, 64).t() + W[f"{n}_bias"].reshape(-1)).view(2, 24, 4, 16)  # noqa: E731
+        q, k, v = proj("q"), proj("k"), proj("v")
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) / math.sqrt(16)
+    if causal:
+        s = s.masked_fill(torch.ones(24, 24, dtype=torch.bool).triu(1), float("-inf"))
+    o = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v).reshape(48, 64)
+    ref = (o @ W["o_weight"].reshape(64, 64).t() + W["o_bias"]).view(2, 24, 64)
+    assert _rel(out, ref) < 1e-5

@@ -73,7 +73,8 @@ def _build(case, ff):
         lab = rng.integers(0, bc.vocab, (B, bc.seq, 1)).astype(np.int32)
         return [ids, pos], feeds, lab, LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY
     from flexflow_amd.models import build
-    name = {"dlrm_small": "dlrm", "inception_small": "inception_v3"}[case]
+    name = {"dlrm_small": "dlrm", "inception_small": "inception_v3", "mlp_unify_small": "mlp_unify",
+            "candle_uno_small": "candle_uno", "xdl_small": "xdl"}[case]
     inputs, _, loss, _, make_batch = build(name, ff, B, small=True)
     arrs, lab = make_batch(rng)
     return inputs, list(arrs), lab, loss
@@ -200,7 +201,8 @@ def _compare(par, ref, tag, rtol=3e-4, atol=3e-5):
 
 
 @pytest.mark.parametrize("case,world", [("siblings", 2), ("bert_tiny", 4), ("dlrm_small", 8), ("bert_tiny", 8),
-                                        ("inception_small", 4)])
+                                        ("inception_small", 4), ("mlp_unify_small", 4), ("candle_uno_small", 8),
+                                        ("xdl_small", 4)])
 def test_searched_strategy_matches_single(case, world, monkeypatch):
     monkeypatch.setenv("FF_JOINT_BUDGET", "3")
     par, search, tmp = _run(case, world)
@@ -212,11 +214,13 @@ def test_searched_strategy_matches_single(case, world, monkeypatch):
     used = {d for v in search["strategy"].values() for d in v["devices"]}
     print(case, world, "devices used", sorted(used), "rewrites", search["rewrites"],
           {k: search["report"].get(k) for k in ("predicted_ms", "predicted_dp_ms", "graphs_costed")})
-    if case == "dlrm_small":
-        # not data parallel: some weighted op is split along a non-sample axis (the embedding tables
-        # parameter-parallel), or runs on a strict subset of the ranks
-        non_dp = [k for k, v in search["strategy"].items()
-                  if any(d > 1 for d in v["degrees"][1:]) or len(set(v["devices"])) not in (1, world)]
+    if case in ("dlrm_small", "mlp_unify_small", "candle_uno_small", "xdl_small"):
+        # not data parallel: some op is split along a non-sample axis (tables / channels parameter-
+        # parallel) or placed on a subset of the ranks (operator placement), where data parallelism
+        # would split the sample dim over all `world` ranks
+        non_dp = [k for k, v in search["strategy"].items() if not k.startswith("input")
+                  and (v["degrees"][0] != world or any(d > 1 for d in v["degrees"][1:])
+                       or sorted(v["devices"]) != list(range(world)))]
         assert non_dp, search["strategy"]
     if case == "siblings":
         # the accepted rewrite changed the graph the strategy is chosen for
