@@ -21,6 +21,7 @@ struct AttnArgs {
   int B = 0, H = 0, Sq = 0, Sk = 0, D = 64;
   float scale = 1.f;
   int causal = 0;
+  float rescale_thr = 8.f;  // forward: deferred-max threshold, log2 units (attn_set_rescale_thr)
 };
 
 void attn_fwd(AttnArgs a, hipStream_t st);
@@ -30,5 +31,7 @@ int attn_bwd_variant();
 void attn_set_bwd_variant(int v);
 int attn_fwd_variant();
 void attn_set_fwd_variant(int v);
+float attn_rescale_thr();
+void attn_set_rescale_thr(float t);
 
 }  // namespace ffk

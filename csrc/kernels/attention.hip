@@ -143,6 +143,27 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
   float m = -INFINITY, lsum = 0.f;
   const float sl2 = a.scale * LOG2E;
 
+  // This lane's fragment byte offsets inside a K / V tile image, computed once: the 32-row key
+  // half (kt), the V tile and the double-buffer slot are additive (ds_read immediates; the swizzle
+  // does not see row bit 5), only the swizzled chunk bits need a register each. Recomputing them
+  // per tile was ~100 of the loop's ~300 VALU instructions.
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  int ko[D / 16], vo[D / 32][2][2];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
+    asm volatile("" : "+v"(ko[s]));  // keep in a register (no per-tile rematerialisation)
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
+        asm volatile("" : "+v"(vo[dt][s2][hi]));
+      }
+
   int nkv = (a.Sk + KV - 1) / KV;
   if (a.causal) nkv = min(nkv, (min(qblk0 + 128, a.Sq) + KV - 1) / KV);
 
@@ -164,10 +185,13 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
     }
     __syncthreads();
   }
-  for (int t = 0; t < nkv; ++t) {
-    const char* kl = smem + (t & 1) * 2 * TB;
+  // one K/V tile; the double-buffer slot PAR is a compile-time constant (the loop below is unrolled
+  // by two) so that the slot base is an immediate of every ds_read, not a per-address add
+  auto tile = [&](auto par, int t) {
+    constexpr int PAR = decltype(par)::value;
+    const char* kl = smem + PAR * 2 * TB;
     const char* vl = kl + TB;
-    char* nk = smem + ((t + 1) & 1) * 2 * TB;
+    char* nk = smem + (PAR ^ 1) * 2 * TB;
     const bool more = t + 1 < nkv;
     if (more) {
       if (DMA) {
@@ -184,8 +208,7 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
     for (int s = 0; s < D / 16; ++s) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        const int row = 32 * kt + (lane & 31);
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + aoff<D>(row, 16 * s + 8 * h));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
         sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
       }
     }
@@ -210,45 +233,48 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kt][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-    const float mnew = fmaxf(m, mx);
-    const float msafe = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = fast_exp2(m - msafe);
-    float rs = 0.f;
+    // deferred max (cdna_hip_programming.md T13): the running max moves (and O / l are rescaled)
+    // only when some row's tile max exceeds it by more than a.rescale_thr (log2 units); otherwise P is
+    // taken against the old max and stays <= 2^rescale_thr. Decided before this tile's P exists, so
+    // nothing is ever at two scales.
+    if (!__all(mx <= m + a.rescale_thr)) {
+      const float mnew = fmaxf(m, mx);
+      const float alpha = fast_exp2(m - (mnew == -INFINITY ? 0.f : mnew));
+      lsum *= alpha;
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+      m = mnew;
+    }
+    const float msafe = m == -INFINITY ? 0.f : m;
+    float rs0 = 0.f, rs1 = 0.f;  // two chains: half the dependent-add latency
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = fast_exp2(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
         sacc[kt][r] = p;
-        rs += p;
+        if (r & 1) rs1 += p;
+        else rs0 += p;
       }
     }
+    float rs = rs0 + rs1;
     rs += __shfl_xor(rs, 32, 64);
-    lsum = lsum * alpha + rs;
-    m = mnew;
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+    lsum += rs;
     // O^T[d][q] += V^T[d][key] . P^T[key][q]
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) { pf[kt][0] = pack8(sacc[kt], 0); pf[kt][1] = pack8(sacc[kt], 8); }
-    const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt) {
-      const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const int r0 = 32 * kt + 16 * s2 + 4 * h + qi;
-          const bf16x4 lo = tr_read(vl, aoff<D>(r0, col));
-          const bf16x4 hi = tr_read(vl, aoff<D>(r0 + 8, col));
-          bf16x8 vf;
-          vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
-          vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
-          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s2], oacc[dt], 0, 0, 0);
+          const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
+          const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(lo, hi), pf[kt][s2], oacc[dt], 0, 0, 0);
         }
       }
     }
@@ -260,6 +286,10 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
       }
     }
     __syncthreads();
+  };
+  for (int t = 0; t < nkv; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nkv) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   // epilogue: O^T accumulators (lane = query row, d = 32dt + 8g + 4h + 0..3) -> [128 q][D] LDS
   // image (16-B chunks XOR-swizzled by row & 7) -> whole-row 16-B stores
@@ -927,9 +957,22 @@ int attn_fwd_variant() {
 }
 void attn_set_fwd_variant(int v) { g_fwd_variant = v; }
 
+// Deferred-max threshold of the forward (log2 units; 0 = rescale whenever a row max grows, the
+// textbook online softmax). Default 8 (P <= 256 in bf16 between rescales), FF_ATTN_RESCALE_THR.
+static float g_rescale_thr = -1.f;
+float attn_rescale_thr() {
+  if (g_rescale_thr < 0.f) {
+    const char* e = getenv("FF_ATTN_RESCALE_THR");
+    g_rescale_thr = e ? fmaxf(0.f, (float)atof(e)) : 8.f;
+  }
+  return g_rescale_thr;
+}
+void attn_set_rescale_thr(float t) { g_rescale_thr = fmaxf(0.f, t); }
+
 void attn_fwd(AttnArgs a, hipStream_t st) {
   const dim3 grid((unsigned)((a.Sq + 127) / 128 * a.B * a.H));
   const bool mask = a.causal || a.Sk % 64 != 0;
+  a.rescale_thr = attn_rescale_thr();
   // the DMA path needs 16-B aligned K / V rows and buffer offsets below 2 GiB
   const bool dma = attn_fwd_variant() == 1 && ((uintptr_t)a.k & 15) == 0 && ((uintptr_t)a.v & 15) == 0 &&
                    a.k_ss % 8 == 0 && a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&

@@ -34,7 +34,7 @@ T* ptr(const optional<Tensor>& t) {
 void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> Z, int64_t M, int64_t N,
           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sA, int64_t sB, int64_t sC, int64_t batch,
           bool a_k, bool b_k, double alpha, double beta, int64_t act, int64_t splitk, optional<Tensor> ws,
-          int64_t impl) {
+          int64_t impl, bool skip_reduce) {
   check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A/B must be bf16");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm: C must be bf16/fp32");
@@ -69,6 +69,7 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
                 "gemm: split-K workspace too small");
     p.splitk = splitk;
     p.ws = reinterpret_cast<float*>(ws->data_ptr());
+    p.skip_reduce = skip_reduce;
   }
   ffk::gemm_bf16(p, cur_stream());
 }
@@ -171,18 +172,27 @@ void dropout_bwd(Tensor dy, Tensor mask, Tensor dx, double rate, bool acc) {
   ffk::dropout_bwd(dtcode(dy), dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), rate, acc,
                    cur_stream());
 }
+int64_t bias_act_bwd_ws(int64_t rows, int64_t cols) { return (int64_t)ffk::bias_act_bwd_chunks(rows, cols) * cols; }
+
+// stage 0: row pass + slab fold; 1: row pass into `ws_in`; 2: slab fold of `ws_in` into dbias
 void bias_act_bwd(Tensor dy, optional<Tensor> z, optional<Tensor> dz, optional<Tensor> dbias, int64_t rows,
-                  int64_t cols, int64_t act) {
+                  int64_t cols, int64_t act, optional<Tensor> ws_in, int64_t stage) {
   TORCH_CHECK(dy.numel() == rows * cols);
   if (dbias.has_value() && dbias->defined()) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->numel() >= cols);
   Tensor ws;
   float* wsp = nullptr;
   if (dbias.has_value() && dbias->defined()) {
-    ws = at::empty({(int64_t)ffk::bias_act_bwd_chunks(rows, cols) * cols}, dy.options().dtype(at::kFloat));
+    if (ws_in.has_value() && ws_in->defined()) {
+      TORCH_CHECK(ws_in->scalar_type() == at::kFloat && ws_in->numel() >= bias_act_bwd_ws(rows, cols), "bias_act_bwd: ws");
+      ws = *ws_in;
+    } else {
+      TORCH_CHECK(stage == 0, "bias_act_bwd: a staged call needs its workspace");
+      ws = at::empty({bias_act_bwd_ws(rows, cols)}, dy.options().dtype(at::kFloat));
+    }
     wsp = ws.data_ptr<float>();
   }
   ffk::bias_act_bwd(dtcode(dy), dy.data_ptr(), ptr(z), ptr(dz), ptr<float>(dbias), wsp, rows, cols, act,
-                    cur_stream());
+                    cur_stream(), (int)stage);
 }
 void layernorm_fwd(Tensor x, optional<Tensor> res, optional<Tensor> sum_out, optional<Tensor> gamma,
                    optional<Tensor> beta, Tensor y, Tensor mean, Tensor rstd, int64_t rows, int64_t cols,
@@ -191,17 +201,27 @@ void layernorm_fwd(Tensor x, optional<Tensor> res, optional<Tensor> sum_out, opt
   ffk::layernorm_fwd(dtcode(x), x.data_ptr(), ptr(res), ptr(sum_out), ptr(gamma), ptr(beta), y.data_ptr(),
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, cols, eps, cur_stream());
 }
+int64_t layernorm_bwd_ws(int64_t rows, int64_t cols) {
+  return 3 * (int64_t)ffk::layernorm_bwd_waves(rows) * cols + (int64_t)ffk::bias_act_bwd_chunks(rows, cols) * cols;
+}
+
+// stage as bias_act_bwd's (the slab folds of dgamma / dbeta / dsum run in stage 2)
 void layernorm_bwd(Tensor dy, Tensor x, optional<Tensor> gamma, Tensor mean, Tensor rstd, Tensor dx,
                    optional<Tensor> dres, optional<Tensor> dgamma, optional<Tensor> dbeta, int64_t rows,
-                   int64_t cols, bool acc, optional<Tensor> dsum) {
+                   int64_t cols, bool acc, optional<Tensor> dsum, optional<Tensor> ws_in, int64_t stage) {
   TORCH_CHECK(dy.numel() == rows * cols && dx.numel() == rows * cols);
   TORCH_CHECK(!dsum || (dsum->scalar_type() == at::kFloat && dsum->numel() >= cols), "layernorm_bwd: dsum");
-  const int64_t nw = ffk::layernorm_bwd_waves(rows);
-  Tensor ws = at::empty({3 * nw * cols + ffk::bias_act_bwd_chunks(rows, cols) * cols},
-                        dy.options().dtype(at::kFloat));
+  Tensor ws;
+  if (ws_in.has_value() && ws_in->defined()) {
+    TORCH_CHECK(ws_in->scalar_type() == at::kFloat && ws_in->numel() >= layernorm_bwd_ws(rows, cols), "layernorm_bwd: ws");
+    ws = *ws_in;
+  } else {
+    TORCH_CHECK(stage == 0, "layernorm_bwd: a staged call needs its workspace");
+    ws = at::empty({layernorm_bwd_ws(rows, cols)}, dy.options().dtype(at::kFloat));
+  }
   ffk::layernorm_bwd(dtcode(dy), dy.data_ptr(), x.data_ptr(), ptr(gamma), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dx.data_ptr(), ptr(dres), ptr<float>(dgamma), ptr<float>(dbeta),
-                     ptr<float>(dsum), ws.data_ptr<float>(), rows, cols, acc, cur_stream());
+                     ptr<float>(dsum), ws.data_ptr<float>(), rows, cols, acc, cur_stream(), (int)stage);
 }
 void softmax_fwd(Tensor x, Tensor y, int64_t rows, int64_t cols, double scale) {
   TORCH_CHECK(x.numel() == rows * cols);
@@ -676,7 +696,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("Z"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("sA"), py::arg("sB"),
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
-        py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2);
+        py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2, py::arg("skip_reduce") = false);
   m.def("gemm_dact", &gemm_dact);
   m.def("lstm_fwd_cell", &lstm_fwd_cell);
   m.def("lstm_bwd_cell", &lstm_bwd_cell);
@@ -696,12 +716,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast", &cast);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
-  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("bias_act_bwd", &bias_act_bwd, py::arg("dy"), py::arg("z"), py::arg("dz"), py::arg("dbias"), py::arg("rows"),
+        py::arg("cols"), py::arg("act"), py::arg("ws") = py::none(), py::arg("stage") = 0);
+  m.def("bias_act_bwd_ws", &bias_act_bwd_ws);
+  m.def("layernorm_bwd_ws", &layernorm_bwd_ws);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("rows"),
-        py::arg("cols"), py::arg("acc"), py::arg("dsum") = py::none());
+        py::arg("cols"), py::arg("acc"), py::arg("dsum") = py::none(), py::arg("ws") = py::none(),
+        py::arg("stage") = 0);
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
   m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("loss"), py::arg("dlogits"),
@@ -739,6 +763,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd_variant", []() { return ffk::attn_fwd_variant(); });
   m.def("attn_set_fwd_variant", [](int v) { ffk::attn_set_fwd_variant(v); });
   m.def("attn_bwd_variant", []() { return ffk::attn_bwd_variant(); });
+  m.def("attn_rescale_thr", []() { return ffk::attn_rescale_thr(); });
+  m.def("attn_set_rescale_thr", [](double t) { ffk::attn_set_rescale_thr((float)t); });
   m.def("batchnorm_fwd", &batchnorm_fwd);
   m.def("batchnorm_bwd", &batchnorm_bwd);
   m.def("bn_ws", &bn_ws);

@@ -579,13 +579,19 @@ void bias_act_fwd(const void* z, const void* bias, int bias_bf16, void* zout, vo
 }
 
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
-                  int act, hipStream_t st) {
+                  int act, hipStream_t st, int stage) {
   if (rows == 0 || cols == 0) return;
   int gx, gy, rpb;
   bab_geometry(rows, cols, gx, gy, rpb);
+  // stage 0: both passes; 1: the row pass only (slab into ws); 2: the slab fold only (the caller
+  // queues it on a side stream: the bias gradient is needed by the optimizer, not by the backward)
+  if (stage == 2) {
+    if (dbias) col_reduce_add(ws, dbias, gy, cols, st);
+    return;
+  }
   if (dt == DT_BF16 && act == ACT_NONE && dbias && (cols & 7) && !(cols & 1) && ((uintptr_t)dy & 3) == 0) {
     hipLaunchKernelGGL(colsum_pairs_kernel, dim3(gx, gy), dim3(256), 0, st, (const bf16_t*)dy, ws, rows, cols, rpb);
-    col_reduce_add(ws, dbias, gy, cols, st);
+    if (stage == 0) col_reduce_add(ws, dbias, gy, cols, st);
     return;
   }
   FFK_DT_DISPATCH(dt, {
@@ -596,7 +602,7 @@ void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias,
       hipLaunchKernelGGL((bias_act_bwd_kernel<T, false>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy, (const T*)z,
                          (T*)dz, ws, rows, cols, act, rpb);
   });
-  if (dbias) col_reduce_add(ws, dbias, gy, cols, st);
+  if (dbias && stage == 0) col_reduce_add(ws, dbias, gy, cols, st);
 }
 
 }  // namespace ffk

@@ -33,6 +33,7 @@ struct GemmArgs {
   float* colpart = nullptr;
   bool dact = false;
   int ablate = 0;  // measurement builds only (impl 40 / 41 in the probes): see gemm_w4p.hip
+  bool skip_reduce = false;  // split-K: write the slabs only (the caller runs slab_sum, e.g. on a side stream)
 };
 
 void gemm_bf16(GemmArgs p, hipStream_t stream);

@@ -411,6 +411,7 @@ void gemm_bf16(GemmArgs p, hipStream_t stream) {
     p.kchunk = ((p.K + p.splitk - 1) / p.splitk + BK - 1) / BK * BK;
     dim3 grid(tm * tn, p.batch * p.splitk);
     if (!try_large(p, a_al, b_al, stream)) dispatch_layout<2>(p, grid, stream, a_al, b_al);
+    if (p.skip_reduce) return;
     const int64_t total = (int64_t)p.M * p.N * p.batch;
     if (p.out_f32 && p.batch == 1 && p.ldc == p.N && !p.bias && !p.Z && p.act == ACT_NONE && total % 4 == 0 &&
         aligned16(p.C) && aligned16(p.ws)) {

@@ -264,7 +264,7 @@ int layernorm_bwd_waves(int rows) { return std::max(1, std::min((rows + 15) / 16
 
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    void* dx, const void* dres_in, float* dgamma, float* dbeta, float* dsum, float* ws, int rows,
-                   int cols, int accumulate, hipStream_t st) {
+                   int cols, int accumulate, hipStream_t st, int stage) {
   if (rows == 0) return;
   const int esz = dt == DT_BF16 ? 2 : 4;
   const int V = 16 / esz;
@@ -280,6 +280,11 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   float* pd = dsum ? ws + 2 * (int64_t)nw * cols : nullptr;
   bool used_slab = false;
   const bool fused_ok = vec && nch <= 4;
+  if (stage == 2) {  // the slab folds only (bias_act_bwd's stage comment)
+    if (fused_ok) col_reduce_add3(ws, dgamma, dbeta, dsum, nw, cols, st);
+    else if (dsum) bias_act_bwd(dt, dx, nullptr, nullptr, dsum, ws + 2 * (int64_t)nw * cols, rows, cols, ACT_NONE, st, 2);
+    return;
+  }
 #define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 4 * cols * sizeof(float), st, (const T*)dy, (const T*)x, \
                                      (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, pd, rows, cols, accumulate); } while (0)
   if (dt == DT_BF16) {
@@ -295,10 +300,10 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
   }
 #undef LNB
   if (used_slab) {
-    col_reduce_add3(ws, dgamma, dbeta, dsum, nw, cols, st);
+    if (stage == 0) col_reduce_add3(ws, dgamma, dbeta, dsum, nw, cols, st);
   } else if (dsum) {
     // generic path (unaligned / very wide rows): the colsum as its own pass over the written dx
-    bias_act_bwd(dt, dx, nullptr, nullptr, dsum, ws + 2 * (int64_t)nw * cols, rows, cols, ACT_NONE, st);
+    bias_act_bwd(dt, dx, nullptr, nullptr, dsum, ws + 2 * (int64_t)nw * cols, rows, cols, ACT_NONE, st, stage);
   }
   (void)fused_ok;
 }

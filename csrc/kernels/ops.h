@@ -34,7 +34,7 @@ void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t 
 void bias_act_fwd(const void* z, const void* bias, int bias_bf16, void* zout, void* y, int64_t rows, int cols,
                   int act, hipStream_t st);
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
-                  int act, hipStream_t st);
+                  int act, hipStream_t st, int stage = 0);
 int bias_act_bwd_chunks(int rows, int cols);
 void col_reduce_add(const float* part, float* out, int R, int C, hipStream_t st);
 void slab_sum(const float* slabs, float* out, int64_t n, int S, float beta, hipStream_t st);
@@ -69,7 +69,7 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 // dsum (optional) += colsum(dx): the bias gradient of the Linear that produced the LN input.
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    void* dx, const void* dres_in, float* dgamma, float* dbeta, float* dsum, float* ws, int rows,
-                   int cols, int accumulate, hipStream_t st);
+                   int cols, int accumulate, hipStream_t st, int stage = 0);
 int layernorm_bwd_waves(int rows);
 
 // softmax.hip

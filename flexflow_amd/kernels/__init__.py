@@ -278,8 +278,21 @@ def _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, S):
     a3 = a2.as_strided((S, M, kc), (kc * a2.stride(1), a2.stride(0), a2.stride(1)))
     b3 = b2.as_strided((S, kc, N), (kc * b2.stride(0), b2.stride(0), b2.stride(1)))
     slabs = torch.empty((S, M, N), device=C.device, dtype=torch.float32)
+    if _fold_slabs_ok(C, None, None, ACT_NONE, 1, N, N, M, beta):
+        _fold(lambda: torch.bmm(a3, b3, out_dtype=torch.float32, out=slabs),
+              lambda: ext().slab_sum(slabs, C, S, beta), (slabs,))
+        return
     torch.bmm(a3, b3, out_dtype=torch.float32, out=slabs)
     ext().slab_sum(slabs, C, S, beta)
+
+
+def _fold_slabs_ok(C, bias, Z, act, batch, ldc, N, M, beta) -> bool:
+    """A split-K weight gradient's slab fold may leave the compute stream when the GEMM owns its
+    fp32 output (beta = 0: the weight's only user, nothing on the compute stream reads or adds to
+    it before the optimizer) and the fold is the plain slab_sum."""
+    return (_RED["stream"] is not None and beta == 0.0 and C.dtype == torch.float32 and bias is None and Z is None
+            and act == ACT_NONE and batch == 1 and ldc == N and C.is_contiguous() and (M * N) % 4 == 0
+            and not torch.cuda.is_current_stream_capturing())
 
 
 # ------------------------------------------------------------------ hipBLASLt, called directly
@@ -437,6 +450,11 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             ws = None
             if s > 1:
                 ws = torch.empty(M * N * batch * s, device=C.device, dtype=torch.float32)
+                if _fold_slabs_ok(out, bias, Z, act, batch, ldc, N, M, beta):
+                    _fold(lambda: X.gemm(A, B, out, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k,
+                                         alpha, beta, act, s, ws, impl, True),
+                          lambda: X.slab_sum(ws, out, s, beta), (ws,))
+                    return
             X.gemm(A, B, out, bias, Z, M, N, K, lda, ldb, ldc, sA, sB, sC, batch, a_k, b_k, alpha, beta, act,
                    s, ws, impl)
 
@@ -478,7 +496,11 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                     if bias is not None and act != ACT_NONE:
                         cands["lib_bias_act"] = lambda: _lib_gemm_bias_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda,
                                                                            ldb, bias, act)
-                times = _time_all(cands)
+                red, _RED["stream"] = _RED["stream"], None  # time every candidate with its folds inline
+                try:
+                    times = _time_all(cands)
+                finally:
+                    _RED["stream"] = red
                 if _LT and C.dtype in (torch.bfloat16, torch.float32):
                     _lt_candidates(A, B, C, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, Z, act,
                                    batch, sA, sB, sC, plain, times)
@@ -659,18 +681,62 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
     return dx
 
 
+# Deferred gradient reductions. The slab folds that finish a parameter gradient (bias / LayerNorm
+# column sums, split-K weight-gradient slabs) are needed by the optimizer, not by the rest of the
+# backward: while the executor runs an overlapped update it hands its side stream here, and the
+# folds queue on it (behind an event of the compute stream, ahead of the bucket updates queued
+# there later) instead of between the backward's GEMMs. set_reduce_stream(None) restores inline folds.
+_RED = {"stream": None, "deferred": 0}
+
+
+def set_reduce_stream(stream):
+    _RED["stream"] = stream
+
+
+def reductions_deferred() -> int:
+    return _RED["deferred"]
+
+
+def _fold(main, fold, keep=()):
+    """main() on the current stream, then fold() inline or on the reduction stream."""
+    main()
+    st = _RED["stream"]
+    if st is None:
+        fold()
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    with torch.cuda.stream(st):
+        st.wait_event(ev)
+        fold()
+    for t in keep:  # workspaces read on the side stream stay allocated until it has run
+        t.record_stream(st)
+    _RED["deferred"] += 1
+
+
 def bias_grad(dy2d, db):
     if native(dy2d):
-        ext().bias_act_bwd(dy2d, None, None, db, dy2d.shape[0], dy2d.shape[1], ACT_NONE)
+        _bias_act_bwd_dev(dy2d, None, None, db, ACT_NONE)
     else:
         db.add_(dy2d.float().sum(0))
+
+
+def _bias_act_bwd_dev(dy2d, z, dz, db, act):
+    X = ext()
+    rows, cols = dy2d.shape
+    if db is None or _RED["stream"] is None:
+        X.bias_act_bwd(dy2d, z, dz, db, rows, cols, act)
+        return
+    ws = torch.empty(int(X.bias_act_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)
+    _fold(lambda: X.bias_act_bwd(dy2d, z, dz, db, rows, cols, act, ws, 1),
+          lambda: X.bias_act_bwd(dy2d, z, dz, db, rows, cols, act, ws, 2), (ws,))
 
 
 def bias_act_bwd(dy2d, z, act, db):
     """dz = dy*act'(z); db += colsum(dz)."""
     if native(dy2d):
         dz = torch.empty_like(dy2d)
-        ext().bias_act_bwd(dy2d, z, dz, db, dy2d.shape[0], dy2d.shape[1], act)
+        _bias_act_bwd_dev(dy2d, z, dz, db, act)
         return dz
     dz = (dy2d.float() * act_grad_ref(z.float(), act)).to(dy2d.dtype)
     if db is not None:
@@ -757,8 +823,16 @@ def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None, dsum=
     gradient of the Linear feeding this LayerNorm, computed in the same pass."""
     rows, cols = dy2d.shape
     if native(dy2d):
+        X = ext()
         dx = torch.empty_like(dy2d)
-        ext().layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False, dsum)
+        if _RED["stream"] is None or (dgamma is None and dbeta is None and dsum is None):
+            X.layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False, dsum)
+            return dx
+        ws = torch.empty(int(X.layernorm_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)
+        _fold(lambda: X.layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False,
+                                      dsum, ws, 1),
+              lambda: X.layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False,
+                                      dsum, ws, 2), (ws, dx))
         return dx
     xh = (xs2d.float() - mean[:, None]) * rstd[:, None]
     dy = dy2d.float()

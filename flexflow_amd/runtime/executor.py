@@ -614,7 +614,31 @@ class Executor:
     def backward(self, overlap_update: bool = False):
         """overlap_update: update each gradient bucket as soon as it is final (see
         _on_bucket_ready); only train_step passes it, because the weights then change during
-        backward() — the separate backward()/update() API keeps the reference's semantics."""
+        backward() — the separate backward()/update() API keeps the reference's semantics.
+
+        With the overlapped update on one rank, the slab folds that finish parameter gradients
+        (bias / LayerNorm column sums, split-K weight-gradient slabs) also run on the update's side
+        stream, ahead of the bucket updates that read them (kernels.set_reduce_stream); every
+        reader of gradients on the compute stream joins that stream first (_join_folds).
+        FF_DEFER_FOLDS=0 keeps them inline."""
+        defer = (bool(overlap_update) and not self.comm.distributed and self._overlap_possible()
+                 and os.environ.get("FF_DEFER_FOLDS", "1") != "0")
+        if defer:
+            if self._upd_stream is None:
+                self._upd_stream = torch.cuda.Stream(device=self.device)
+            K.set_reduce_stream(self._upd_stream)
+            self._folds_pending = True
+        try:
+            return self._backward(overlap_update)
+        finally:
+            K.set_reduce_stream(None)
+
+    def _join_folds(self):
+        if getattr(self, "_folds_pending", False):
+            torch.cuda.current_stream(self.device).wait_stream(self._upd_stream)
+            self._folds_pending = False
+
+    def _backward(self, overlap_update: bool = False):
         if self._ag_pending:  # sharded optimizer: weights of layers this rank did not run
             self.wait_all_gathers()
         self.bucketer.reset()
@@ -892,6 +916,7 @@ class Executor:
         return out or None
 
     def zero_gradients(self):
+        self._join_folds()
         # tables updated by the row-sparse SGD had their touched gradient rows cleared by it
         skip = self._sparse_cleared if os.environ.get("FF_ZERO_ALL_GRADS") != "1" else {}
         self._sparse_cleared = {}
@@ -966,6 +991,7 @@ class Executor:
                 g.add_(torch.sign(m), alpha=l1)
 
     def update(self, optimizer):
+        self._join_folds()
         if self._ag_pending:
             self.wait_all_gathers()
         self.bucketer.flush()
@@ -1117,6 +1143,7 @@ class Executor:
         return self.gather_full(w, loc, self.weight_layout[w.guid].with_(partial=False), dtype=torch.float32)
 
     def get_weight_grad(self, w):
+        self._join_folds()
         loc = None
         if w.guid in self.weight_loc:
             loc = self.weight_loc[w.guid][0].views(self.weight_loc[w.guid][1])[1]

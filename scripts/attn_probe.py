@@ -52,6 +52,20 @@ for var in (0, 1):
           f"(rounds {[round(t, 4) for t in fres[var]]})")
 print(f"fwd variants identical: {torch.equal(fouts[0][0], fouts[1][0]) and torch.equal(fouts[0][1], fouts[1][1])}")
 X.attn_set_fwd_variant(default_fwd)
+# deferred-max threshold A/B (0 = textbook rescale on every max increase; default 8)
+default_thr = X.attn_rescale_thr()
+tres, touts = {0.0: [], default_thr: []}, {}
+for rnd in range(3):
+    for thr in tres:
+        X.attn_set_rescale_thr(thr)
+        Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
+        touts[thr] = o.clone()
+        tres[thr].append(timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)))
+for thr in tres:
+    ms = min(tres[thr])
+    print(f"attn fwd rescale_thr {thr}: {ms:.4f} ms {fl_f / ms / 1e9:.1f} TFLOPS (rounds {[round(t, 4) for t in tres[thr]]})")
+print(f"max |thr0 - thr{default_thr}|: {(touts[0.0].float() - touts[default_thr].float()).abs().max().item():.4g}")
+X.attn_set_rescale_thr(default_thr)
 lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
 # backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
 default_variant = X.attn_bwd_variant()

@@ -218,6 +218,44 @@ def test_flash_attention(ffC, S, D, causal, variant):
     ffC.attn_set_bwd_variant(prev_variant)
 
 
+@pytest.mark.parametrize("thr", [0.0, 3.0, 8.0])
+@pytest.mark.parametrize("ramp,causal", [(2.0, False), (-2.0, False), (6.0, True), (0.5, True)])
+def test_flash_attention_deferred_max(ffC, thr, ramp, causal):
+    """Forward deferred-max rescale (T13): scores ramp by `ramp` nats per 64-key tile, so the running
+    max grows past the threshold every few tiles (both the keep branch, with P up to 2^thr, and the
+    rescale branch run; ramp < 0: the first tile holds the max, no rescale after it). Output and
+    logsumexp against fp32 torch, and the backward from that lse."""
+    torch.manual_seed(11)
+    prev = ffC.attn_rescale_thr()
+    ffC.attn_set_rescale_thr(thr)
+    try:
+        B, H, S, D = 2, 2, 512, 64
+        scale = 0.125
+        base = torch.randn(D, device=DEV)
+        base = base / base.norm()
+        q = (torch.randn(B, H, S, D, device=DEV) * 0.2 + 8.0 * base).bfloat16()
+        steps = torch.arange(S, device=DEV, dtype=torch.float32) / 64 * ramp / scale / 8.0
+        k = (torch.randn(B, H, S, D, device=DEV) * 0.2 + steps[:, None] * base).bfloat16()
+        v = torch.randn(B, H, S, D, device=DEV).bfloat16()
+        o = torch.empty_like(q)
+        lse = torch.empty(B * H * S, device=DEV)
+        st = [H * S * D, S * D, D]
+        ffC.attn_fwd(q, st, k, st, v, st, o, st, lse, B, H, S, S, D, scale, causal)
+        qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+        ref, ref_lse = _attn_ref(qf, kf, vf, scale, causal)
+        assert _rel(o, ref) < 2e-2
+        assert _rel(lse.view(B, H, S), ref_lse) < 1e-3
+        do = torch.randn_like(q)
+        ref.backward(do.float())
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        ws = torch.empty(ffC.attn_bwd_ws(B, H, S, S, D), device=DEV)
+        ffC.attn_bwd(q, st, k, st, v, st, o, st, do, st, lse, dq, st, dk, st, dv, st, ws, B, H, S, S, D, scale, causal)
+        assert _rel(dv, vf.grad) < 3e-2
+        assert _rel(dq, qf.grad) < 5e-2
+    finally:
+        ffC.attn_set_rescale_thr(prev)
+
+
 def test_flash_attention_bwd_default_chain(ffC):
     """B*H >= 256 takes the chained backward by default (no dQ slabs, no finishing pass): BERT-Large
     attention shape with the fused [B,S,3,H,D] projection layout, against fp32 autograd."""
