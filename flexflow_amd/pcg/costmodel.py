@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from typing import Dict, Tuple
 
 import torch
@@ -66,61 +67,126 @@ def analytic_cost(layer, cfg: OpConfig, compute_dtype: DataType) -> Tuple[float,
     return t * 1e3, 2.0 * t * 1e3
 
 
-def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: int = 10) -> Tuple[float, float]:
-    """Time the op's own forward/backward on this GPU with the shard shapes of `cfg`."""
+def _step_layout(t):
+    """A 4-D activation as a training step holds it: channel-last when the kernels take it so
+    (kernels.cl_ok: bf16, channels % 8 == 0), so the isolated timing does not pay a layout
+    conversion the step never runs (CNN forwards were timed 2-4x slow, r4 calibration)."""
+    from .. import kernels as K
+    if t.dim() == 4 and K.cl_ok(t, t.shape[1]):
+        return t.contiguous(memory_format=torch.channels_last)
+    return t
+
+
+def _saturate(device):
+    """Keep the GPU busy while the timed launches are queued, so the events measure device time
+    and not Python launch overhead (in a training step the GPU runs behind the host: an op's
+    span is its kernels' time; isolated small ops were timed 3-5x too slow, r3/r4 calibration)."""
+    try:
+        torch.cuda._sleep(2_000_000)
+    except Exception:
+        pass
+
+
+def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: int = 8) -> Tuple[float, float]:
+    """Time the op's own forward/backward on this GPU with the shard shapes of `cfg`, the way a
+    training step runs it (reference simulator.cu measure_operator_cost; model.cu:38-75):
+      * `reps` forwards on distinct input copies, each saving into its own context, then the
+        `reps` backwards: a backward reads activations saved long before (cold caches), not the
+        ones its own forward just wrote;
+      * the input gradient only when the input has a producer (the executor's need_dx0);
+      * launches queued behind a device-side busy wait (_saturate)."""
     from ..ops import OpCtx
     lo = op_layouts(layer, cfg)
+    need_dx0 = bool(layer.inputs) and layer.inputs[0].owner_layer is not None and \
+        layer.inputs[0].owner_layer.op_type != OperatorType.OP_INPUT
     key = (layer.op_type, layer.impl.params_key(), tuple(l.local_shape(0) for l in lo.inputs),
-           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype)
+           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0)
     if key in _measured:
         return _measured[key]
     ct = torch.bfloat16 if compute_dtype == DataType.DT_BF16 else torch.float32
-    xs = []
-    for t, l in zip(layer.inputs, lo.inputs):
-        shp = l.local_shape(0)
-        if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
-            hi = 2
-            if layer.op_type == OperatorType.OP_EMBEDDING:
-                hi = layer.attrs["num_entries"] // max(1, cfg.degrees[-1])
-            xs.append(torch.randint(0, max(1, hi), shp, device=device, dtype=torch.int32))
-        else:
-            xs.append(torch.randn(shp, device=device, dtype=ct))
-    # identical tensors in the graph stay identical (fused self-attention)
-    seen = {}
-    for i, t in enumerate(layer.inputs):
-        if t.guid in seen and lo.inputs[i].key() == lo.inputs[seen[t.guid]].key():
-            xs[i] = xs[seen[t.guid]]
-        else:
-            seen.setdefault(t.guid, i)
+
+    def make_inputs():
+        xs = []
+        for t, l in zip(layer.inputs, lo.inputs):
+            shp = l.local_shape(0)
+            if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
+                hi = 2
+                if layer.op_type == OperatorType.OP_EMBEDDING:
+                    hi = layer.attrs["num_entries"] // max(1, cfg.degrees[-1])
+                xs.append(torch.randint(0, max(1, hi), shp, device=device, dtype=torch.int32))
+            else:
+                xs.append(_step_layout(torch.randn(shp, device=device, dtype=ct)))
+        # identical tensors in the graph stay identical (fused self-attention)
+        seen = {}
+        for i, t in enumerate(layer.inputs):
+            if t.guid in seen and lo.inputs[i].key() == lo.inputs[seen[t.guid]].key():
+                xs[i] = xs[seen[t.guid]]
+            else:
+                seen.setdefault(t.guid, i)
+        return xs
+
     ws = [torch.randn(l.local_shape(0), device=device, dtype=ct) * 0.02 for l in lo.weights]
-    ctx = OpCtx(layer=layer, part_coords=(0,) * len(cfg.degrees), degrees=cfg.degrees, compute_dtype=compute_dtype)
-    ctx.wgrads = [torch.zeros(w.shape, device=device, dtype=torch.float32) for w in ws]
-    ctx.extra["need_dx0"] = True
+    wgrads = [torch.zeros(w.shape, device=device, dtype=torch.float32) for w in ws]
     impl = layer.impl
 
-    def fwd():
-        return impl.forward(ctx, xs, ws)
+    fused_relu = relu_fused_into_producer(layer)
+    # the executor's backward fusions, as the step runs them
+    ln_fused = ln_bias_fusion_producer(layer)
+    ln_db = torch.zeros(layer.inputs[0].dims[-1], device=device, dtype=torch.float32) if ln_fused is not None else None
+    bias_fused = bias_grad_fused_away(layer)
+
+    def make_ctx():
+        ctx = OpCtx(layer=layer, part_coords=(0,) * len(cfg.degrees), degrees=cfg.degrees,
+                    compute_dtype=compute_dtype)
+        ctx.wgrads = wgrads
+        ctx.extra["need_dx0"] = need_dx0
+        if fused_relu:
+            ctx.extra["fused_into_producer"] = True
+        if ln_fused is not None:
+            ctx.extra["colsum_out"] = ln_db
+        if bias_fused:
+            ctx.extra["bias_grad_fused"] = True
+        return ctx
 
     try:
-        outs = fwd()
-        douts = [torch.randn_like(o) if o.is_floating_point() else None for o in outs]
-        impl.backward(ctx, douts)
+        # warm-up (kernel selection / tuning happens here, outside the timing)
+        c0, x0 = make_ctx(), make_inputs()
+        outs = impl.forward(c0, x0, ws)
+        douts = [_step_layout(torch.randn(o.shape, device=o.device, dtype=o.dtype)) if o.is_floating_point()
+                 else None for o in outs]
+        impl.backward(c0, douts)
+        del c0, x0, outs
+        in_bytes = sum(math.prod(l.local_shape(0)) for l in lo.inputs) * (2 if ct == torch.bfloat16 else 4)
+        n = max(2, min(reps, int(math.ceil(768e6 / max(in_bytes, 1)))))  # copies past the 256 MB MALL
+        xs_all = [make_inputs() for _ in range(n)]
+        ctxs = [make_ctx() for _ in range(n)]
         torch.cuda.synchronize()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # device time (queue saturated) and host time (the op's own dispatch): an eager step runs
+        # an op no faster than the host issues it, so the cost is the larger of the two
+        # forward on n distinct input copies, each saving into its own context: in a step the
+        # inputs of most ops were written long enough before to be out of the caches (timing the
+        # forward on one cache-warm input made LayerNorm 16 % and Embedding 17 % fast, r4)
+        _saturate(device)
         st.record()
-        for _ in range(reps):
-            fwd()
-            ctx.saved.clear()
+        h0 = time.perf_counter()
+        for c, xs in zip(ctxs, xs_all):
+            impl.forward(c, xs, ws)
+        hf = (time.perf_counter() - h0) * 1e3 / n
         en.record()
         en.synchronize()
-        tf = st.elapsed_time(en) / reps
+        tf = max(st.elapsed_time(en) / n, hf)
+        # the backward on those n contexts: the activations they saved are cold too
+        _saturate(device)
         st.record()
-        for _ in range(reps):
-            fwd()
-            impl.backward(ctx, douts)
+        h0 = time.perf_counter()
+        for c in ctxs:
+            impl.backward(c, douts)
+        hb = (time.perf_counter() - h0) * 1e3 / n
         en.record()
         en.synchronize()
-        tb = max(st.elapsed_time(en) / reps - tf, 0.0)
+        tb = max(st.elapsed_time(en) / n, hb)
+        del ctxs, xs_all
     except Exception:
         tf, tb = analytic_cost(layer, cfg, compute_dtype)
     _measured[key] = (tf, tb)
@@ -167,27 +233,109 @@ def fused_xent_cost(layer, cfg: OpConfig, compute_dtype: DataType, measure: bool
             from .. import kernels as K
             x = torch.randn(rows, V, device=device, dtype=torch.bfloat16)
             lab = torch.randint(0, V, (rows,), device=device, dtype=torch.int32)
-            acc = torch.zeros(3, device=device, dtype=torch.float32)
-            K.softmax_xent(x, lab, 1.0, acc)
+            lab64 = lab.long()
+            macc = torch.zeros(8, device=device, dtype=torch.float32)
+
+            def loss_pass():  # what executor.compute_loss_grad launches around the fused kernel
+                acc = torch.zeros(3, dtype=torch.float32, device=device)
+                g, _ = K.softmax_xent(x, lab64.reshape(-1).to(torch.int32), 1.0, acc)
+                macc[0] += acc[1]
+                return g
+
+            loss_pass()
             torch.cuda.synchronize()
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            _saturate(device)
             st.record()
+            h0 = time.perf_counter()
             for _ in range(5):
-                K.softmax_xent(x, lab, 1.0, acc)
+                loss_pass()
+            hf = (time.perf_counter() - h0) * 1e3 / 5
             en.record()
             en.synchronize()
-            _measured[key] = (st.elapsed_time(en) / 5, 0.0)
+            _measured[key] = (max(st.elapsed_time(en) / 5, hf), 0.0)
         return _measured[key]
     elem = 2 if compute_dtype == DataType.DT_BF16 else 4
     t = 2.0 * rows * V * elem / HBM + LAUNCH_S
     return t * 1e3, 0.0
 
 
+def relu_fused_into_producer(layer) -> bool:
+    """The executor applies a ReLU inside the element-wise binary op that produces its input
+    (runtime/executor._plan_inplace + _plan_binary_relu: ResNet's residual add + ReLU) when that
+    input has no other reader and the producer's backward does not need it: the ReLU's forward is
+    then free (its backward still runs). Same conditions, decided from the graph alone."""
+    if layer.op_type != OperatorType.OP_RELU or len(layer.inputs) != 1 or os.environ.get("FF_NO_BINARY_RELU") == "1":
+        return False
+    from ..ops.elementwise import BINARY
+    t = layer.inputs[0]
+    P = t.owner_layer
+    m = getattr(layer, "model", None)
+    if P is None or P.op_type not in BINARY or m is None or len(P.outputs) != 1:
+        return False
+    if P.impl.saves_output() or t.data_type != layer.outputs[0].data_type:
+        return False
+    out = m.output_tensor()
+    if out is not None and out.guid == t.guid:
+        return False
+    readers = sum(1 for L in m.layers for x in L.inputs if x.guid == t.guid)
+    return readers == 1
+
+
+# Per-op, per-phase floor of an eagerly executed step: the host-side dispatch of one op (Python op
+# call, transfers' bookkeeping, kernel launch) when its kernels are shorter than that, measured as
+# the in-step span of ops that do no GPU work (flatten, the fused ReLU, a residual add's backward:
+# 4.7-6 us; profiles/sim_calibration_*_r4.txt). FF_SIM_OP_FLOOR_US overrides (e.g. ~1 for a
+# step replayed from a hipGraph).
+OP_FLOOR_MS = float(os.environ.get("FF_SIM_OP_FLOOR_US", "5.0")) * 1e-3
+
+
+def _sole_reader(t, m):
+    return sum(1 for L in m.layers for x in L.inputs if x.guid == t.guid) == 1
+
+
+def ln_bias_fusion_producer(layer):
+    """The producer whose bias gradient a LayerNorm's backward sums for it (executor
+    _plan_bias_grad_fusion: a Linear without activation, or an attention's out-projection, whose
+    output only this LayerNorm reads), or None."""
+    m = getattr(layer, "model", None)
+    if layer.op_type != OperatorType.OP_LAYERNORM or m is None or os.environ.get("FF_NO_BIAS_FUSION") == "1":
+        return None
+    out = m.output_tensor()
+    for t in layer.inputs:
+        P = t.owner_layer
+        if P is None or not _sole_reader(t, m) or (out is not None and out.guid == t.guid):
+            continue
+        if P.op_type == OperatorType.OP_LINEAR and P.impl.act == 10 and len(P.weights) > 1:
+            return P
+        if P.op_type == OperatorType.OP_MULTIHEAD_ATTENTION and P.attrs.get("bias", True):
+            return P
+    return None
+
+
+def bias_grad_fused_away(layer) -> bool:
+    """The op's own bias-gradient pass is done by the LayerNorm that consumes its output."""
+    m = getattr(layer, "model", None)
+    if m is None or layer.op_type not in (OperatorType.OP_LINEAR, OperatorType.OP_MULTIHEAD_ATTENTION):
+        return False
+    o = layer.outputs[0]
+    for L in m.layers:
+        if L.op_type == OperatorType.OP_LAYERNORM and any(x.guid == o.guid for x in L.inputs):
+            return ln_bias_fusion_producer(L) is layer
+    return False
+
+
 def op_cost(layer, cfg: OpConfig, compute_dtype: DataType, measure: bool, device=None):
     if layer.op_type == OperatorType.OP_INPUT:
         return 0.0, 0.0
-    if _loss_fused_softmax(layer):
-        return fused_xent_cost(layer, cfg, compute_dtype, measure, device)
-    if measure and device is not None and device.type == "cuda":
-        return measure_cost(layer, cfg, compute_dtype, device)
-    return analytic_cost(layer, cfg, compute_dtype)
+    on_gpu = measure and device is not None and device.type == "cuda"
+    if relu_fused_into_producer(layer):
+        f, b = (measure_cost(layer, cfg, compute_dtype, device) if on_gpu else analytic_cost(layer, cfg, compute_dtype))
+        f = 0.0
+    elif _loss_fused_softmax(layer):
+        f, b = fused_xent_cost(layer, cfg, compute_dtype, measure, device)
+    elif on_gpu:
+        f, b = measure_cost(layer, cfg, compute_dtype, device)
+    else:
+        f, b = analytic_cost(layer, cfg, compute_dtype)
+    return max(f, OP_FLOOR_MS), max(b, OP_FLOOR_MS)

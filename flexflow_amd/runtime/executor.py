@@ -663,7 +663,14 @@ class Executor:
                 grads[guid] = v if (prev is None or prev is v) else prev + v
 
         if self.output_tensor is not None and self.loss_type is not None:
-            g = self.compute_loss_grad()
+            owner = self.output_tensor.owner_layer
+            if self.softmax_fused and self.hooks and owner is not None:
+                # the fused softmax-cross-entropy pass IS the output softmax's work (the simulator
+                # books it there: pcg/costmodel.fused_xent_cost): profile it under that op
+                with self._hooked(owner, "fwd"):
+                    g = self.compute_loss_grad()
+            else:
+                g = self.compute_loss_grad()
             if g is not None:
                 grads[self.output_tensor.guid] = g
         for L in reversed(self.layers):

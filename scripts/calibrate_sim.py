@@ -105,6 +105,15 @@ upd_pred = sim.makespan_ms - tot_pred_ops
 print(f"{'ops total':28s} {'':4s} {tot_pred_ops:9.3f} {tot_meas_ops:9.3f}  (fwd+bwd, pred vs measured per-op sums)")
 print(f"simulated step {sim.makespan_ms:.3f} ms (ops {tot_pred_ops:.3f} + update/sync {upd_pred:.3f}) "
       f"vs measured step {step_ms:.3f} ms: error {100 * (sim.makespan_ms / step_ms - 1):+.1f}%")
+# per-op detail: the largest absolute disagreements (what a per-class error is made of)
+det = []
+for name, (op, f, b) in pred.items():
+    m = meas.get(name, {"fwd_ms": 0.0, "bwd_ms": 0.0})
+    det.append((abs(f - m["fwd_ms"]) + abs(b - m["bwd_ms"]), name, op, f, m["fwd_ms"], b, m["bwd_ms"]))
+det.sort(reverse=True)
+print("largest per-op disagreements (ms): name op pred_fwd meas_fwd pred_bwd meas_bwd")
+for d, name, op, f, mf, b, mb in det[:12]:
+    print(f"  {name:34s} {op:24s} {f:8.3f} {mf:8.3f} {b:8.3f} {mb:8.3f}")
 print(json.dumps({"model": model, "batch": batch, "measured_step_ms": round(step_ms, 3),
                   "simulated_step_ms": round(sim.makespan_ms, 3),
                   "error_pct": round(100 * (sim.makespan_ms / step_ms - 1), 2),
