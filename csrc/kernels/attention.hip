@@ -322,6 +322,235 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
   }
 }
 
+// ------------------------------------------------------------------------ forward, ping-pong
+// 8 waves, 256 query rows per workgroup: group A = waves 0-3 (rows 0-127), group B = waves 4-7
+// (rows 128-255), one wave of each group per SIMD. Each K/V tile is two barrier-separated
+// segments in which the two groups do opposite work, so one wave of every SIMD issues MFMAs while
+// its partner runs the softmax VALU (cdna_hip_programming.md 'Two waves per SIMD'):
+//   segment 1 of tile t:  A: softmax(t)                   B: [P(t-1) V(t-1)], S(t) = Q K(t)^T
+//   segment 2 of tile t:  A: P(t) V(t), S(t+1)            B: softmax(t)
+// The one-group-per-segment structure of the 4-wave kernel above left the MFMA pipe idle while a
+// wave's softmax ran (its waves only overlapped by chance across workgroups). K and V slots rotate
+// independently (V(t+1) and K(t+2) are requested at the start of segment 2 of tile t, into the
+// slots their predecessors left in segment 1, and waited for at the end of segment 1 of t+1), so
+// one 32-KiB double-buffered image serves both groups. The per-wave softmax, T13 deferred max, LDS
+// images and fragment offsets are those of attn_fwd_kernel.
+// Measured (profiles/attn_fwd_pingpong_r4.txt): bitwise equal to the 4-wave kernel but 5-20 %
+// slower at D = 64 for S = 256..4096 (one or two 256-row workgroups per CU pay the per-block Q load
+// and first K/V tiles in more rounds, and each segment lasts as long as its slower group); at
+// D = 128 (spills at 128 registers) 3-4x slower, so only D = 64 is built. Opt-in: variant 2.
+template <int D, bool MASK>
+__global__ void __launch_bounds__(512, 4) attn_fwd_pp_kernel(AttnArgs a) {
+  constexpr int KV = 64;
+  constexpr int TB = KV * D * 2;
+  constexpr int QB = 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // K slots at 0, TB; V slots at 2TB, 3TB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bool grpB = wave >= 4;
+  const int nqb = (a.Sq + QB - 1) / QB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = lid / nqb, b = bh / a.H, hh = bh % a.H;
+  const int qblk0 = (lid % nqb) * QB;
+  const int q0 = qblk0 + wave * 32;
+  const int qrow = q0 + (lane & 31);
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qrow < a.Sq) qf[s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
+    else qf[s] = bf16x8{};
+  }
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+  const float sl2 = a.scale * LOG2E;
+
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  int ko[D / 16], vo[D / 32][2][2];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
+    asm volatile("" : "+v"(ko[s]));
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
+        asm volatile("" : "+v"(vo[dt][s2][hi]));
+      }
+
+  int nkv = (a.Sk + KV - 1) / KV;
+  if (a.causal) nkv = min(nkv, (min(qblk0 + QB, a.Sq) + KV - 1) / KV);
+  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
+  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, kb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, vb, 0x00020000);
+
+  f32x16 sacc[2];
+  bf16x8 pf[2][2];
+  // S(t) = Q K(t)^T from K slot KS
+  auto qk = [&](auto ks_c) __attribute__((always_inline)) {
+    constexpr int KS = decltype(ks_c)::value;
+    const char* kl = smem + KS * TB;
+    sacc[0] = f32x16{};
+    sacc[1] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
+      }
+  };
+  // O += P(t) V(t) from V slot VS
+  auto pv = [&](auto vs_c) __attribute__((always_inline)) {
+    constexpr int VS = decltype(vs_c)::value;
+    const char* vl = smem + (2 + VS) * TB;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
+          const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(lo, hi), pf[kt][s2], oacc[dt], 0, 0, 0);
+        }
+  };
+  // online softmax of sacc (tile t) -> pf
+  auto softmax = [&](int t) __attribute__((always_inline)) {
+    const int kbase = t * KV;
+    const bool need_mask = MASK && ((kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0));
+    if (need_mask) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (key >= a.Sk || (a.causal && key > qrow)) sacc[kt][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kt][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+    if (!__all(mx <= m + a.rescale_thr)) {
+      const float mnew = fmaxf(m, mx);
+      const float alpha = fast_exp2(m - (mnew == -INFINITY ? 0.f : mnew));
+      lsum *= alpha;
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+      m = mnew;
+    }
+    const float msafe = m == -INFINITY ? 0.f : m;
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fast_exp2(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
+        sacc[kt][r] = p;
+        if (r & 1) rs1 += p;
+        else rs0 += p;
+      }
+    float rs = rs0 + rs1;
+    rs += __shfl_xor(rs, 32, 64);
+    lsum += rs;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) { pf[kt][0] = pack8(sacc[kt], 0); pf[kt][1] = pack8(sacc[kt], 8); }
+  };
+  auto dma_k = [&](int slot, int t) __attribute__((always_inline)) {
+    dma_tile<D, 8>(rk, smem + slot * TB, a.k_ss, t * KV, wave, lane);
+  };
+  auto dma_v = [&](int slot, int t) __attribute__((always_inline)) {
+    dma_tile<D, 8>(rv, smem + (2 + slot) * TB, a.v_ss, t * KV, wave, lane);
+  };
+  auto raw_barrier = []() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (nkv > 0) {
+    dma_k(0, 0);
+    dma_v(0, 0);
+    if (nkv > 1) dma_k(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (!grpB) qk(std::integral_constant<int, 0>());
+  }
+  // tile t with PAR = t & 1 (K(t), V(t) in slot PAR)
+  auto tile = [&](auto par_c, int t) __attribute__((always_inline)) {
+    constexpr int PAR = decltype(par_c)::value;
+    // segment 1
+    if (!grpB) {
+      softmax(t);
+    } else {
+      if (t > 0) pv(std::integral_constant<int, PAR ^ 1>());
+      qk(std::integral_constant<int, PAR>());
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V(t) and K(t+1), requested in segment 2 of t-1
+    raw_barrier();
+    // segment 2: V(t+1) into the slot V(t-1) left, K(t+2) into K(t)'s
+    if (t + 1 < nkv) dma_v(PAR ^ 1, t + 1);
+    if (t + 2 < nkv) dma_k(PAR, t + 2);
+    if (!grpB) {
+      pv(std::integral_constant<int, PAR>());
+      if (t + 1 < nkv) qk(std::integral_constant<int, PAR ^ 1>());
+    } else {
+      softmax(t);
+    }
+    raw_barrier();
+  };
+  for (int t = 0; t < nkv; t += 2) {
+    tile(std::integral_constant<int, 0>(), t);
+    if (t + 1 < nkv) tile(std::integral_constant<int, 1>(), t + 1);
+  }
+  if (grpB && nkv > 0) {
+    if ((nkv - 1) & 1) pv(std::integral_constant<int, 1>());
+    else pv(std::integral_constant<int, 0>());
+  }
+  // epilogue: as attn_fwd_kernel, 256 rows through the (now free) 32-KiB image
+  __syncthreads();
+  {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const int row = wave * 32 + (lane & 31);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 4 * dt + g;
+        *reinterpret_cast<uint2*>(smem + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
+            make_uint2((unsigned)f2bf(oacc[dt][4 * g] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 1] * inv) << 16),
+                       (unsigned)f2bf(oacc[dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 3] * inv) << 16));
+      }
+    if (h == 0 && a.lse && qrow < a.Sq) a.lse[(int64_t)bh * a.Sq + qrow] = lsum > 0.f ? (m * LN2 + __logf(lsum)) : INFINITY;
+  }
+  __syncthreads();
+  {
+    constexpr int CPR = D / 8;
+    bf16_t* Ob = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh;
+#pragma unroll
+    for (int i = 0; i < QB * CPR / 512; ++i) {
+      const int id = tid + i * 512, r = id / CPR, c = id % CPR;
+      if (qblk0 + r < a.Sq)
+        *reinterpret_cast<uint4*>(Ob + (int64_t)(qblk0 + r) * a.o_ss + 8 * c) =
+            *reinterpret_cast<const uint4*>(smem + r * (D * 2) + ((c ^ (r & 7)) << 4));
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ backward
 // delta[bh][q] = sum_d dO[q][d] * O[q][d]
 template <int D>
@@ -945,8 +1174,9 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
-// Forward K/V staging at D = 64: 1 = LDS-DMA (default), 0 = through registers (attn_set_fwd_variant;
-// default from FF_ATTN_FWD).
+// Forward structure: 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64 / 128), 1 = 4-wave with
+// LDS-DMA K/V staging (default), 0 = 4-wave through registers (attn_set_fwd_variant; default from
+// FF_ATTN_FWD).
 static int g_fwd_variant = -1;
 int attn_fwd_variant() {
   if (g_fwd_variant < 0) {
@@ -974,9 +1204,18 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   const bool mask = a.causal || a.Sk % 64 != 0;
   a.rescale_thr = attn_rescale_thr();
   // the DMA path needs 16-B aligned K / V rows and buffer offsets below 2 GiB
-  const bool dma = attn_fwd_variant() == 1 && ((uintptr_t)a.k & 15) == 0 && ((uintptr_t)a.v & 15) == 0 &&
-                   a.k_ss % 8 == 0 && a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
-                   (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
+  const bool dma_ok = ((uintptr_t)a.k & 15) == 0 && ((uintptr_t)a.v & 15) == 0 && a.k_ss % 8 == 0 &&
+                      a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
+                      (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
+  const bool dma = attn_fwd_variant() >= 1 && dma_ok;
+  if (attn_fwd_variant() == 2 && dma_ok) {  // 8-wave ping-pong (attn_fwd_pp_kernel), D = 64 only
+    const dim3 g2((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
+    if (a.D == 64) {
+      if (mask) hipLaunchKernelGGL((attn_fwd_pp_kernel<64, true>), g2, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_pp_kernel<64, false>), g2, dim3(512), 0, st, a);
+      return;
+    }
+  }
   if (a.D == 64) {
     if (dma) {
       if (mask) hipLaunchKernelGGL((attn_fwd_kernel<64, true, true>), grid, dim3(256), 0, st, a);
