@@ -719,6 +719,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_act_bwd", &bias_act_bwd, py::arg("dy"), py::arg("z"), py::arg("dz"), py::arg("dbias"), py::arg("rows"),
         py::arg("cols"), py::arg("act"), py::arg("ws") = py::none(), py::arg("stage") = 0);
   m.def("bias_act_bwd_ws", &bias_act_bwd_ws);
+  m.def("col_reduce_add3", [](Tensor part, c10::optional<Tensor> o0, c10::optional<Tensor> o1, c10::optional<Tensor> o2,
+                              int64_t R, int64_t C) {
+    TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= 3 * R * C || part.numel() >= R * C, "col_reduce_add3: part");
+    auto fp = [](c10::optional<Tensor>& t) { return t ? t->data_ptr<float>() : (float*)nullptr; };
+    ffk::col_reduce_add3(part.data_ptr<float>(), fp(o0), fp(o1), fp(o2), (int)R, (int)C, cur_stream());
+  });
+  m.def("col_reduce_set_gy", [](int64_t g) { ffk::col_reduce_set_gy((int)g); });
+  m.def("col_reduce_gy", []() { return ffk::col_reduce_gy(); });
   m.def("layernorm_bwd_ws", &layernorm_bwd_ws);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("layernorm_fwd", &layernorm_fwd);

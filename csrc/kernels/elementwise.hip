@@ -389,6 +389,50 @@ __global__ void col_reduce_add_kernel(const float* __restrict__ part, Outs3 o, i
   }
 }
 
+// Deterministic variant (gy = 0): one 1024-thread block per 64 columns and output, 16 row lanes
+// summed in a fixed order, a plain read-modify-write of the output (no float atomics: the atomic
+// form's adds contended with the overlapped optimizer's traffic in the step, 6 us median but up to
+// 150 us per call, and its sum order varied run to run).
+__global__ void __launch_bounds__(1024) col_reduce_det_kernel(const float* __restrict__ part, Outs3 o, int R, int C) {
+  __shared__ float red[16][65];
+  const int k = o.which[blockIdx.y];
+  const float* p = part + (int64_t)k * R * C;
+  float* out = o.p[k];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  float s = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < C) {
+    int r = rl;
+    for (; r + 48 < R; r += 64) {
+      s += p[(int64_t)r * C + c];
+      s1 += p[(int64_t)(r + 16) * C + c];
+      s2 += p[(int64_t)(r + 32) * C + c];
+      s3 += p[(int64_t)(r + 48) * C + c];
+    }
+    for (; r < R; r += 16) s += p[(int64_t)r * C + c];
+  }
+  red[rl][threadIdx.x & 63] = (s + s1) + (s2 + s3);
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+    out[c] += t;
+  }
+}
+
+// row chunks per column block (atomic adders per output address); 0 = the deterministic kernel
+// above (default); FF_COLRED_GY / col_reduce_set_gy
+static int g_cr_gy = -1;
+int col_reduce_gy() {
+  if (g_cr_gy < 0) {
+    const char* e = getenv("FF_COLRED_GY");
+    g_cr_gy = e ? std::max(0, atoi(e)) : 0;
+  }
+  return g_cr_gy;
+}
+void col_reduce_set_gy(int g) { g_cr_gy = std::max(0, g); }
+
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st) {
   if (R == 0 || C == 0) return;
   Outs3 o{{out0, out1, out2}, {0, 0, 0}};
@@ -396,7 +440,11 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
   for (int k = 0; k < 3; ++k)
     if (o.p[k]) o.which[nz++] = k;
   if (!nz) return;
-  const int gy = std::max(1, std::min(32, R / 8));
+  if (col_reduce_gy() == 0) {
+    hipLaunchKernelGGL(col_reduce_det_kernel, dim3((C + 63) / 64, nz), dim3(1024), 0, st, part, o, R, C);
+    return;
+  }
+  const int gy = std::max(1, std::min(col_reduce_gy(), R / 8));
   hipLaunchKernelGGL(col_reduce_add_kernel, dim3((C + 63) / 64, gy, nz), dim3(256), 0, st, part, o, R, C);
 }
 void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st) {

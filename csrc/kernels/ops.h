@@ -41,6 +41,8 @@ void slab_sum(const float* slabs, float* out, int64_t n, int S, float beta, hipS
 // out0 += colsum(part[0:R]); out1 += colsum(part[R:2R]) (out1 may be null)
 void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, hipStream_t st);
 // out_k += colsum(part[k*R:(k+1)*R]) for each non-null out_k, k < 3 (slab k at offset k*R*C)
+int col_reduce_gy();
+void col_reduce_set_gy(int g);
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st);
 
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully

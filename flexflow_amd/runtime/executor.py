@@ -616,13 +616,16 @@ class Executor:
         _on_bucket_ready); only train_step passes it, because the weights then change during
         backward() — the separate backward()/update() API keeps the reference's semantics.
 
-        With the overlapped update on one rank, the slab folds that finish parameter gradients
-        (bias / LayerNorm column sums, split-K weight-gradient slabs) also run on the update's side
-        stream, ahead of the bucket updates that read them (kernels.set_reduce_stream); every
-        reader of gradients on the compute stream joins that stream first (_join_folds).
-        FF_DEFER_FOLDS=0 keeps them inline."""
+        FF_DEFER_FOLDS=1 (with the overlapped update on one rank): the slab folds that finish
+        parameter gradients (bias / LayerNorm column sums, split-K weight-gradient slabs) run on the
+        update's side stream, ahead of the bucket updates that read them
+        (kernels.set_reduce_stream); every reader of gradients on the compute stream joins that
+        stream first (_join_folds). Off by default: same-box A/B at BERT-Large b32 measured no step
+        gain (45.74-45.75 vs 45.78-45.83 ms, profiles/defer_folds_ab_r4.txt) — the folds are
+        bandwidth-light but launch-bound, and running them beside the backward stretched them
+        (col_reduce 1.4 -> 6.4 ms of busy time per step, bert_large_b32_r4_v2_steps.txt)."""
         defer = (bool(overlap_update) and not self.comm.distributed and self._overlap_possible()
-                 and os.environ.get("FF_DEFER_FOLDS", "1") != "0")
+                 and os.environ.get("FF_DEFER_FOLDS", "0") == "1")
         if defer:
             if self._upd_stream is None:
                 self._upd_stream = torch.cuda.Stream(device=self.device)

@@ -4,6 +4,7 @@ every batch must reach the GPU shard in order, across epoch boundaries), and the
 workspace arena."""
 import numpy as np
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 
@@ -155,10 +156,12 @@ def test_graph_trial_policy_matches_eager():
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5, err_msg=str(k))
 
 
-def test_begin_end_trace_replays_hipgraph():
+@pytest.mark.parametrize("model", ["candle_uno", "dlrm"])
+def test_begin_end_trace_replays_hipgraph(model):
     """FFConfig.begin_trace / end_trace (reference: Legion tracing): from the third iteration the
     recorded forward / zero_gradients / backward sequence replays as one hipGraph; weights after 6
-    iterations match an untraced eager run."""
+    iterations match an untraced eager run. DLRM under SGD takes the row-sparse embedding update,
+    whose host bookkeeping a replay would skip: its trace runs eagerly (same weights)."""
     from flexflow_amd.core import FFConfig, FFModel, SGDOptimizer
     from flexflow_amd.models import build
 
@@ -166,7 +169,7 @@ def test_begin_end_trace_replays_hipgraph():
         cfg = FFConfig(["--dtype", "bf16"] + ([] if trace else ["--no-hip-graphs"]))
         cfg.batch_size = 64
         ff = FFModel(cfg)
-        inputs, out, loss, mets, make_batch = build("dlrm", ff, 64, small=True)
+        inputs, out, loss, mets, make_batch = build(model, ff, 64, small=True)
         ff.optimizer = SGDOptimizer(ff, 0.05)
         ff.compile(loss_type=loss, metrics=mets)
         rng = np.random.default_rng(0)
@@ -187,7 +190,45 @@ def test_begin_end_trace_replays_hipgraph():
 
     cfg, a = run(True)
     st = cfg._trace_state[111]
-    assert st.graph is not None and not st.off and st.seq == ["forward", "zero_gradients", "backward"]
+    assert st.seq == ["forward", "zero_gradients", "backward"]
+    if model == "dlrm":
+        assert st.graph is None and st.off
+    else:
+        assert st.graph is not None and not st.off
     _, b = run(False)
     for k, (x, y) in enumerate(zip(a, b)):
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5, err_msg=str(k))
+
+
+def test_deferred_gradient_folds_match_inline(monkeypatch):
+    """FF_DEFER_FOLDS=1: the bias / LayerNorm column folds and split-K slab sums of the backward
+    run on the overlapped update's side stream (executor.backward). Weights after 4 train steps of
+    a small BERT equal the inline-fold run's (same kernels, same order per gradient)."""
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(defer):
+        monkeypatch.setenv("FF_DEFER_FOLDS", "1" if defer else "0")
+        cfg = FFConfig(["--dtype", "bf16", "--no-hip-graphs"])
+        cfg.batch_size = 4
+        ff = FFModel(cfg)
+        bc = BertConfig(vocab=512, hidden=128, layers=2, heads=2, ffn=512, seq=64)
+        ids, pos, _ = build_bert(ff, 4, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        rng = np.random.default_rng(0)
+        ids.set_tensor(ff, rng.integers(0, bc.vocab, (4, bc.seq), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (4, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (4, bc.seq, 1), dtype=np.int32))
+        for _ in range(4):
+            ff.train_step()
+        torch.cuda.synchronize()
+        return ff, [np.asarray(w.get_weights(ff), dtype=np.float32) for L in ff.layers for w in L.weights]
+
+    from flexflow_amd import kernels as K
+    n0 = K.reductions_deferred()
+    _, a = run(True)
+    assert K.reductions_deferred() > n0  # the folds did go to the side stream
+    _, b = run(False)
+    for k, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-6, err_msg=str(k))
