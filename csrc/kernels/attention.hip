@@ -322,6 +322,202 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
   }
 }
 
+// ------------------------------------------------------------------ forward, 64 rows per wave
+// attn_fwd_kernel with two 32-row query blocks per wave (256 rows per 4-wave workgroup, two
+// workgroups per CU at <= 256 registers): every K fragment, V fragment and DMA piece serves two
+// row blocks. Why: summing a wave-tile's issue cycles (16 MFMAs hold the SIMD's issue for 128
+// cycles, ~176 VALU instructions ~720, 4 LDS-DMA pieces ~250-400, 24 LDS reads ~150) gives ~1400
+// per 512 cycles of MFMA work. Measured (profiles/attn_fwd_variants_r4.txt): +2..6 % for S >= 512
+// (708 -> 725-740 TF/s at B32 H16 S512, 794 -> 840 at S4096), -1..7 % at S = 256; taking the row
+// sums on the matrix core (ones x P^T) as well did not help. Bitwise equal to the 4-wave kernel.
+// D = 64; the default for Sq >= 512 (variant 3).
+template <bool MASK>
+__global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
+  constexpr int D = 64, KV = 64, QB = 2, ROWS = 4 * 32 * QB;
+  constexpr int TB = KV * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[ROWS * D * 2 > 4 * TB ? ROWS * D * 2 : 4 * TB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int nqb = (a.Sq + ROWS - 1) / ROWS;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = lid / nqb, b = bh / a.H, hh = bh % a.H;
+  const int qblk0 = (lid % nqb) * ROWS;
+  const int q0 = qblk0 + wave * 32 * QB;  // rows q0 + 32 qb + (lane & 31)
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+
+  bf16x8 qf[QB][D / 16];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int qrow = q0 + 32 * qb + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      if (qrow < a.Sq) qf[qb][s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
+      else qf[qb][s] = bf16x8{};
+    }
+  }
+  f32x16 oacc[QB][D / 32];
+  float m[QB], lsum[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) oacc[qb][i] = f32x16{};
+    m[qb] = -INFINITY;
+    lsum[qb] = 0.f;
+  }
+  const float sl2 = a.scale * LOG2E;
+
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  int ko[D / 16], vo[D / 32][2][2];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
+    asm volatile("" : "+v"(ko[s]));
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
+        asm volatile("" : "+v"(vo[dt][s2][hi]));
+      }
+
+  int nkv = (a.Sk + KV - 1) / KV;
+  if (a.causal) nkv = min(nkv, (min(qblk0 + ROWS, a.Sq) + KV - 1) / KV);
+  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
+  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, kb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, vb, 0x00020000);
+  if (nkv > 0) {
+    dma_tile<D, 4>(rk, smem, a.k_ss, 0, wave, lane);
+    dma_tile<D, 4>(rv, smem + TB, a.v_ss, 0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  auto tile = [&](auto par, int t) {
+    constexpr int PAR = decltype(par)::value;
+    const char* kl = smem + PAR * 2 * TB;
+    const char* vl = kl + TB;
+    char* nk = smem + (PAR ^ 1) * 2 * TB;
+    const bool more = t + 1 < nkv;
+    if (more) {
+      dma_tile<D, 4>(rk, nk, a.k_ss, (t + 1) * KV, wave, lane);
+      dma_tile<D, 4>(rv, nk + TB, a.v_ss, (t + 1) * KV, wave, lane);
+    }
+    f32x16 sacc[QB][2];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+          sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
+      }
+    const int kbase = t * KV;
+    bf16x8 pf[QB][2][2];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const int qrow = q0 + 32 * qb + (lane & 31);
+      const bool need_mask = MASK && ((kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0 + 32 * qb));
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= a.Sk || (a.causal && key > qrow)) sacc[qb][kt][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[qb][kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+      if (!__all(mx <= m[qb] + a.rescale_thr)) {
+        const float mnew = fmaxf(m[qb], mx);
+        const float alpha = fast_exp2(m[qb] - (mnew == -INFINITY ? 0.f : mnew));
+        lsum[qb] *= alpha;
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[qb][i][r] *= alpha;
+        m[qb] = mnew;
+      }
+      const float msafe = m[qb] == -INFINITY ? 0.f : m[qb];
+      float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(__builtin_fmaf(sacc[qb][kt][r], sl2, -msafe));
+          sacc[qb][kt][r] = p;
+          if (r & 1) rs1 += p;
+          else rs0 += p;
+        }
+      float rs = rs0 + rs1;
+      rs += __shfl_xor(rs, 32, 64);
+      lsum[qb] += rs;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) { pf[qb][kt][0] = pack8(sacc[qb][kt], 0); pf[qb][kt][1] = pack8(sacc[qb][kt], 8); }
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
+          const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
+          const bf16x8 vf = cat8(lo, hi);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            oacc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][kt][s2], oacc[qb][dt], 0, 0, 0);
+        }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int t = 0; t < nkv; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nkv) tile(std::integral_constant<int, 1>{}, t + 1);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const float inv = lsum[qb] > 0.f ? 1.f / lsum[qb] : 0.f;
+    const int row = wave * 32 * QB + 32 * qb + (lane & 31);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 4 * dt + g;
+        *reinterpret_cast<uint2*>(smem + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
+            make_uint2((unsigned)f2bf(oacc[qb][dt][4 * g] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 1] * inv) << 16),
+                       (unsigned)f2bf(oacc[qb][dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 3] * inv) << 16));
+      }
+    const int qrow = q0 + 32 * qb + (lane & 31);
+    if (h == 0 && a.lse && qrow < a.Sq)
+      a.lse[(int64_t)bh * a.Sq + qrow] = lsum[qb] > 0.f ? (m[qb] * LN2 + __logf(lsum[qb])) : INFINITY;
+  }
+  __syncthreads();
+  {
+    constexpr int CPR = D / 8;
+    bf16_t* Ob = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh;
+#pragma unroll
+    for (int i = 0; i < ROWS * CPR / 256; ++i) {
+      const int id = tid + i * 256, r = id / CPR, c = id % CPR;
+      if (qblk0 + r < a.Sq)
+        *reinterpret_cast<uint4*>(Ob + (int64_t)(qblk0 + r) * a.o_ss + 8 * c) =
+            *reinterpret_cast<const uint4*>(smem + r * (D * 2) + ((c ^ (r & 7)) << 4));
+    }
+  }
+}
+
 // ------------------------------------------------------------------------ forward, ping-pong
 // 8 waves, 256 query rows per workgroup: group A = waves 0-3 (rows 0-127), group B = waves 4-7
 // (rows 128-255), one wave of each group per SIMD. Each K/V tile is two barrier-separated
@@ -1174,14 +1370,15 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
-// Forward structure: 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64 / 128), 1 = 4-wave with
-// LDS-DMA K/V staging (default), 0 = 4-wave through registers (attn_set_fwd_variant; default from
+// Forward structure: 3 = 64 rows per wave (attn_fwd2_kernel, D = 64 and Sq >= 512, else 1;
+// default), 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64), 1 = 4-wave with
+// LDS-DMA K/V staging, 0 = 4-wave through registers (attn_set_fwd_variant; default from
 // FF_ATTN_FWD).
 static int g_fwd_variant = -1;
 int attn_fwd_variant() {
   if (g_fwd_variant < 0) {
     const char* e = getenv("FF_ATTN_FWD");
-    g_fwd_variant = e ? atoi(e) : 1;
+    g_fwd_variant = e ? atoi(e) : 3;
   }
   return g_fwd_variant;
 }
@@ -1208,6 +1405,14 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
                       a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
                       (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
   const bool dma = attn_fwd_variant() >= 1 && dma_ok;
+  // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
+  // (half the workgroups), profiles/attn_fwd_variants_r4.txt
+  if (attn_fwd_variant() == 3 && dma_ok && a.D == 64 && a.Sq >= 512) {
+    const dim3 g3((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
+    if (mask) hipLaunchKernelGGL((attn_fwd2_kernel<true>), g3, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd2_kernel<false>), g3, dim3(256), 0, st, a);
+    return;
+  }
   if (attn_fwd_variant() == 2 && dma_ok) {  // 8-wave ping-pong (attn_fwd_pp_kernel), D = 64 only
     const dim3 g2((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
     if (a.D == 64) {
