@@ -689,6 +689,7 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     (1, 130, 17, 17, 200, (1, 7), (1, 1), (0, 3), 1),   # Inception 1x7, channels past one tile
     (2, 192, 35, 35, 64, (1, 1), (1, 1), (0, 0), 1),   # Inception A 1x1: 3 channel tiles, odd HW
     (2, 64, 16, 16, 64, (3, 3), (1, 1), (1, 1), 32),   # ResNeXt grouped 3x3: Cp = 8 per group
+    (2, 256, 8, 8, 128, (1, 1), (1, 1), (0, 0), 2),    # grouped 1x1, 128 channels per group: no pack pass
 ])
 def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     """Our implicit-GEMM MFMA convolution (forward with bias + ReLU, backward data, backward filter
