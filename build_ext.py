@@ -26,6 +26,11 @@ BUILD = os.path.join(ROOT, "build")
 PKG = os.path.join(ROOT, "flexflow_amd")
 ARCH = os.environ.get("FF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# Per-file code generation flags. attention.hip: no SLP vectorisation — hipcc packed the backward's
+# adjacent f32 multiplies / adds into v_pk_mul_f32 / v_pk_add_f32 (56 per 64-query tile), which
+# beside MFMAs cost more issue cycles than the scalar pairs they replace (MI355X_MICROARCH.md,
+# 'price of one filler beside MFMAs'). A flag change rebuilds the file (the command is hashed).
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _torch_paths():
@@ -70,15 +75,20 @@ def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
         obj = os.path.join(BUILD, "kernels", s + ".o")
         objs.append(obj)
         if s.endswith(".hip"):
-            cmd = [HIPCC, f"--offload-arch={ARCH}", *common, "-c", src, "-o", obj]
+            cmd = [HIPCC, f"--offload-arch={ARCH}", *common, *FILE_FLAGS.get(s, []), "-c", src, "-o", obj]
         else:  # torch glue: host code only
             cmd = [HIPCC, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C",
                    "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations",
                    *sum([["-isystem", i] for i in inc], []), "-isystem", py_inc, "-c", src, "-o", obj]
-        if _newer(src, obj, headers):
+        stamp = obj + ".cmd"  # the compile command: a flag change rebuilds the object
+        prev = open(stamp).read() if os.path.exists(stamp) else ""
+        if _newer(src, obj, headers) or prev != " ".join(cmd):
             jobs_list.append(cmd)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(_run, jobs_list))
+    for cmd in jobs_list:  # stamped once every compile succeeded
+        with open(cmd[-1] + ".cmd", "w") as f:
+            f.write(" ".join(cmd))
     out = os.path.join(PKG, "_C.so")
     if jobs_list or not os.path.exists(out):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-L", tlib, f"-Wl,-rpath,{tlib}",
