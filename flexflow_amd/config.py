@@ -73,7 +73,8 @@ class FFConfig:
         # enough for launch overhead to matter (runtime/graph.py), True always, False never
         self.hip_graphs = "auto"
         self.graph_min_step_ms = 15.0
-        self.graph_trial_max_ms = 30.0  # eager steps up to this long are captured on trial (runtime/graph.py)
+        # eager steps up to this long are captured on trial (runtime/graph.py); FF_GRAPH_TRIAL_MAX_MS
+        self.graph_trial_max_ms = float(os.environ.get("FF_GRAPH_TRIAL_MAX_MS", "30"))
         self.search_algo = "unity"  # unity | mcmc | dp (data-parallel only) | none
         self.mcmc_iterations = 2000
         self.grad_bucket_mb = 64.0

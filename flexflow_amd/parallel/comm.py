@@ -13,8 +13,12 @@ src/parallel_ops/kernels/*.cu) with explicit collectives chosen per edge:
     all_to_all        partitioned along a -> partitioned along b     (Combine(a) + Repartition(b)
                       on the same devices: every rank sends 1/k of its shard to each peer,
                       one link per peer on the fully connected xGMI node)
-    generic P2P       anything else (placement changes, halos, uneven device sets):
-                      batched isend/irecv of exactly the overlapping blocks.
+    exchange          any other re-partition among ONE device set (uneven splits, several dims
+                      at once, permuted placement, no replicas / partial sums): one
+                      all_to_all_single with per-peer split sizes over the packed overlaps
+    generic P2P       anything else (placement changes between device groups, halos, partial
+                      sums onto a different layout): batched isend/irecv of exactly the
+                      overlapping blocks (no zero fill unless partial sums are added).
 
 and the weight-gradient synchronisation (reference: one ncclAllReduce per weight followed by an
 execution fence, src/runtime/optimizer_kernel.cu:88-94 / optimizer.cc:193) with bucketed
@@ -32,6 +36,8 @@ from __future__ import annotations
 
 import os
 from typing import Dict, Optional, Sequence
+
+import math
 
 import torch
 import torch.distributed as dist
@@ -165,7 +171,7 @@ class Transfer:
         self.group_ranks: tuple = ()
         self._classify()
         self.items: Optional[list[TransferItem]] = None
-        if self.kind == "generic":
+        if self.kind in ("generic", "exchange"):
             self.items = plan_transfer(src, dst, src_partial)
 
     # ------------------------------------------------------------------ classification
@@ -202,6 +208,13 @@ class Transfer:
             if a2a is not None:
                 self.kind, self.dim = "all_to_all", a2a
                 return
+            # any other re-partition among one device set (uneven splits, several dims at once,
+            # permuted placement): one all_to_all_single with per-peer split sizes
+            if (S.replicas == 1 and D.replicas == 1 and set(S.devices) == set(D.devices)
+                    and len(set(S.devices)) == len(S.devices) and len(set(D.devices)) == len(D.devices)
+                    and len(S.devices) > 1):
+                self.kind = "exchange"
+                self.group_ranks = tuple(sorted(set(S.devices)))
 
     @staticmethod
     def _subblock_devices_match(coarse: Layout, fine: Layout, d: int, k: int, subset=False) -> bool:
@@ -237,6 +250,8 @@ class Transfer:
             for blk in self.src.blocks():
                 if blk[a] == 0:
                     out.append(tuple(sorted(_a2a_devices(self.src, self.dst, blk, a, b, k)[0])))
+        elif self.kind == "exchange":
+            out.append(self.group_ranks)
         return out
 
     def bytes_moved(self, elem_bytes: int) -> int:
@@ -309,7 +324,54 @@ class Transfer:
             if x is None:
                 return Pending(value=None)
             return self._all_to_all(comm, x)
+        if self.kind == "exchange":
+            if x is None:
+                return Pending(value=None)
+            return self._exchange(comm, x)
         return self._generic(comm, x, like)
+
+    def _exchange(self, comm, x):
+        """Every rank of the device set sends each peer the overlap of its source block with the
+        peer's destination block, packed into one buffer in group-rank order, through ONE
+        all_to_all_single with per-peer split sizes (the overlaps are listed in the same order on
+        every rank: plan_transfer is deterministic)."""
+        S, D, r = self.src, self.dst, self.rank
+        grp = list(self.group_ranks)
+        send = {p: [] for p in grp}
+        recv = {p: [] for p in grp}
+        for it in self.items:
+            sd, dd = S.devices[it.src_part], D.devices[it.dst_part]
+            if sd == r:
+                send[dd].append(it)
+            if dd == r:
+                recv[sd].append(it)
+        chunks, in_splits = [], []
+        for p in grp:
+            n = 0
+            for it in send[p]:
+                v = x[_slices(it.region, S.region(it.src_part))].reshape(-1)
+                chunks.append(v)
+                n += v.numel()
+            in_splits.append(n)
+        inp = torch.cat(chunks) if chunks else x.new_empty(0)
+        out_splits = [sum(math.prod(hi - lo for lo, hi in it.region) for it in recv[p]) for p in grp]
+        flat = torch.empty(sum(out_splits), dtype=x.dtype, device=x.device)
+        h = dist.all_to_all_single(flat, inp.contiguous(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                   group=comm.group(grp), async_op=True)
+        q = D.parts_on(r)[0]
+
+        def finish():
+            out = torch.empty(D.local_shape(q), dtype=x.dtype, device=x.device)  # the overlaps tile it
+            off = 0
+            for p in grp:
+                for it in recv[p]:
+                    shp = tuple(hi - lo for lo, hi in it.region)
+                    n = math.prod(shp)
+                    out[_slices(it.region, D.region(it.dst_part))].copy_(flat[off:off + n].view(shp))
+                    off += n
+            return out
+        sent = sum(n for p, n in zip(grp, in_splits) if p != r) * x.element_size()
+        return Pending([h], finish, kind="exchange", nbytes=sent)
 
     def _all_to_all(self, comm, x):
         S, D, r = self.src, self.dst, self.rank
@@ -385,7 +447,10 @@ class Transfer:
         out = None
         if dparts:
             q = dparts[0]
-            out = torch.zeros(D.local_shape(q), dtype=ref.dtype, device=ref.device)
+            # without partial sums or halos the overlaps tile the destination block: no zero fill
+            # (a halo'd block reaching past the tensor's edge keeps zeros there)
+            alloc = torch.zeros if (self.sp or D.halo or S.halo) else torch.empty
+            out = alloc(D.local_shape(q), dtype=ref.dtype, device=ref.device)
         ops = []
         pending = []
         for it in self.items:
