@@ -793,10 +793,20 @@ static void launch_igemm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_
 // workgroups as fit the CUs at once (3 per CU at 64 rows, 2 at 128: LDS), each over at least 4
 // steps of 64 pixels; slabs capped at 64 MB
 static int wgrad_tm(int Kg) { return Kg <= 64 ? 64 : 128; }
+// FF_CONV_WGRAD_SLOTS scales the workgroup target (percent, default 100): fewer splits write and
+// re-read fewer fp32 slabs, more splits fill the CUs
+static int wgrad_slot_pct() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_CONV_WGRAD_SLOTS");
+    v = e ? std::max(1, atoi(e)) : 100;
+  }
+  return v;
+}
 static int wgrad_splits(int64_t P, int G, int Kg, int NC) {
   const int TM = wgrad_tm(Kg);
   const int64_t tiles = (int64_t)G * ((Kg + TM - 1) / TM) * ((NC + 127) / 128);
-  const int64_t nsteps = (P + 63) / 64, slots = TM == 64 ? 768 : 512;
+  const int64_t nsteps = (P + 63) / 64, slots = (TM == 64 ? 768 : 512) * (int64_t)wgrad_slot_pct() / 100;
   int64_t S = std::min<int64_t>(nsteps / 4, (slots + tiles - 1) / tiles);
   S = std::min<int64_t>(S, (int64_t)(16 << 20) / std::max<int64_t>(1, (int64_t)G * Kg * NC));
   return (int)std::max<int64_t>(1, S);
