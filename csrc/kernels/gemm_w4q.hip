@@ -93,7 +93,8 @@ __device__ __forceinline__ void wait_after(int n_after, bool stores) {
 // ABL (timing-only builds, impl 50+ in the probes; outputs are NOT valid): bit 0 drops every
 // store (range check), bit 1 issues no main-loop DMA (the MFMAs re-read the prologue's K-tiles),
 // bit 2 also drops the per-step barrier — what is left is the MFMA + LDS-read stream alone;
-// bit 3 keeps every DMA but re-reads K-tiles 0..3 (L2-resident: the issue cost without the latency).
+// bit 3 keeps every DMA but re-reads K-tiles 0..3 (L2-resident: the issue cost without the latency);
+// bit 5: global_load_lds instead of buffer_load ... lds (outputs valid; whole tiles only).
 // CPOL: cache-policy bits of the operand DMAs (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16).
 template <bool A_K, bool B_K, bool F32OUT, int ABL = 0, int CPOL = 0>
 __global__ void __launch_bounds__(NTH, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -125,9 +126,16 @@ gemm_w4q_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
       vb[q] = isA ? piece_lane_off<A_K>(p.lda, tmi * BM, wl, q, lane) : piece_lane_off<B_K>(p.ldb, tni * BN, wl, q, lane);
   };
   // piece g of this wave's share of K-tile t into slot `slot`; dma() issues all 8 (prologue, seam)
+  const char* gbase = (const char*)(isA ? p.A : p.B);
   auto dma1 = [&](int slot, int t, int g) __attribute__((always_inline)) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + slot * STAGE + (wave * PW + g) * 1024), 16,
-                                             vb[g & 3] + g * gstride, t * kstride, 0, CPOL);
+    if constexpr (ABL & 32) {  // global_load_lds instead of the buffer form (timing ablation: no range check)
+      typedef __attribute__((address_space(1))) void* gptr_t;
+      __builtin_amdgcn_global_load_lds((gptr_t)(gbase + (int64_t)(vb[g & 3] + g * gstride) + (int64_t)t * kstride),
+                                       (lds_ptr_t)(smem + slot * STAGE + (wave * PW + g) * 1024), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + slot * STAGE + (wave * PW + g) * 1024), 16,
+                                               vb[g & 3] + g * gstride, t * kstride, 0, CPOL);
+    }
   };
   auto dma = [&](int slot, int t) __attribute__((always_inline)) {
 #pragma unroll
@@ -369,7 +377,10 @@ bool gemm_w4q_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStrea
     else if (p.ablate == 3) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 3>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
     else if (p.ablate == 7) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 7>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
     else if (p.ablate == 9) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 9>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
-    else if (p.ablate == 21) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 0, 16>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
+    else if (p.ablate == 32) {  // global_load_lds operands: whole tiles only (no range check)
+      if (p.M % 256 || p.N % 256) return false;
+      hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 32>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
+    } else if (p.ablate == 21) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 0, 16>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
     else if (p.ablate == 22) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 0, 2>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
     else if (p.ablate == 23) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 0, 18>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
     else if (p.ablate == 24) hipLaunchKernelGGL((gemm_w4q_kernel<true, true, false, 0, 1>), grid, dim3(NTH), 0, stream, p, a_bytes, b_bytes);
