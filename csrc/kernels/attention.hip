@@ -518,6 +518,223 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------- forward, 64 rows per wave, persistent
+// attn_fwd2_kernel's tile loop with the per-block fixed costs overlapped: two workgroups per CU
+// walk their 256-row query blocks (block = blockIdx.x, + gridDim.x, ... in xcd_remap order, so a
+// (batch, head)'s blocks stay on one XCD), the K/V tile stream continues across block seams (the
+// last tile of a block requests the next block's first tile), the next block's Q is loaded while
+// this block's O leaves through its own 32-KiB staging image, and those stores drain under the
+// next block's first tile. Why: at S = 512 one K/V tile per workgroup runs at ~1400 TF/s and eight
+// at ~650 (profiles/attn_fwd_lab_r2.txt) — the Q load, first tile and O store of every block were
+// paid by all workgroups at once. Non-causal, Sq % 256 == 0, Sk % 128 == 0, D = 64; bitwise equal to
+// attn_fwd2_kernel.
+__global__ void __launch_bounds__(256, 2) attn_fwd2p_kernel(AttnArgs a, int nblocks) {
+  constexpr int D = 64, KV = 64, QB = 2, ROWS = 256;
+  constexpr int TB = KV * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + ROWS * D * 2];
+  char* epi = smem + 4 * TB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int nqb = a.Sq / ROWS;
+  const int nkv = a.Sk / KV;  // even
+  const int nmine = (nblocks - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const float sl2 = a.scale * LOG2E;
+  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
+  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
+
+  struct Blk {
+    int bh, b, hh, qblk0;
+  };
+  auto mk = [&](int i) {
+    Blk r;
+    const int lid = xcd_remap((int)blockIdx.x + i * (int)gridDim.x, nblocks);
+    r.bh = lid / nqb;
+    r.b = r.bh / a.H;
+    r.hh = r.bh % a.H;
+    r.qblk0 = (lid % nqb) * ROWS;
+    return r;
+  };
+  auto rsrc_k = [&](const Blk& k) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.k + (int64_t)k.b * a.k_sb + (int64_t)k.hh * a.k_sh), (short)0, kb,
+                                             0x00020000);
+  };
+  auto rsrc_v = [&](const Blk& k) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.v + (int64_t)k.b * a.v_sb + (int64_t)k.hh * a.v_sh), (short)0, vb,
+                                             0x00020000);
+  };
+  auto load_q = [&](const Blk& k, bf16x8 (&q)[QB][D / 16]) {
+    const bf16_t* Q = a.q + (int64_t)k.b * a.q_sb + (int64_t)k.hh * a.q_sh;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const int qrow = k.qblk0 + wave * 32 * QB + 32 * qb + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s)
+        q[qb][s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
+    }
+  };
+
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
+  int ko[D / 16], vo[D / 32][2][2];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
+    asm volatile("" : "+v"(ko[s]));
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
+        asm volatile("" : "+v"(vo[dt][s2][hi]));
+      }
+
+  Blk cur = mk(0);
+  __amdgpu_buffer_rsrc_t rk = rsrc_k(cur), rv = rsrc_v(cur);
+  bf16x8 qf[QB][D / 16];
+  load_q(cur, qf);
+  dma_tile<D, 4>(rk, smem, a.k_ss, 0, wave, lane);
+  dma_tile<D, 4>(rv, smem + TB, a.v_ss, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int i = 0; i < nmine; ++i) {
+    const bool has_next = i + 1 < nmine;
+    f32x16 oacc[QB][D / 32];
+    float m[QB], lsum[QB];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
+      for (int j = 0; j < D / 32; ++j) oacc[qb][j] = f32x16{};
+      m[qb] = -INFINITY;
+      lsum[qb] = 0.f;
+    }
+    auto tile = [&](auto par, int t) {
+      constexpr int PAR = decltype(par)::value;
+      const char* kl = smem + PAR * 2 * TB;
+      const char* vl = kl + TB;
+      char* nk = smem + (PAR ^ 1) * 2 * TB;
+      // the tile stream: the next tile of this block, or the next block's first
+      bool more = true;
+      if (t + 1 < nkv) {
+        dma_tile<D, 4>(rk, nk, a.k_ss, (t + 1) * KV, wave, lane);
+        dma_tile<D, 4>(rv, nk + TB, a.v_ss, (t + 1) * KV, wave, lane);
+      } else if (has_next) {  // rk / rv move on to the next block: this one's tiles are all in LDS
+        const Blk nb = mk(i + 1);
+        rk = rsrc_k(nb);
+        rv = rsrc_v(nb);
+        dma_tile<D, 4>(rk, nk, a.k_ss, 0, wave, lane);
+        dma_tile<D, 4>(rv, nk + TB, a.v_ss, 0, wave, lane);
+      } else {
+        more = false;
+      }
+      f32x16 sacc[QB][2];
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
+        }
+      // this block's Q is dead after its last S tile: the next block's Q loads land in its registers
+      if (t + 1 == nkv && has_next) load_q(mk(i + 1), qf);
+      bf16x8 pf[QB][2][2];
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[qb][kt][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
+        if (!__all(mx <= m[qb] + a.rescale_thr)) {
+          const float mnew = fmaxf(m[qb], mx);
+          const float alpha = fast_exp2(m[qb] - (mnew == -INFINITY ? 0.f : mnew));
+          lsum[qb] *= alpha;
+#pragma unroll
+          for (int j = 0; j < D / 32; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[qb][j][r] *= alpha;
+          m[qb] = mnew;
+        }
+        const float msafe = m[qb] == -INFINITY ? 0.f : m[qb];
+        float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(__builtin_fmaf(sacc[qb][kt][r], sl2, -msafe));
+            sacc[qb][kt][r] = p;
+            if (r & 1) rs1 += p;
+            else rs0 += p;
+          }
+        float rs = rs0 + rs1;
+        rs += __shfl_xor(rs, 32, 64);
+        lsum[qb] += rs;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) { pf[qb][kt][0] = pack8(sacc[qb][kt], 0); pf[qb][kt][1] = pack8(sacc[qb][kt], 8); }
+      }
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
+            const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
+            const bf16x8 vf = cat8(lo, hi);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+              oacc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][kt][s2], oacc[qb][dt], 0, 0, 0);
+          }
+      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    for (int t = 0; t < nkv; t += 2) {
+      tile(std::integral_constant<int, 0>{}, t);
+      tile(std::integral_constant<int, 1>{}, t + 1);
+    }
+    // epilogue through the block's own staging image (the K/V ring holds the next block's tile 0)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float inv = lsum[qb] > 0.f ? 1.f / lsum[qb] : 0.f;
+      const int row = wave * 32 * QB + 32 * qb + (lane & 31);
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 4 * dt + g;
+          *reinterpret_cast<uint2*>(epi + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
+              make_uint2((unsigned)f2bf(oacc[qb][dt][4 * g] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 1] * inv) << 16),
+                         (unsigned)f2bf(oacc[qb][dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 3] * inv) << 16));
+        }
+      const int qrow = cur.qblk0 + wave * 32 * QB + 32 * qb + (lane & 31);
+      if (h == 0 && a.lse)
+        a.lse[(int64_t)cur.bh * a.Sq + qrow] = lsum[qb] > 0.f ? (m[qb] * LN2 + __logf(lsum[qb])) : INFINITY;
+    }
+    // LDS-only barrier: the previous block's O stores need not drain
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    {
+      constexpr int CPR = D / 8;
+      bf16_t* Ob = a.o + (int64_t)cur.b * a.o_sb + (int64_t)cur.hh * a.o_sh;
+#pragma unroll
+      for (int j = 0; j < ROWS * CPR / 256; ++j) {
+        const int id = tid + j * 256, r = id / CPR, c = id % CPR;
+        *reinterpret_cast<uint4*>(Ob + (int64_t)(cur.qblk0 + r) * a.o_ss + 8 * c) =
+            *reinterpret_cast<const uint4*>(epi + r * (D * 2) + ((c ^ (r & 7)) << 4));
+      }
+    }
+    if (!has_next) break;
+    cur = mk(i + 1);
+  }
+}
+
 // ------------------------------------------------------------------------ forward, ping-pong
 // 8 waves, 256 query rows per workgroup: group A = waves 0-3 (rows 0-127), group B = waves 4-7
 // (rows 128-255), one wave of each group per SIMD. Each K/V tile is two barrier-separated
@@ -1370,8 +1587,9 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
 }
 
-// Forward structure: 3 = 64 rows per wave (attn_fwd2_kernel, D = 64 and Sq >= 512, else 1;
-// default), 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64), 1 = 4-wave with
+// Forward structure: 4 = persistent 64 rows per wave (attn_fwd2p_kernel; D = 64, non-causal,
+// Sq % 256 == 0, Sk % 128 == 0, else 1), 3 = 64 rows per wave (attn_fwd2_kernel, D = 64 and
+// Sq >= 512, else 1; default), 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64), 1 = 4-wave with
 // LDS-DMA K/V staging, 0 = 4-wave through registers (attn_set_fwd_variant; default from
 // FF_ATTN_FWD).
 static int g_fwd_variant = -1;
@@ -1405,6 +1623,22 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
                       a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
                       (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
   const bool dma = attn_fwd_variant() >= 1 && dma_ok;
+  // persistent 64-rows-per-wave kernel (attn_fwd2p_kernel): two workgroups per CU walk the query
+  // blocks with the K/V stream running across block seams
+  if (attn_fwd_variant() == 4 && dma_ok && a.D == 64 && !a.causal && a.Sq % 256 == 0 && a.Sk % 128 == 0) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const int nblocks = a.Sq / 256 * a.B * a.H;
+    int g = std::min(nblocks, 2 * cus);
+    if (g > 8) g -= g % 8;  // equal residues mod 8: a workgroup's blocks stay on its XCD's chunk
+    hipLaunchKernelGGL(attn_fwd2p_kernel, dim3((unsigned)g), dim3(256), 0, st, a, nblocks);
+    return;
+  }
   // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
   // (half the workgroups), profiles/attn_fwd_variants_r4.txt
   if (attn_fwd_variant() == 3 && dma_ok && a.D == 64 && a.Sq >= 512) {

@@ -37,21 +37,22 @@ def timed(fn):
 
 
 fl_f = 4.0 * B * H * S * S * D
-# forward K/V staging variants (0: through registers, 1: LDS-DMA), interleaved rounds
+# forward structures (0: registers, 1: LDS-DMA, 2: ping-pong, 3: 64 rows/wave, 4: persistent), interleaved
 default_fwd = X.attn_fwd_variant()
-fres, fouts = {0: [], 1: [], 2: [], 3: []}, {}
+FV = (0, 1, 2, 3, 4)
+fres, fouts = {v: [] for v in FV}, {}
 for rnd in range(3):
-    for var in (0, 1, 2, 3):
+    for var in FV:
         X.attn_set_fwd_variant(var)
         lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
         fouts[var] = (o.clone(), lse.clone())
         fres[var].append(timed(lambda: Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)))
-for var in (0, 1, 2, 3):
+for var in FV:
     ms = min(fres[var])
     print(f"attn fwd variant {var} B={B} H={H} S={S} D={D}: {ms:.4f} ms {fl_f / ms / 1e9:.1f} TFLOPS "
           f"(rounds {[round(t, 4) for t in fres[var]]})")
 print("fwd variants identical: " + str(all(torch.equal(fouts[0][0], fouts[v][0]) and torch.equal(fouts[0][1], fouts[v][1])
-                                           for v in (1, 2, 3))))
+                                           for v in FV[1:])))
 X.attn_set_fwd_variant(default_fwd)
 # deferred-max threshold A/B (0 = textbook rescale on every max increase; default 8)
 default_thr = X.attn_rescale_thr()
