@@ -117,14 +117,30 @@ struct IGemmArgs {
   int relu;
   int out_nhwc;      // channel-last output (M % 8 == 0)
   int accum;         // add into the existing output (a gradient summed over several consumers)
+  int nph;           // backward-data by stride phase (sh * sw sub-GEMMs, grid z = G * nph); 0 / 1: off
+};
+
+// Column -> output pixel of the implicit GEMMs: the identity, or (stride-phase backward-data) the
+// pixel (n, py + sh jy, px + sw jx) of phase column (n, jy, jx)
+struct IdPix {
+  __device__ __forceinline__ int64_t operator()(int64_t p) const { return p; }
+};
+struct PhasePix {
+  int Hq, Wq, py, px, sh, sw, H, W;
+  __device__ __forceinline__ int64_t operator()(int64_t p) const {
+    const int64_t HW = (int64_t)Hq * Wq;
+    const int64_t n = p / HW;
+    const int r = (int)(p - n * HW), jy = r / Wq, jx = r - jy * Wq;
+    return (n * H + py + sh * jy) * W + px + sw * jx;
+  }
 };
 
 // Epilogue of the implicit GEMMs: acc[i][j] row = channel (r&3) + 8(r>>2) + 4h of the wave's
 // (BM/2)-row block, column = pixel lane & 31 of its (BN/2)-pixel block; bias, ReLU, accumulate.
 // smem: >= BN * (2 BM + 16) bytes, free (every wave past its last read of the K loop's images).
-template <int BM, int BN>
+template <int BM, int BN, class PixMap = IdPix>
 __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)[BM / 64][BN / 64], char* smem,
-                                               int m0, int64_t p0, int64_t P, int g) {
+                                               int m0, int64_t p0, int64_t P, int g, PixMap pix = PixMap{}) {
   constexpr int MI = BM / 64, NB = BN / 64, RS = BM * 2 + 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
@@ -175,7 +191,7 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)
       const int64_t p = p0 + px;
       const int m = m0 + c * 8;
       if (p < P && m < a.M) {
-        uint4* dst = reinterpret_cast<uint4*>(a.out + p * ldo + (int64_t)g * a.M + m);
+        uint4* dst = reinterpret_cast<uint4*>(a.out + pix(p) * ldo + (int64_t)g * a.M + m);
         uint4 v = *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
         if (a.accum) {  // fp32 sum of the staged value and the existing gradient, one rounding
           const uint4 o = *dst;
@@ -198,7 +214,7 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)
   for (int j = 0; j < NB; ++j) {
     const int64_t p = p0 + (BN / 2) * wn + 32 * j + (lane & 31);
     if (p >= P) continue;
-    const int64_t n = p / HoWo, pp = p - n * HoWo;
+    const int64_t rp = pix(p), n = rp / HoWo, pp = rp - n * HoWo;
     bf16_t* ob = a.out + (n * a.G + g) * (int64_t)a.M * HoWo + pp;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -342,7 +358,12 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(IGemmArgs a) {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 __device__ __forceinline__ int off64(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
-template <bool BWD, int BM, int BN>
+// PH (backward-data, stride > 1): one sub-GEMM per stride phase (py, px) = (ih % sh, iw % sw).
+// The input pixels of a phase receive only the taps kh = kh0 + sh th, kw = kw0 + sw tw (kh0 =
+// (py + ph) % sh), and their output-gradient source is (jy + oy0 - th, jx + ox0 - tw): a dense
+// GEMM over ~1 / (sh sw) of the taps. Without phases every input pixel walks all KH x KW taps and
+// 3 of 4 (stride 2) read zeros: the MFMA work of the stride-2 convolutions' backward-data was 4x.
+template <bool BWD, int BM, int BN, bool PH = false>
 __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
   constexpr int BK = 64, MI = BM / 64, NB = BN / 64;
   constexpr int TA = BM * BK * 2, TB = BN * BK * 2;
@@ -353,11 +374,32 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int g = blockIdx.z;
+  int g = blockIdx.z;
   const int m0 = blockIdx.y * BM;
-  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+  int64_t P = (int64_t)a.N * a.Ho * a.Wo;
   const int64_t p0 = (int64_t)blockIdx.x * BN;
   const int C8 = a.Cs / 8;
+  // stride phase (PH): column geometry Hq x Wq, tap subset KHq x KWq from (kh0, kw0)
+  PhasePix pm{a.Ho, a.Wo, 0, 0, 1, 1, a.Ho, a.Wo};
+  int KHq = a.KH, KWq = a.KW, kh0 = 0, kw0 = 0, oy0 = 0, ox0 = 0;
+  if (PH) {
+    const int nph = a.sh * a.sw, phz = (int)blockIdx.z % nph;
+    g = (int)blockIdx.z / nph;
+    pm.py = phz / a.sw;
+    pm.px = phz % a.sw;
+    pm.sh = a.sh;
+    pm.sw = a.sw;
+    pm.Hq = (a.Ho - pm.py + a.sh - 1) / a.sh;
+    pm.Wq = (a.Wo - pm.px + a.sw - 1) / a.sw;
+    kh0 = (pm.py + a.ph) % a.sh;
+    kw0 = (pm.px + a.pw) % a.sw;
+    KHq = (a.KH - kh0 + a.sh - 1) / a.sh;
+    KWq = (a.KW - kw0 + a.sw - 1) / a.sw;
+    oy0 = (pm.py + a.ph - kh0) / a.sh;
+    ox0 = (pm.px + a.pw - kw0) / a.sw;
+    P = (int64_t)a.N * pm.Hq * pm.Wq;
+    if (p0 >= P) return;  // whole workgroup: this phase has fewer columns than the grid's widest
+  }
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.A + (int64_t)g * a.M * a.Kp), (short)0, a.M * a.Kp * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
@@ -367,36 +409,44 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
 #pragma unroll
   for (int i = 0; i < WA; ++i) {
     const int m = m0 + (i * 4 + wave) * 8 + (lane >> 3);
-    aoff[i] = m < a.M ? (m * a.Kp + ch * 8) * 2 : BAD;
+    aoff[i] = m < a.M ? (m * a.Kp + (PH ? 0 : ch * 8)) * 2 : BAD;
   }
   int pbase[WB], prow[WB], pcol[WB];
   bool pok[WB];
+  const int Hc = PH ? pm.Hq : a.Ho, Wc = PH ? pm.Wq : a.Wo;  // column image geometry
 #pragma unroll
   for (int i = 0; i < WB; ++i) {
     const int64_t p = p0 + (i * 4 + wave) * 8 + (lane >> 3);
     pok[i] = p < P;
     const int64_t pp = pok[i] ? p : 0;
-    const int n = (int)(pp / ((int64_t)a.Ho * a.Wo));
-    const int rem = (int)(pp - (int64_t)n * a.Ho * a.Wo);
-    prow[i] = rem / a.Wo;
-    pcol[i] = rem - prow[i] * a.Wo;
+    const int n = (int)(pp / ((int64_t)Hc * Wc));
+    const int rem = (int)(pp - (int64_t)n * Hc * Wc);
+    prow[i] = rem / Wc;
+    pcol[i] = rem - prow[i] * Wc;
     pbase[i] = n * a.Hs * a.Ws;
   }
-  // reduction cursor of this lane's chunk: K index ks * 8 + ch -> (kh, kw, c8)
-  int c8 = ch % C8, kw = (ch / C8) % a.KW, kh = ch / C8 / a.KW;
+  // reduction cursor of this lane's chunk: K index ks * 8 + ch -> (kh, kw, c8); with PH, (th, tw,
+  // c8) over the phase's taps (kh, kw below hold th, tw)
+  const int KWc = PH ? (KWq > 0 ? KWq : 1) : a.KW, KHc = PH ? KHq : a.KH;
+  int c8 = ch % C8, kw = (ch / C8) % KWc, kh = ch / C8 / KWc;
   auto issue = [&](int buf, int ks) {
     char* la = smem + buf * (TA + TB);
     char* lb = la + TA;
+    int acol = ks * (BK * 2);
+    if (PH) acol = kh < KHc ? (((kh0 + a.sh * kh) * a.KW + kw0 + a.sw * kw) * a.Cs + c8 * 8) * 2 : BAD;
 #pragma unroll
     for (int i = 0; i < WA; ++i) {
-      const int off = aoff[i] == BAD ? BAD : aoff[i] + ks * (BK * 2);
+      const int off = (aoff[i] == BAD || acol == BAD) ? BAD : aoff[i] + acol;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(la + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < WB; ++i) {
-      bool ok = pok[i] && kh < a.KH;
+      bool ok = pok[i] && kh < KHc;
       int sy, sx;
-      if (!BWD) {
+      if (PH) {
+        sy = prow[i] + oy0 - kh;
+        sx = pcol[i] + ox0 - kw;
+      } else if (!BWD) {
         sy = prow[i] * a.sh - a.ph + kh;
         sx = pcol[i] * a.sw - a.pw + kw;
       } else {  // source (output-gradient) pixel whose window at (kh, kw) covers this input pixel
@@ -412,7 +462,7 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
     c8 += 8;  // next step: 8 chunks on
     while (c8 >= C8) {
       c8 -= C8;
-      if (++kw == a.KW) { kw = 0; ++kh; }
+      if (++kw == KWc) { kw = 0; ++kh; }
     }
   };
   f32x16 acc[MI][NB];
@@ -420,8 +470,8 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
-  const int nks = a.Kp / BK;
-  issue(0, 0);
+  const int nks = PH ? (KHq * KWq * C8 + 7) / 8 : a.Kp / BK;  // a phase without taps: zeros
+  if (nks > 0) issue(0, 0);
   for (int ks = 0; ks < nks; ++ks) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // step ks visible to all waves; every wave is done reading the other buffer
@@ -444,7 +494,8 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
     }
   }
   __syncthreads();  // the epilogue reuses the images
-  igemm_epilogue<BM, BN>(a, acc, smem, m0, p0, P, g);
+  if (PH) igemm_epilogue<BM, BN>(a, acc, smem, m0, p0, P, g, pm);
+  else igemm_epilogue<BM, BN>(a, acc, smem, m0, p0, P, g);
 }
 
 // ------------------------------------------------------------------------------- bwd-filter
@@ -774,6 +825,13 @@ template <bool BWD, int BM>
 static void launch_igemm_bm(const IGemmArgs& a, int64_t P, int M, int G, hipStream_t st) {
   const int64_t t128 = ((P + 127) / 128) * ((M + BM - 1) / BM) * G;
   const bool dma = (int64_t)a.N * a.Hs * a.Ws * a.G * a.Cs * 2 < 0x7fff0000LL && (int64_t)a.M * a.Kp * 2 < 0x7fff0000LL;
+  if (BWD && dma && a.nph > 1) {  // stride phases: grid over the widest phase (py = px = 0)
+    const int64_t Pq = (int64_t)a.N * ((a.Ho + a.sh - 1) / a.sh) * ((a.Wo + a.sw - 1) / a.sw);
+    const unsigned gz = (unsigned)(G * a.nph), gy = (unsigned)((M + BM - 1) / BM);
+    if (t128 >= 512) hipLaunchKernelGGL((conv_igemm_dma_kernel<true, BM, 128, true>), dim3((unsigned)((Pq + 127) / 128), gy, gz), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_igemm_dma_kernel<true, BM, 64, true>), dim3((unsigned)((Pq + 63) / 64), gy, gz), dim3(256), 0, st, a);
+    return;
+  }
   const dim3 g128((unsigned)((P + 127) / 128), (M + BM - 1) / BM, G), g64((unsigned)((P + 63) / 64), (M + BM - 1) / BM, G);
   if (t128 >= 512) {
     if (dma) hipLaunchKernelGGL((conv_igemm_dma_kernel<BWD, BM, 128>), g128, dim3(256), 0, st, a);
@@ -813,6 +871,16 @@ static int wgrad_splits(int64_t P, int G, int Kg, int NC) {
 }
 
 static int64_t align8(int64_t v) { return (v + 7) / 8 * 8; }
+
+// stride-phase backward-data (conv_igemm_dma_kernel<.., PH>): FF_CONV_DGRAD_PHASES=0 turns it off
+static bool conv_dgrad_phases() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_CONV_DGRAD_PHASES");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v != 0;
+}
 
 int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH, int KW, int G) {
   // bf16 elements: channel-last input + channel-last output gradient + packed weights (fwd / bwd)
@@ -870,7 +938,7 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
     hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
                        wp, G, Kg, Cg, KH, KW, Kp, 1);
     IGemmArgs a{wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc,
-                accum_dx};
+                accum_dx, conv_dgrad_phases() ? sh * sw : 1};
     launch_igemm<true>(a, (int64_t)N * H * W, Cg, G, st);
   }
   if (dw) {

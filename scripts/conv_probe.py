@@ -25,6 +25,13 @@ SHAPES = [  # name, N, C, H, W, K, (kh, kw), (sh, sw), (ph, pw), groups
     ("inception.stem3", 64, 32, 147, 147, 64, (3, 3), (1, 1), (1, 1), 1),
     ("inception.E1x1", 64, 1280, 8, 8, 320, (1, 1), (1, 1), (0, 0), 1),
     ("resnext.g32", 32, 256, 28, 28, 256, (3, 3), (1, 1), (1, 1), 32),
+    ("resnet.c4_ds1x1s2", 64, 512, 28, 28, 1024, (1, 1), (2, 2), (0, 0), 1),
+    ("resnet.c5_3x3s2", 64, 512, 14, 14, 512, (3, 3), (2, 2), (1, 1), 1),
+    ("resnet.c3_3x3s2", 64, 128, 56, 56, 128, (3, 3), (2, 2), (1, 1), 1),
+    ("resnet.c5_7x7_3x3", 64, 512, 7, 7, 512, (3, 3), (1, 1), (1, 1), 1),
+    ("inception.B3x3s2", 64, 288, 35, 35, 384, (3, 3), (2, 2), (0, 0), 1),
+    ("inception.D3x3s2", 64, 192, 17, 17, 320, (3, 3), (2, 2), (0, 0), 1),
+    ("inception.7x1_192", 64, 192, 17, 17, 192, (7, 1), (1, 1), (3, 0), 1),
 ]
 
 

@@ -716,6 +716,11 @@ def test_pool2d_asymmetric_pads(is_max, inc):
     (2, 192, 35, 35, 64, (1, 1), (1, 1), (0, 0), 1),   # Inception A 1x1: 3 channel tiles, odd HW
     (2, 64, 16, 16, 64, (3, 3), (1, 1), (1, 1), 32),   # ResNeXt grouped 3x3: Cp = 8 per group
     (2, 256, 8, 8, 128, (1, 1), (1, 1), (0, 0), 2),    # grouped 1x1, 128 channels per group: no pack pass
+    # stride-phase backward-data: phases without taps (1x1 s2), odd extents, the 7x7 s2 stem, grouped
+    (2, 128, 15, 15, 256, (1, 1), (2, 2), (0, 0), 1),
+    (2, 96, 17, 17, 96, (3, 3), (2, 2), (0, 0), 1),
+    (2, 3, 40, 40, 64, (7, 7), (2, 2), (3, 3), 1),
+    (2, 64, 14, 14, 64, (3, 3), (2, 2), (1, 1), 32),
 ])
 def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     """Our implicit-GEMM MFMA convolution (forward with bias + ReLU, backward data, backward filter
