@@ -811,6 +811,82 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   if (c < Cg) dw[((int64_t)(g * Kg + m) * Cg + c) * KK + kp] += v;
 }
 
+// The same fold for few splits (S <= 32): a thread per 4 consecutive slab elements (one 16-B load
+// per split, fixed order), grid-stride. wgrad_reduce_kernel's 16 row-groups x 16 elements per
+// workgroup left 12 of 16 groups idle at S = 4 and launched 147k workgroups for a 512 x 4608
+// gradient: 73 us, 1.5x the backward-filter GEMM it reduces (profiles/conv_wgrad_pmc_r4.txt).
+__global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, int G,
+                                                            int S, int Kg, int NC, int Cg, int Cp, int KK) {
+  const int64_t slab = (int64_t)Kg * NC, total4 = (int64_t)G * slab / 4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = q * 4;
+    const int g = (int)(i / slab);
+    const int64_t rem = i - (int64_t)g * slab;
+    const float* p = ws + (int64_t)g * S * slab + rem;
+    float4 v = *reinterpret_cast<const float4*>(p);
+    for (int s = 1; s < S; ++s) {
+      const float4 t = *reinterpret_cast<const float4*>(p + s * slab);
+      v.x += t.x;
+      v.y += t.y;
+      v.z += t.z;
+      v.w += t.w;
+    }
+    // NC and Cp are multiples of 8: the 4 columns share one row and one (kh, kw)
+    const int m = (int)(rem / NC), colx = (int)(rem - (int64_t)m * NC);
+    const int kp = colx / Cp, c = colx - kp * Cp;
+    float* d = dw + ((int64_t)(g * Kg + m) * Cg + c) * KK + kp;
+    if (KK == 1 && c + 3 < Cg && ((uintptr_t)d & 15) == 0) {
+      float4 o = *reinterpret_cast<float4*>(d);
+      o.x += v.x;
+      o.y += v.y;
+      o.z += v.z;
+      o.w += v.w;
+      *reinterpret_cast<float4*>(d) = o;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < Cg) d[k * KK] += vv[k];
+    }
+  }
+}
+
+// Few splits and a k x k filter: a workgroup per gradient row m. The S slab rows (column order
+// (kh, kw, c)) are summed with coalesced 16-B loads into an LDS row (padded by one float per tap,
+// so the transposing reads below are conflict-free), then the dW row ([c][kh][kw] order) is
+// updated with coalesced read-modify-writes. wgrad_reduce4_kernel's dW updates were 4-B stores at
+// a KH*KW stride.
+constexpr int WRED_ROW_FLOATS = 16384;  // 64 KiB of LDS
+__global__ void __launch_bounds__(256) wgrad_reduce_row_kernel(const float* __restrict__ ws, float* __restrict__ dw, int G,
+                                                               int S, int Kg, int NC, int Cg, int Cp, int KK) {
+  __shared__ float row[WRED_ROW_FLOATS];
+  const int g = blockIdx.x / Kg, m = blockIdx.x - g * Kg;
+  const int64_t slab = (int64_t)Kg * NC;
+  const float* base = ws + (int64_t)g * S * slab + (int64_t)m * NC;
+  for (int j = threadIdx.x * 4; j < NC; j += 1024) {
+    float4 v = *reinterpret_cast<const float4*>(base + j);
+    for (int s = 1; s < S; ++s) {
+      const float4 t = *reinterpret_cast<const float4*>(base + s * slab + j);
+      v.x += t.x;
+      v.y += t.y;
+      v.z += t.z;
+      v.w += t.w;
+    }
+    const int kp = j / Cp, c = j - kp * Cp;  // Cp % 8 == 0: one tap per 4 columns
+    float* r = row + kp * (Cp + 1) + c;
+    r[0] = v.x;
+    r[1] = v.y;
+    r[2] = v.z;
+    r[3] = v.w;
+  }
+  __syncthreads();
+  float* d = dw + (int64_t)(g * Kg + m) * Cg * KK;
+  for (int e = threadIdx.x; e < Cg * KK; e += 256) {
+    const int c = e / KK, kp = e - c * KK;
+    d[e] += row[kp * (Cp + 1) + c];
+  }
+}
+
 // ------------------------------------------------------------------------------- host
 static int round8(int v) { return (v + 7) / 8 * 8; }
 static int kpad(int KH, int KW, int redp) { return (KH * KW * redp + 63) / 64 * 64; }  // whole 64-deep K steps
@@ -962,8 +1038,15 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
       if (TM == 128) hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(256), 0, st, b);
     }
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)G * Kg * NC + 15) / 16)), dim3(256), 0, st, slabs,
-                       dw, G, S, Kg, NC, Cg, Cp, KH * KW);
+    if (S <= 32 && KH * KW > 1 && KH * KW * (Cp + 1) <= WRED_ROW_FLOATS)
+      hipLaunchKernelGGL(wgrad_reduce_row_kernel, dim3((unsigned)(G * Kg)), dim3(256), 0, st, slabs, dw, G, S, Kg, NC, Cg,
+                         Cp, KH * KW);
+    else if (S <= 32)
+      hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3(ew_grid((int64_t)G * Kg * NC / 4, 256)), dim3(256), 0, st, slabs, dw,
+                         G, S, Kg, NC, Cg, Cp, KH * KW);
+    else
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)G * Kg * NC + 15) / 16)), dim3(256), 0, st, slabs,
+                         dw, G, S, Kg, NC, Cg, Cp, KH * KW);
   }
 }
 
