@@ -1416,6 +1416,7 @@ def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
 # GEMMs; FF_CONV_IMPL=ours|lib forces one. The choices land in TUNE_LOG.
 _conv_tuned: dict = {}
 _CONV_IMPL = _os.environ.get("FF_CONV_IMPL", "")
+_CONV_LIB_MARGIN = float(_os.environ.get("FF_CONV_LIB_MARGIN", "0.1"))
 
 
 def conv_geometry(x, w, stride, pad, groups):
@@ -1469,7 +1470,10 @@ def _conv_pick(kind, key, cands):
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             return "ours"
         times = _time_all(cands, rounds=2)  # interleaved, best of 2 rounds: single passes flipped choices
-        choice = min(times, key=lambda k: times[k])
+        # MIOpen must win by _CONV_LIB_MARGIN: its timing in isolation leaves out the layout copies
+        # and tensor ops around it in the step (Inception-v3 b64: per-site picks 14.17 ms/step, all
+        # ours 14.02, with MIOpen ahead by 1-3 % at 9 of its 12 sites; profiles/conv_pick_ab_r4.txt)
+        choice = "lib" if times["lib"] < (1.0 - _CONV_LIB_MARGIN) * times["ours"] else "ours"
         TUNE_LOG.append({"op": f"conv2d_{kind}", "geom": list(key), "times_ms": {k: round(v, 4) for k, v in
                                                                                times.items()}, "choice": choice})
         _conv_tuned[(kind, key)] = choice
