@@ -1458,9 +1458,42 @@ def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False):
                      accum_dx)
 
 
+def _pointwise_gemm_ok(g, *ts):
+    """A 1x1, stride-1, unpadded, ungrouped convolution over channel-last tensors is a plain GEMM
+    over the N*H*W pixel rows: y[P][K] = x[P][C] . w[K][C]^T (csrc/kernels GEMMs, tuned per call
+    site like any Linear)."""
+    return (g[7] == 1 and g[8] == 1 and g[9] == 1 and g[10] == 1 and g[11] == 0 and g[12] == 0 and g[13] == 1
+            and all(t is not None and is_nhwc(t) for t in ts))
+
+
+def _rows(t):
+    """[N][C][H][W] channel-last tensor -> its [N*H*W][C] row view."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _conv_gemm_fwd(x, w, b, g, relu):
+    P, C, K_ = g[0] * g[5] * g[6], g[1], g[4]
+    y = torch.empty((g[0], K_, g[5], g[6]), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    gemm(_rows(x), w.reshape(K_, C), _rows(y), P, K_, C, True, True, C, C, K_, bias=b,
+         act=ACT_RELU if relu else ACT_NONE)
+    return y
+
+
+def _conv_gemm_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False):
+    """dx[P][C] (+)= dy[P][K] . w[K][C];  dw[K][C] += dy^T . x (fp32)."""
+    P, C, K_ = g[0] * g[5] * g[6], g[1], g[4]
+    dyr = _rows(dy)
+    if dx_out is not None:
+        gemm(dyr, w.reshape(K_, C), _rows(dx_out), P, C, K_, True, False, K_, C, C, beta=1.0 if accum_dx else 0.0)
+    if dw_out is not None:
+        gemm(dyr, _rows(x), dw_out.view(K_, C), K_, C, P, False, False, K_, C, C, beta=1.0)
+
+
 def _conv_pick(kind, key, cands):
     if _CONV_IMPL in ("ours", "lib"):
         return _CONV_IMPL
+    if _CONV_IMPL == "gemm":
+        return "gemm" if "gemm" in cands else "ours"
     choice = _conv_tuned.get((kind, key))
     if choice is None:
         choice = _tune_cache_lookup("conv", (kind, key))
@@ -1473,7 +1506,8 @@ def _conv_pick(kind, key, cands):
         # MIOpen must win by _CONV_LIB_MARGIN: its timing in isolation leaves out the layout copies
         # and tensor ops around it in the step (Inception-v3 b64: per-site picks 14.17 ms/step, all
         # ours 14.02, with MIOpen ahead by 1-3 % at 9 of its 12 sites; profiles/conv_pick_ab_r4.txt)
-        choice = "lib" if times["lib"] < (1.0 - _CONV_LIB_MARGIN) * times["ours"] else "ours"
+        mine = min((k for k in times if k != "lib"), key=lambda k: times[k])
+        choice = "lib" if times["lib"] < (1.0 - _CONV_LIB_MARGIN) * times[mine] else mine
         TUNE_LOG.append({"op": f"conv2d_{kind}", "geom": list(key), "times_ms": {k: round(v, 4) for k, v in
                                                                                times.items()}, "choice": choice})
         _conv_tuned[(kind, key)] = choice
@@ -1496,8 +1530,12 @@ def conv2d_fwd(x, w, b, stride, pad, groups, relu):
             y = _conv_lib_fwd(x, w, b, g, relu)
             return cl_dense(y, y_nhwc)
 
-        choice = _conv_pick("fwd", tuple(g) + (is_nhwc(x),),
-                            {"ours": lambda: _conv_ours_fwd(x, w, b, g, relu, y_nhwc), "lib": lib})
+        cands = {"ours": lambda: _conv_ours_fwd(x, w, b, g, relu, y_nhwc), "lib": lib}
+        if y_nhwc and _pointwise_gemm_ok(g, x):
+            cands["gemm"] = lambda: _conv_gemm_fwd(x, w, b, g, relu)
+        choice = _conv_pick("fwd", tuple(g) + (is_nhwc(x),), cands)
+        if choice == "gemm":
+            return _conv_gemm_fwd(x, w, b, g, relu)
         if choice == "ours":
             return _conv_ours_fwd(x, w, b, g, relu, y_nhwc)
         return lib()
@@ -1522,8 +1560,26 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None):
             _conv_ours_bwd(x, w, dy, g, dxo, dwo)
             return dxo, dwo
 
-        choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None, is_nhwc(x)),
-                            {"ours": ours, "lib": lambda: _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)})
+        cands = {"ours": ours, "lib": lambda: _conv_lib_bwd(x, w, dy, g, need_dx, dw is not None)}
+        gemm_ok = _pointwise_gemm_ok(g, x, dy) and (dw is None or (dw.dtype == torch.float32 and dw.is_contiguous()))
+        if gemm_ok:
+            def gemm_c():
+                dxo = torch.empty_like(x) if need_dx else None
+                dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
+                _conv_gemm_bwd(x, w, dy, g, dxo, dwo)
+                return dxo, dwo
+            cands["gemm"] = gemm_c
+        choice = _conv_pick("bwd", tuple(g) + (need_dx, dw is not None, is_nhwc(x)), cands)
+        if choice == "gemm" and gemm_ok:
+            acc_in = dx_acc is not None and dx_acc.dtype == x.dtype and is_nhwc(dx_acc)
+            dxo = dx_acc if acc_in else (torch.empty_like(x) if need_dx else None)
+            _conv_gemm_bwd(x, w, dy, g, dxo, dw, acc_in)
+            if dx_acc is not None and not acc_in:
+                dx_acc.add_(dxo)
+                return dx_acc
+            return dxo
+        if choice == "gemm":
+            choice = "ours"
         if choice == "ours":
             acc_in = dx_acc is not None and dx_acc.dtype == x.dtype and is_nhwc(dx_acc) == is_nhwc(x) and \
                 (dx_acc.is_contiguous() or is_nhwc(dx_acc))

@@ -762,6 +762,37 @@ def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     assert _rel(db, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("N,C,H,W,Ko", [(2, 64, 14, 14, 256), (4, 512, 7, 7, 128), (1, 256, 5, 3, 64)])
+def test_conv_pointwise_gemm(N, C, H, W, Ko):
+    """1x1 stride-1 convolutions over channel-last tensors as plain GEMMs over the pixel rows (the
+    conv pick's "gemm" candidate): forward with bias + ReLU, backward data (also accumulating into an
+    existing gradient) and backward filter (fp32, +=) against fp32 torch autograd."""
+    from flexflow_amd import kernels as K
+    torch.manual_seed(37)
+    x = K.cl_dense(torch.randn(N, C, H, W, device=DEV).bfloat16(), True)
+    w = (torch.randn(Ko, C, 1, 1, device=DEV) / math.sqrt(C)).bfloat16()
+    b = torch.randn(Ko, device=DEV).bfloat16()
+    g = K.conv_geometry(x, w, (1, 1), (0, 0), 1)
+    assert K._pointwise_gemm_ok(g, x)
+    y = K._conv_gemm_fwd(x, w, b, g, True)
+    assert K.is_nhwc(y)
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    ref = torch.relu(torch.nn.functional.conv2d(xr, wr, br))
+    assert _rel(y, ref) < 1e-2
+    dy = K.cl_dense(torch.randn_like(ref).bfloat16(), True)
+    ref.backward(dy.float() * (ref > 0).float())
+    dz = K.cl_dense((dy.float() * (y.float() > 0).float()).bfloat16(), True)
+    dx = torch.empty_like(x)
+    dw = torch.ones(w.shape, device=DEV)
+    K._conv_gemm_bwd(x, w, dz, g, dx, dw)
+    assert _rel(dx, xr.grad) < 1.5e-2
+    assert _rel(dw - 1.0, wr.grad) < 1e-2
+    acc0 = K.cl_dense(torch.randn_like(x), True)
+    acc = acc0.clone()
+    K._conv_gemm_bwd(x, w, dz, g, acc, None, True)
+    assert _rel(acc, acc0.float() + xr.grad) < 1.5e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("rows,d", [(300, 512), (64, 4096), (33, 100), (8, 8192)])
 def test_rmsnorm(rows, d, dtype):
