@@ -655,8 +655,12 @@ int64_t conv_ws(std::vector<int64_t> g) {
   const auto gi = conv_geom(g);
   return ffk::conv_ws_elems(gi[0], gi[1], gi[2], gi[3], gi[4], gi[5], gi[6], gi[7], gi[8], gi[13]);
 }
+int64_t conv_wpack(std::vector<int64_t> g) {
+  const auto gi = conv_geom(g);
+  return ffk::conv_wpack_elems(gi[1], gi[4], gi[7], gi[8], gi[13]);
+}
 void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, std::vector<int64_t> g, bool relu,
-                bool x_nhwc, bool y_nhwc) {
+                bool x_nhwc, bool y_nhwc, optional<Tensor> wpack_bwd) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
@@ -668,11 +672,13 @@ void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, 
               w.numel() == g[4] * (g[1] / g[13]) * g[7] * g[8], "conv2d_fwd: sizes");
   TORCH_CHECK(!bias.has_value() || (bias->scalar_type() == at::kBFloat16 && bias->numel() >= g[4]), "conv2d: bias");
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_fwd: workspace too small");
+  TORCH_CHECK(!wpack_bwd.has_value() || (wpack_bwd->scalar_type() == at::kBFloat16 && wpack_bwd->numel() >= conv_wpack(g)),
+              "conv2d_fwd: wpack_bwd");
   ffk::conv2d_fwd(x.data_ptr(), w.data_ptr(), ptr(bias), y.data_ptr(), ws.data_ptr(), gi.data(), relu, x_nhwc, y_nhwc,
-                  cur_stream());
+                  cur_stream(), ptr(wpack_bwd));
 }
 void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Tensor> dw, Tensor ws,
-                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc, bool accum_dx) {
+                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc, bool accum_dx, optional<Tensor> wpack) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv2d: bf16 tensors");
@@ -685,8 +691,10 @@ void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Ten
   TORCH_CHECK(!dw.has_value() || (dw->numel() == w.numel() && dw->scalar_type() == at::kFloat && dw->is_contiguous()),
               "conv2d_bwd: dw must be fp32 like w");
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_bwd: workspace too small");
+  TORCH_CHECK(!wpack.has_value() || (wpack->scalar_type() == at::kBFloat16 && wpack->numel() >= conv_wpack(g)),
+              "conv2d_bwd: wpack");
   ffk::conv2d_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), ptr(dx), ptr<float>(dw), ws.data_ptr(), gi.data(),
-                  dx.has_value(), x_nhwc, dy_nhwc, accum_dx && dx.has_value(), cur_stream());
+                  dx.has_value(), x_nhwc, dy_nhwc, accum_dx && dx.has_value(), cur_stream(), ptr(wpack));
 }
 
 }  // namespace
@@ -782,6 +790,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool2d_fwd", &pool2d_fwd);
   m.def("pool2d_bwd", &pool2d_bwd);
   m.def("conv_ws", &conv_ws);
+  m.def("conv_wpack", &conv_wpack);
   m.def("conv2d_fwd", &conv2d_fwd);
   m.def("conv2d_bwd", &conv2d_bwd);
 }

@@ -83,24 +83,32 @@ static void launch_nhwc(const bf16_t* x, bf16_t* xt, int N, int G, int Cg, int H
 
 // w [G*Kg][Cg][KH][KW] -> wp [G][Kg][KH][KW][Cp] + zero tail to Kp per row (forward operand), or
 // (transpose = 1) wp [G][Cg][KH][KW][Kgp] + tail (backward-data operand: rows = input channels)
+// wp2 (optional): the transposed image too (Kp2 per row), in the same launch — the forward packs the
+// backward-data operand of its step along with its own (conv2d_fwd's wpack_bwd)
 __global__ void __launch_bounds__(256) conv_pack_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp, int G,
-                                                        int Kg, int Cg, int KH, int KW, int Kp, int transpose) {
-  const int rows = transpose ? Cg : Kg;         // GEMM rows per group
-  const int red = transpose ? Kg : Cg;          // reduction channels
-  const int redp = (red + 7) / 8 * 8;
-  const int64_t total = (int64_t)G * rows * Kp;
+                                                        int Kg, int Cg, int KH, int KW, int Kp, int transpose,
+                                                        bf16_t* __restrict__ wp2 = nullptr, int Kp2 = 0) {
+  const int64_t total1 = wp ? (int64_t)G * (transpose ? Cg : Kg) * Kp : 0;
+  const int64_t total = total1 + (wp2 ? (int64_t)G * Cg * Kp2 : 0);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int k = (int)(i % Kp);
-    const int64_t gr = i / Kp;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < total; i0 += stride) {
+    const bool second = i0 >= total1;
+    const int tr = second ? 1 : transpose;
+    const int K_ = second ? Kp2 : Kp;
+    const int64_t i = second ? i0 - total1 : i0;
+    const int rows = tr ? Cg : Kg;  // GEMM rows per group
+    const int red = tr ? Kg : Cg;   // reduction channels
+    const int redp = (red + 7) / 8 * 8;
+    const int k = (int)(i % K_);
+    const int64_t gr = i / K_;
     const int row = (int)(gr % rows), g = (int)(gr / rows);
     const int c = k % redp, t = k / redp, kw = t % KW, kh = t / KW;
     uint16_t v = 0;
     if (kh < KH && c < red) {
-      const int co = transpose ? c : row, ci = transpose ? row : c;
+      const int co = tr ? c : row, ci = tr ? row : c;
       v = w[(((int64_t)(g * Kg + co) * Cg + ci) * KH + kh) * KW + kw];
     }
-    wp[i] = v;
+    (second ? wp2 : wp)[i] = v;
   }
 }
 
@@ -969,8 +977,12 @@ int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH,
   return xt + yt + align8(std::max(wf, wb)) + 2 * slabs + 64;
 }
 
+int64_t conv_wpack_elems(int C, int K, int KH, int KW, int G) {
+  return (int64_t)G * (C / G) * kpad(KH, KW, round8(K / G));
+}
+
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
-                int x_nhwc, int y_nhwc, hipStream_t st) {
+                int x_nhwc, int y_nhwc, hipStream_t st, void* wpack_bwd) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg);
@@ -986,17 +998,20 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   // a 1 x 1 filter over 64k input channels per group IS the packed operand ([G][Kg][Cg], rows of
   // Kp == Cg): no pack pass (36 of ResNet-50's 53 forward convolutions)
   const bf16_t* A = wp;
-  if (KH == 1 && KW == 1 && Cg % 64 == 0 && Kp == Cg) A = (const bf16_t*)w;
-  else
-    hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Kg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
-                       wp, G, Kg, Cg, KH, KW, Kp, 0);
+  const bool no_pack = KH == 1 && KW == 1 && Cg % 64 == 0 && Kp == Cg;
+  if (no_pack) A = (const bf16_t*)w;
+  const int Kpb = kpad(KH, KW, round8(Kg));
+  const int64_t packed = (no_pack ? 0 : (int64_t)G * Kg * Kp) + (wpack_bwd ? (int64_t)G * Cg * Kpb : 0);
+  if (packed > 0)
+    hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid(packed, 256)), dim3(256), 0, st, (const bf16_t*)w,
+                       no_pack ? nullptr : wp, G, Kg, Cg, KH, KW, Kp, 0, (bf16_t*)wpack_bwd, Kpb);
   IGemmArgs a{A, src, (bf16_t*)y, (const bf16_t*)bias, N, G, Kg, Kp, H, W, Cp, OH, OW, KH, KW, sh, sw, ph, pw, relu,
               y_nhwc, 0};
   launch_igemm<false>(a, (int64_t)N * OH * OW, Kg, G, st);
 }
 
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st) {
+                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st, const void* wpack) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
@@ -1011,9 +1026,11 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
   }
   if (need_dx) {
     const int Kp = kpad(KH, KW, Kgp);
-    hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st, (const bf16_t*)w,
-                       wp, G, Kg, Cg, KH, KW, Kp, 1);
-    IGemmArgs a{wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc,
+    // the operand packed by this step's forward (wpack), or packed here
+    if (!wpack)
+      hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st,
+                         (const bf16_t*)w, wp, G, Kg, Cg, KH, KW, Kp, 1, nullptr, 0);
+    IGemmArgs a{wpack ? (const bf16_t*)wpack : wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc,
                 accum_dx, conv_dgrad_phases() ? sh * sw : 1};
     launch_igemm<true>(a, (int64_t)N * H * W, Cg, G, st);
   }

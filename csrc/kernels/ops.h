@@ -157,9 +157,13 @@ void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint
 // staged through channel-last padded copies in ws; dx takes x's layout. geom: N C H W K OH OW KH KW
 // sh sw ph pw G
 int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH, int KW, int G);  // bf16 elems
+// wpack_bwd (optional, conv_wpack_elems): the forward also packs the backward-data weight operand,
+// which conv2d_bwd then takes as wpack instead of packing it again
+int64_t conv_wpack_elems(int C, int K, int KH, int KW, int G);
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
-                int x_nhwc, int y_nhwc, hipStream_t st);
+                int x_nhwc, int y_nhwc, hipStream_t st, void* wpack_bwd = nullptr);
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st);  // accum_dx: dx +=
+                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st,
+                const void* wpack = nullptr);  // accum_dx: dx +=
 
 }  // namespace ffk

@@ -1416,7 +1416,7 @@ def pool2d_bwd(x, y, dy, idx, kh, kw, sh, sw, pads, is_max, include_pad, relu):
 # GEMMs; FF_CONV_IMPL=ours|lib forces one. The choices land in TUNE_LOG.
 _conv_tuned: dict = {}
 _CONV_IMPL = _os.environ.get("FF_CONV_IMPL", "")
-_CONV_LIB_MARGIN = float(_os.environ.get("FF_CONV_LIB_MARGIN", "0.1"))
+_CONV_LIB_MARGIN = float(_os.environ.get("FF_CONV_LIB_MARGIN", "0.25"))
 
 
 def conv_geometry(x, w, stride, pad, groups):
@@ -1440,11 +1440,11 @@ def _conv_lib_bwd(x, w, dy, g, need_dx, need_dw):
     return dx, dw
 
 
-def _conv_ours_fwd(x, w, b, g, relu, y_nhwc):
+def _conv_ours_fwd(x, w, b, g, relu, y_nhwc, wpack_bwd=None):
     y = torch.empty((g[0], g[4], g[5], g[6]), device=x.device, dtype=x.dtype,
                     memory_format=torch.channels_last if y_nhwc else torch.contiguous_format)
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
-    ext().conv2d_fwd(x, w, b, y, ws, g, relu, _nhwc_flag(x, g[1] // g[13]), y_nhwc)
+    ext().conv2d_fwd(x, w, b, y, ws, g, relu, _nhwc_flag(x, g[1] // g[13]), y_nhwc, wpack_bwd)
     return y
 
 
@@ -1452,10 +1452,10 @@ def _nhwc_flag(t, c):
     return cl_ok(t, c) and is_nhwc(t)
 
 
-def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False):
+def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False, wpack=None):
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
     ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g, _nhwc_flag(x, g[1] // g[13]), _nhwc_flag(dy, g[4] // g[13]),
-                     accum_dx)
+                     accum_dx, wpack)
 
 
 def _pointwise_gemm_ok(g, *ts):
@@ -1503,9 +1503,10 @@ def _conv_pick(kind, key, cands):
         if not _TUNE or torch.cuda.is_current_stream_capturing():
             return "ours"
         times = _time_all(cands, rounds=2)  # interleaved, best of 2 rounds: single passes flipped choices
-        # MIOpen must win by _CONV_LIB_MARGIN: its timing in isolation leaves out the layout copies
-        # and tensor ops around it in the step (Inception-v3 b64: per-site picks 14.17 ms/step, all
-        # ours 14.02, with MIOpen ahead by 1-3 % at 9 of its 12 sites; profiles/conv_pick_ab_r4.txt)
+        # MIOpen must win by _CONV_LIB_MARGIN (25 %): its timing in isolation leaves out the layout
+        # copies and tensor ops around it in the step (Inception-v3 b64: per-site picks 14.17
+        # ms/step, all ours 14.02, with MIOpen ahead by 1-20 % at its 12 sites;
+        # profiles/conv_pick_ab_r4.txt)
         mine = min((k for k in times if k != "lib"), key=lambda k: times[k])
         choice = "lib" if times["lib"] < (1.0 - _CONV_LIB_MARGIN) * times[mine] else mine
         TUNE_LOG.append({"op": f"conv2d_{kind}", "geom": list(key), "times_ms": {k: round(v, 4) for k, v in
@@ -1514,11 +1515,19 @@ def _conv_pick(kind, key, cands):
     return choice
 
 
-def conv2d_fwd(x, w, b, stride, pad, groups, relu):
+def _bwd_picks_ours(g, nhwc):
+    """May this geometry's backward run our implicit-GEMM dgrad (its pick is "ours" or not made)?"""
+    seen = [_conv_tuned.get(("bwd", tuple(g) + (True, dw, nhwc))) for dw in (True, False)]
+    seen = [c for c in seen if c is not None]
+    return _CONV_IMPL in ("", "ours") and (not seen or "ours" in seen)
+
+
+def conv2d_fwd(x, w, b, stride, pad, groups, relu, bwd_pack=None):
     """y = [relu](conv2d(x, w) + b) (NCHW logical shapes). bf16 on the device: our implicit-GEMM
     kernel or MIOpen, whichever the per-geometry timing picked, with a channel-last output when
     CHANNELS_LAST (and the output channels per group are a multiple of 8); otherwise torch (fp32 /
-    CPU reference)."""
+    CPU reference). bwd_pack (a dict, training): our forward kernel also packs the backward-data
+    weight operand in its pack launch and leaves it in bwd_pack["w"] for conv2d_bwd(wpack=...)."""
     g = conv_geometry(x, w, stride, pad, groups)
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
         x = cl_dense(x, cl_ok(x, g[1] // groups))
@@ -1537,16 +1546,21 @@ def conv2d_fwd(x, w, b, stride, pad, groups, relu):
         if choice == "gemm":
             return _conv_gemm_fwd(x, w, b, g, relu)
         if choice == "ours":
-            return _conv_ours_fwd(x, w, b, g, relu, y_nhwc)
+            wpb = None
+            if bwd_pack is not None and _bwd_picks_ours(g, is_nhwc(x)) and not _pointwise_gemm_ok(g, x):
+                wpb = torch.empty(ext().conv_wpack(g), device=x.device, dtype=torch.bfloat16)
+                bwd_pack["w"] = wpb
+            return _conv_ours_fwd(x, w, b, g, relu, y_nhwc, wpb)
         return lib()
     return _conv_lib_fwd(x, w, b, g, relu)
 
 
-def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None):
+def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None, wpack=None):
     """Backward of conv2d_fwd for geometry g (conv_geometry): returns dx (or None) and adds the
     weight gradient into dw (fp32, shaped like w, may be None). dx_acc: an existing gradient of x
     that dx is added into (and returned): our dgrad kernel accumulates in its epilogue when dx_acc
-    has x's memory layout, otherwise a separate add."""
+    has x's memory layout, otherwise a separate add. wpack: the backward-data weight operand packed
+    by this step's forward (conv2d_fwd bwd_pack), used by our dgrad kernel instead of a pack pass."""
     if not need_dx:
         dx_acc = None
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16:
@@ -1585,10 +1599,10 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None):
                 (dx_acc.is_contiguous() or is_nhwc(dx_acc))
             dxo = dx_acc if acc_in else (torch.empty_like(x) if need_dx else None)
             if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.shape == w.shape:
-                _conv_ours_bwd(x, w, dy, g, dxo, dw, acc_in)  # the slab reduce adds into the gradient
+                _conv_ours_bwd(x, w, dy, g, dxo, dw, acc_in, wpack)  # the slab reduce adds into the gradient
             else:
                 dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
-                _conv_ours_bwd(x, w, dy, g, dxo, dwo, acc_in)
+                _conv_ours_bwd(x, w, dy, g, dxo, dwo, acc_in, wpack)
                 if dw is not None:
                     dw.add_(dwo.view_as(dw))
             if dx_acc is not None and not acc_in:

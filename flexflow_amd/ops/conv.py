@@ -152,15 +152,17 @@ class Conv2D(_Spatial):
         xc = K.cl_dense(xc, K.cl_ok(xc, xc.shape[1] // groups))  # the layout the kernels take (saved as such)
         act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
         relu = act == ActiMode.AC_MODE_RELU
-        z = K.conv2d_fwd(xc, w, b, (sh, sw), pad, groups, relu)
+        pk = {} if ctx.training else None
+        z = K.conv2d_fwd(xc, w, b, (sh, sw), pad, groups, relu, bwd_pack=pk)
         y = z if act in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU) else K.act_ref(z, act.value)
         if ctx.training:
-            ctx.saved.update(xc=xc, w=w, z=z, y=y, pad=pad, x_shape=x.shape, has_b=b is not None)
+            ctx.saved.update(xc=xc, w=w, z=z, y=y, pad=pad, x_shape=x.shape, has_b=b is not None, wpack=pk.get("w"))
         return [y]
 
     def backward(self, ctx, douts):
         s = ctx.saved
-        xc, w, z, y, pad, x_shape, has_b = (s.pop(k) for k in ("xc", "w", "z", "y", "pad", "x_shape", "has_b"))
+        xc, w, z, y, pad, x_shape, has_b, wpack = (s.pop(k) for k in ("xc", "w", "z", "y", "pad", "x_shape", "has_b",
+                                                                        "wpack"))
         act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
         dy = douts[0].to(y.dtype)
         if act not in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU):
@@ -173,7 +175,7 @@ class Conv2D(_Spatial):
         acc = (ctx.extra.get("dx_accum") or {}).get(0)
         if acc is not None and tuple(xc.shape) != tuple(x_shape):
             acc = None  # attribute-parallel crop: dx is scattered into a fresh block below
-        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True), dx_acc=acc)
+        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True), dx_acc=acc, wpack=wpack)
         if dx is None:  # the input needs no gradient (the data, or a frozen producer)
             return [None]
         if tuple(dx.shape) != tuple(x_shape):  # attribute-parallel: scatter crop back into halo'd block

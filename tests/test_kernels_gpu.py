@@ -752,6 +752,13 @@ def test_conv2d_implicit_gemm(geo, layout, monkeypatch):
     K._conv_ours_bwd(x, w, dz, g, dx, dw)
     assert _rel(dx, xr.grad) < 1.5e-2
     assert _rel(dw, wr.grad) < 1e-2
+    # the backward-data operand packed by the forward's pack launch: the same dgrad, bitwise
+    wpb = torch.empty(K.ext().conv_wpack(g), device=DEV, dtype=torch.bfloat16)
+    y2 = K._conv_ours_fwd(x, w, b, g, True, y_nhwc, wpb)
+    assert torch.equal(y2, y)
+    dx2 = torch.empty_like(x)
+    K._conv_ours_bwd(x, w, dz, g, dx2, None, False, wpb)
+    assert torch.equal(dx2, dx)
     # dgrad accumulating into an existing gradient (a tensor with several consumers)
     acc0 = torch.randn_like(x)
     acc = acc0.clone()
