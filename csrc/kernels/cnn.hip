@@ -497,8 +497,17 @@ __global__ void __launch_bounds__(256) bn_bwd_dx_nhwc_kernel(const bf16_t* __res
   }
 }
 
-// splits of the NHWC column reduction: ~1k workgroups over (channel blocks x splits), each split
-// at least one full trip of U x R rows
+// splits of the NHWC column reduction: ~FF_BN_WG (default 1024) workgroups over (channel blocks x
+// splits), each split at least one full trip of U x R rows. Fewer splits make each workgroup's
+// share longer and the finalize's fold shorter.
+static int bn_wg_target() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_BN_WG");
+    v = e ? std::max(1, atoi(e)) : 1024;
+  }
+  return v;
+}
 static ColGeom nhwc_geom(int64_t M, int C, int max_splits = 1024) {
   ColGeom q;
   q.M = M;
@@ -508,7 +517,8 @@ static ColGeom nhwc_geom(int64_t M, int C, int max_splits = 1024) {
   q.R = 256 / q.L;
   const int ncb = (q.C8 + 31) / 32;
   const int64_t trips = (M + 4LL * q.R - 1) / (4LL * q.R);
-  q.S = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(1024 + ncb - 1) / ncb, trips, (int64_t)max_splits}));
+  const int64_t wg = bn_wg_target();
+  q.S = (int)std::max<int64_t>(1, std::min<int64_t>({(wg + ncb - 1) / ncb, trips, (int64_t)max_splits}));
   return q;
 }
 
