@@ -673,15 +673,16 @@ __device__ __forceinline__ int offc_swz(int row) {
                   : (((row & 3) << 2) | ((row >> 2) & 3));
 }
 
-template <int TM>
+// BP pixels per stage, NS stages in the ring (NS - 1 in flight under the MFMAs of the current one)
+template <int TM, int BP = 64, int NS = 2>
 __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
-  constexpr int TN = 128, BP = 64;
+  constexpr int TN = 128;
   constexpr int TIA = BP * TM * 2, TIB = BP * TN * 2;
   constexpr int WA = TIA / 1024 / 4, WB = TIB / 1024 / 4;  // pieces per wave per step
   constexpr int RA = 1024 / (TM * 2), RB = 1024 / (TN * 2);  // image rows per piece
   constexpr int MTM = TM / 64, MTN = TN / 64;
   constexpr int BAD = 0x7ffffff0;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TIA + TIB)];
+  __shared__ __attribute__((aligned(16))) char smem[NS * (TIA + TIB)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int co0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
@@ -735,7 +736,7 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
       const bool ok = bn[i] < a.N && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
       const int off = ok ? (int)(((((int64_t)bn[i] * a.H + ih) * a.W + iw) * a.G * a.Cp + bcol[i]) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
-      bow[i] += dr;  // next step: 64 pixels on
+      bow[i] += dr;  // next step: BP pixels on
       boh[i] += dq;
       if (bow[i] >= a.OW) { bow[i] -= a.OW; ++boh[i]; }
       if (boh[i] >= a.OH) { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
@@ -747,12 +748,16 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
 #pragma unroll
     for (int j = 0; j < MTN; ++j) acc[i][j] = f32x16{};
   const int G4 = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
-  if (s0 < s1) issue(0, s0);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (s0 + q < s1) issue(q, s0 + q);
   for (int64_t st = s0; st < s1; ++st) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // step st visible to all waves; every wave is done reading the other buffer
-    if (st + 1 < s1) issue((int)((st + 1 - s0) & 1), st + 1);
-    const char* la = smem + (int)((st - s0) & 1) * (TIA + TIB);
+    // stage st landed (the NS - 2 stages issued after it may stay in flight)
+    if (NS > 2 && st + NS - 2 < s1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (WA + WB)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st visible to all waves; every wave is done reading stage st - 1's buffer
+    if (st + NS - 1 < s1) issue((int)((st + NS - 1 - s0) % NS), st + NS - 1);
+    const char* la = smem + (int)((st - s0) % NS) * (TIA + TIB);
     const char* lb = la + TIA;
 #pragma unroll
     for (int ks = 0; ks < BP / 16; ++ks) {
@@ -956,6 +961,16 @@ static int wgrad_splits(int64_t P, int G, int Kg, int NC) {
 
 static int64_t align8(int64_t v) { return (v + 7) / 8 * 8; }
 
+// backward-filter ring: 0 = two 64-pixel stages, 1 = four 32-pixel stages (FF_CONV_WGRAD_PIPE)
+static int conv_wgrad_pipe() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_CONV_WGRAD_PIPE");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 // stride-phase backward-data (conv_igemm_dma_kernel<.., PH>): FF_CONV_DGRAD_PHASES=0 turns it off
 static bool conv_dgrad_phases() {
   static int v = -1;
@@ -1048,7 +1063,10 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
     WGradArgs b{ysrc, xsrc, slabs, N, G, Kg, Kgp, Cp, H, W, OH, OW, KH, KW, sh, sw, ph, pw, NC, S};
     const dim3 grid((Kg + TM - 1) / TM, (NC + 127) / 128, G * S);
     const bool dma = P * G * Kgp * 2 < 0x7fff0000LL && (int64_t)N * H * W * G * Cp * 2 < 0x7fff0000LL;
-    if (dma) {
+    if (dma && conv_wgrad_pipe() == 1) {  // 32-pixel stages, 4 deep
+      if (TM == 128) hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 32, 4>), grid, dim3(256), 0, st, b);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 32, 4>), grid, dim3(256), 0, st, b);
+    } else if (dma) {
       if (TM == 128) hipLaunchKernelGGL(conv_wgrad_dma_kernel<128>, grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL(conv_wgrad_dma_kernel<64>, grid, dim3(256), 0, st, b);
     } else {
