@@ -61,6 +61,12 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"compile failed: {cmd[-1] if cmd else ''}")
 
 
+def _stamp_text(cmd) -> str:
+    """The compile command with the tree's own path factored out: a copy of the tree elsewhere (the
+    GPU box's snapshot) does not rebuild objects whose flags did not change."""
+    return " ".join(cmd).replace(os.path.dirname(os.path.abspath(__file__)), "<root>")
+
+
 def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
     inc, tlib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
@@ -82,13 +88,13 @@ def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
                    *sum([["-isystem", i] for i in inc], []), "-isystem", py_inc, "-c", src, "-o", obj]
         stamp = obj + ".cmd"  # the compile command: a flag change rebuilds the object
         prev = open(stamp).read() if os.path.exists(stamp) else ""
-        if _newer(src, obj, headers) or prev != " ".join(cmd):
+        if _newer(src, obj, headers) or prev != _stamp_text(cmd):
             jobs_list.append(cmd)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(_run, jobs_list))
     for cmd in jobs_list:  # stamped once every compile succeeded
         with open(cmd[-1] + ".cmd", "w") as f:
-            f.write(" ".join(cmd))
+            f.write(_stamp_text(cmd))
     out = os.path.join(PKG, "_C.so")
     if jobs_list or not os.path.exists(out):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-L", tlib, f"-Wl,-rpath,{tlib}",
