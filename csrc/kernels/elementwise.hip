@@ -393,30 +393,40 @@ __global__ void col_reduce_add_kernel(const float* __restrict__ part, Outs3 o, i
 // summed in a fixed order, a plain read-modify-write of the output (no float atomics: the atomic
 // form's adds contended with the overlapped optimizer's traffic in the step, 6 us median but up to
 // 150 us per call, and its sum order varied run to run).
+// 32 columns (one 128-B line per row) x 32 row lanes per block, 8 independent loads in flight per
+// lane: the fold of a 1024-row slab is 4 load round trips per lane. (64 columns x 16 lanes with 4 in
+// flight took 16 round trips: 16 us per LayerNorm-backward fold, 1.6 ms of the BERT-Large step.)
 __global__ void __launch_bounds__(1024) col_reduce_det_kernel(const float* __restrict__ part, Outs3 o, int R, int C) {
-  __shared__ float red[16][65];
+  constexpr int CW = 32, RL = 32, U = 8;
+  __shared__ float red[RL][CW + 1];
   const int k = o.which[blockIdx.y];
   const float* p = part + (int64_t)k * R * C;
   float* out = o.p[k];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  float s = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const int c = blockIdx.x * CW + (threadIdx.x % CW);
+  const int rl = threadIdx.x / CW;
+  float acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.f;
   if (c < C) {
     int r = rl;
-    for (; r + 48 < R; r += 64) {
-      s += p[(int64_t)r * C + c];
-      s1 += p[(int64_t)(r + 16) * C + c];
-      s2 += p[(int64_t)(r + 32) * C + c];
-      s3 += p[(int64_t)(r + 48) * C + c];
+    for (; r + (U - 1) * RL < R; r += U * RL) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(r + u * RL) * C + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += v[u];
     }
-    for (; r < R; r += 16) s += p[(int64_t)r * C + c];
+    for (; r < R; r += RL) acc[0] += p[(int64_t)r * C + c];
   }
-  red[rl][threadIdx.x & 63] = (s + s1) + (s2 + s3);
+  float t0 = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) t0 += acc[u];
+  red[rl][threadIdx.x % CW] = t0;
   __syncthreads();
   if (rl == 0 && c < C) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+    for (int i = 0; i < RL; ++i) t += red[i][threadIdx.x];
     out[c] += t;
   }
 }
@@ -441,7 +451,7 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
     if (o.p[k]) o.which[nz++] = k;
   if (!nz) return;
   if (col_reduce_gy() == 0) {
-    hipLaunchKernelGGL(col_reduce_det_kernel, dim3((C + 63) / 64, nz), dim3(1024), 0, st, part, o, R, C);
+    hipLaunchKernelGGL(col_reduce_det_kernel, dim3((C + 31) / 32, nz), dim3(1024), 0, st, part, o, R, C);
     return;
   }
   const int gy = std::max(1, std::min(col_reduce_gy(), R / 8));
