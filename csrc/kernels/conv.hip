@@ -721,25 +721,38 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
     boh[i] = rem / a.OW;
     bow[i] = rem - boh[i] * a.OW;
   }
+  // 32-bit cursors (both buffers are under 2 GiB on this path): the per-step address work is the
+  // kernel's issue bottleneck at small Kg (profiles/conv_wgrad_pmc_r4.txt)
+  const int ldy2 = a.G * a.Kgs * 2, lx2 = a.G * a.Cp * 2, P32 = (int)P;
+  int pa[WA], aoffs[WA];
+#pragma unroll
+  for (int i = 0; i < WA; ++i) {
+    pa[i] = (int)(s0 * BP) + arow[i];
+    aoffs[i] = pa[i] * ldy2 + acol[i] * 2;
+  }
   auto issue = [&](int buf, int64_t st) {
     char* la = smem + buf * (TIA + TIB);
     char* lb = la + TIA;
 #pragma unroll
     for (int i = 0; i < WA; ++i) {
-      const int64_t p = st * BP + arow[i];
-      const int off = (acol[i] >= 0 && p < P) ? (int)((p * a.G * a.Kgs + acol[i]) * 2) : BAD;
+      const int off = (acol[i] >= 0 && pa[i] < P32) ? aoffs[i] : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy, (lds_ptr_t)(la + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+      pa[i] += BP;
+      aoffs[i] += BP * ldy2;
     }
 #pragma unroll
     for (int i = 0; i < WB; ++i) {
       const int ih = boh[i] * a.sh - a.ph + bkh[i], iw = bow[i] * a.sw - a.pw + bkw[i];
-      const bool ok = bn[i] < a.N && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      const int off = ok ? (int)(((((int64_t)bn[i] * a.H + ih) * a.W + iw) * a.G * a.Cp + bcol[i]) * 2) : BAD;
+      const bool ok = bn[i] < a.N && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const int off = ok ? ((bn[i] * a.H + ih) * a.W + iw) * lx2 + bcol[i] * 2 : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
       bow[i] += dr;  // next step: BP pixels on
       boh[i] += dq;
       if (bow[i] >= a.OW) { bow[i] -= a.OW; ++boh[i]; }
-      if (boh[i] >= a.OH) { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
+      if (boh[i] >= a.OH) {
+        if (boh[i] < 2 * a.OH) { boh[i] -= a.OH; ++bn[i]; }  // the usual wrap: no integer division
+        else { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
+      }
     }
   };
   f32x16 acc[MTM][MTN];
