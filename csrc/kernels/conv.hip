@@ -436,6 +436,7 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
   // reduction cursor of this lane's chunk: K index ks * 8 + ch -> (kh, kw, c8); with PH, (th, tw,
   // c8) over the phase's taps (kh, kw below hold th, tw)
   const int KWc = PH ? (KWq > 0 ? KWq : 1) : a.KW, KHc = PH ? KHq : a.KH;
+  const bool unit_stride = a.sh == 1 && a.sw == 1;  // backward-data without the stride divisions
   int c8 = ch % C8, kw = (ch / C8) % KWc, kh = ch / C8 / KWc;
   auto issue = [&](int buf, int ks) {
     char* la = smem + buf * (TA + TB);
@@ -457,6 +458,9 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
       } else if (!BWD) {
         sy = prow[i] * a.sh - a.ph + kh;
         sx = pcol[i] * a.sw - a.pw + kw;
+      } else if (unit_stride) {  // backward-data, stride 1: the source pixel is the shifted one
+        sy = prow[i] + a.ph - kh;
+        sx = pcol[i] + a.pw - kw;
       } else {  // source (output-gradient) pixel whose window at (kh, kw) covers this input pixel
         const int ny = prow[i] + a.ph - kh, nx = pcol[i] + a.pw - kw;
         ok = ok && ny >= 0 && nx >= 0 && ny % a.sh == 0 && nx % a.sw == 0;
