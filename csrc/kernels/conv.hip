@@ -437,6 +437,19 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
   // c8) over the phase's taps (kh, kw below hold th, tw)
   const int KWc = PH ? (KWq > 0 ? KWq : 1) : a.KW, KHc = PH ? KHq : a.KH;
   const bool unit_stride = a.sh == 1 && a.sw == 1;  // backward-data without the stride divisions
+  // fast addressing (forward, stride phases, stride-1 backward-data): the source pixel is
+  // (yb + SG kh, xb + SG kw), so a piece's byte offset is its pixel base plus a per-lane tap term
+  // computed once per step — the operand issue is the kernel's VALU bottleneck
+  constexpr int SG = BWD ? -1 : 1;
+  const bool fast = PH || !BWD || unit_stride;
+  const int GC2 = a.G * a.Cs * 2;
+  int yb[WB], xb[WB], pixb[WB];
+#pragma unroll
+  for (int i = 0; i < WB; ++i) {
+    yb[i] = PH ? prow[i] + oy0 : (!BWD ? prow[i] * a.sh - a.ph : prow[i] + a.ph);
+    xb[i] = PH ? pcol[i] + ox0 : (!BWD ? pcol[i] * a.sw - a.pw : pcol[i] + a.pw);
+    pixb[i] = (pbase[i] + yb[i] * a.Ws + xb[i]) * GC2 + g * a.Cs * 2;
+  }
   int c8 = ch % C8, kw = (ch / C8) % KWc, kh = ch / C8 / KWc;
   auto issue = [&](int buf, int ks) {
     char* la = smem + buf * (TA + TB);
@@ -448,6 +461,16 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
       const int off = (aoff[i] == BAD || acol == BAD) ? BAD : aoff[i] + acol;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(la + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
     }
+    if (fast) {
+      const int tap = (SG * kh * a.Ws + SG * kw) * GC2 + c8 * 16;
+#pragma unroll
+      for (int i = 0; i < WB; ++i) {
+        const bool ok = pok[i] && kh < KHc && (unsigned)(yb[i] + SG * kh) < (unsigned)a.Hs &&
+                        (unsigned)(xb[i] + SG * kw) < (unsigned)a.Ws;
+        const int off = ok ? pixb[i] + tap : BAD;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < WB; ++i) {
       bool ok = pok[i] && kh < KHc;
@@ -470,6 +493,7 @@ __global__ void __launch_bounds__(256) conv_igemm_dma_kernel(IGemmArgs a) {
       ok = ok && sy >= 0 && sy < a.Hs && sx >= 0 && sx < a.Ws;
       const int off = ok ? (((pbase[i] + sy * a.Ws + sx) * a.G + g) * a.Cs + c8 * 8) * 2 : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
+    }
     }
     c8 += 8;  // next step: 8 chunks on
     while (c8 >= C8) {
