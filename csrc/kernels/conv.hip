@@ -752,6 +752,20 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
   // 32-bit cursors (both buffers are under 2 GiB on this path): the per-step address work is the
   // kernel's issue bottleneck at small Kg (profiles/conv_wgrad_pmc_r4.txt)
   const int ldy2 = a.G * a.Kgs * 2, lx2 = a.G * a.Cp * 2, P32 = (int)P;
+  // x pieces: the output pixel's input origin (ihb, iwb) = (oh sh, ow sw) and its byte offset pixb
+  // advance incrementally; the piece's fixed tap (kh - ph, kw - pw) and channel are one constant
+  const int stepB = (dr * a.sw + dq * a.sh * a.W) * lx2, wrapW = (a.sh * a.W - a.OW * a.sw) * lx2,
+            wrapH = (a.H * a.W - a.OH * a.sh * a.W) * lx2;
+  int ihb[WB], iwb[WB], pixb[WB], tapb[WB];
+#pragma unroll
+  for (int i = 0; i < WB; ++i) {
+    ihb[i] = boh[i] * a.sh;
+    iwb[i] = bow[i] * a.sw;
+    pixb[i] = ((bn[i] * a.H + ihb[i]) * a.W + iwb[i]) * lx2;
+    bkh[i] -= a.ph;  // from here on: the tap's offset from the window origin
+    bkw[i] -= a.pw;
+    tapb[i] = (bkh[i] * a.W + bkw[i]) * lx2 + bcol[i] * 2;
+  }
   int pa[WA], aoffs[WA];
 #pragma unroll
   for (int i = 0; i < WA; ++i) {
@@ -770,16 +784,28 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_dma_kernel(WGradArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < WB; ++i) {
-      const int ih = boh[i] * a.sh - a.ph + bkh[i], iw = bow[i] * a.sw - a.pw + bkw[i];
-      const bool ok = bn[i] < a.N && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const int off = ok ? ((bn[i] * a.H + ih) * a.W + iw) * lx2 + bcol[i] * 2 : BAD;
+      const bool ok = bn[i] < a.N && (unsigned)(ihb[i] + bkh[i]) < (unsigned)a.H &&
+                      (unsigned)(iwb[i] + bkw[i]) < (unsigned)a.W;
+      const int off = ok ? pixb[i] + tapb[i] : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(lb + (i * 4 + wave) * 1024), 16, off, 0, 0, 0);
       bow[i] += dr;  // next step: BP pixels on
       boh[i] += dq;
-      if (bow[i] >= a.OW) { bow[i] -= a.OW; ++boh[i]; }
-      if (boh[i] >= a.OH) {
-        if (boh[i] < 2 * a.OH) { boh[i] -= a.OH; ++bn[i]; }  // the usual wrap: no integer division
-        else { bn[i] += boh[i] / a.OH; boh[i] %= a.OH; }
+      iwb[i] += dr * a.sw;
+      ihb[i] += dq * a.sh;
+      pixb[i] += stepB;
+      if (bow[i] >= a.OW) {
+        bow[i] -= a.OW;
+        ++boh[i];
+        iwb[i] -= a.OW * a.sw;
+        ihb[i] += a.sh;
+        pixb[i] += wrapW;
+      }
+      if (boh[i] >= a.OH) {  // next image(s): usually one, no integer division
+        const int k = boh[i] < 2 * a.OH ? 1 : boh[i] / a.OH;
+        boh[i] -= k * a.OH;
+        ihb[i] -= k * a.OH * a.sh;
+        bn[i] += k;
+        pixb[i] += k * wrapH;
       }
     }
   };
