@@ -22,6 +22,8 @@
 //     operands arrive as [pixel][channel] images and are read transposed with ds_read_b64_tr_b16 —
 //     the attention dV^T = dO^T . P operand path; the splits' fp32 tiles go to slabs that one
 //     reduce pass adds into the weight gradient (no atomics).
+#include <stdexcept>
+
 #include "common.h"
 #include "ops.h"
 
@@ -88,25 +90,27 @@ static void launch_nhwc(const bf16_t* x, bf16_t* xt, int N, int G, int Cg, int H
 __global__ void __launch_bounds__(256) conv_pack_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp, int G,
                                                         int Kg, int Cg, int KH, int KW, int Kp, int transpose,
                                                         bf16_t* __restrict__ wp2 = nullptr, int Kp2 = 0) {
-  const int64_t total1 = wp ? (int64_t)G * (transpose ? Cg : Kg) * Kp : 0;
-  const int64_t total = total1 + (wp2 ? (int64_t)G * Cg * Kp2 : 0);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < total; i0 += stride) {
+  // 32-bit index math (weights are far below 2^31 elements; the host checks): the 64-bit divisions
+  // of the first version made a 37k-element pack take ~8 us
+  const unsigned total1 = wp ? (unsigned)G * (transpose ? Cg : Kg) * Kp : 0u;
+  const unsigned total = total1 + (wp2 ? (unsigned)G * Cg * Kp2 : 0u);
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < total; i0 += stride) {
     const bool second = i0 >= total1;
     const int tr = second ? 1 : transpose;
-    const int K_ = second ? Kp2 : Kp;
-    const int64_t i = second ? i0 - total1 : i0;
-    const int rows = tr ? Cg : Kg;  // GEMM rows per group
-    const int red = tr ? Kg : Cg;   // reduction channels
-    const int redp = (red + 7) / 8 * 8;
-    const int k = (int)(i % K_);
-    const int64_t gr = i / K_;
-    const int row = (int)(gr % rows), g = (int)(gr / rows);
-    const int c = k % redp, t = k / redp, kw = t % KW, kh = t / KW;
+    const unsigned K_ = second ? (unsigned)Kp2 : (unsigned)Kp;
+    const unsigned i = second ? i0 - total1 : i0;
+    const unsigned rows = tr ? Cg : Kg;  // GEMM rows per group
+    const int red = tr ? Kg : Cg;        // reduction channels
+    const unsigned redp = (red + 7) / 8 * 8;
+    const unsigned gr = i / K_, k = i - gr * K_;
+    const unsigned g = gr / rows, row = gr - g * rows;
+    const unsigned t = k / redp, c = k - t * redp;
+    const unsigned kh = t / KW, kw = t - kh * KW;
     uint16_t v = 0;
-    if (kh < KH && c < red) {
-      const int co = tr ? c : row, ci = tr ? row : c;
-      v = w[(((int64_t)(g * Kg + co) * Cg + ci) * KH + kh) * KW + kw];
+    if ((int)kh < KH && (int)c < red) {
+      const unsigned co = tr ? c : row, ci = tr ? row : c;
+      v = w[((((size_t)g * Kg + co) * Cg + ci) * KH + kh) * KW + kw];
     }
     (second ? wp2 : wp)[i] = v;
   }
@@ -1084,6 +1088,7 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   if (no_pack) A = (const bf16_t*)w;
   const int Kpb = kpad(KH, KW, round8(Kg));
   const int64_t packed = (no_pack ? 0 : (int64_t)G * Kg * Kp) + (wpack_bwd ? (int64_t)G * Cg * Kpb : 0);
+  if (packed >= (1ll << 31)) throw std::runtime_error("conv2d: packed weights of 2^31 or more elements");
   if (packed > 0)
     hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid(packed, 256)), dim3(256), 0, st, (const bf16_t*)w,
                        no_pack ? nullptr : wp, G, Kg, Cg, KH, KW, Kp, 0, (bf16_t*)wpack_bwd, Kpb);
@@ -1109,6 +1114,7 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
   if (need_dx) {
     const int Kp = kpad(KH, KW, Kgp);
     // the operand packed by this step's forward (wpack), or packed here
+    if ((int64_t)G * Cg * Kp >= (1ll << 31)) throw std::runtime_error("conv2d: packed weights of 2^31 or more elements");
     if (!wpack)
       hipLaunchKernelGGL(conv_pack_kernel, dim3(ew_grid((int64_t)G * Cg * Kp, 256)), dim3(256), 0, st,
                          (const bf16_t*)w, wp, G, Kg, Cg, KH, KW, Kp, 1, nullptr, 0);
