@@ -433,6 +433,7 @@ void aggregate_bwd(Tensor dout, optional<Tensor> gate, std::vector<optional<Tens
   const int64_t B = dout.size(0), D = dout.numel() / B;
   const int64_t n = (int64_t)exps.size();
   TORCH_CHECK(expert.numel() == B * k && pos.numel() == B * k && load.numel() == n && dexps.size() == exps.size());
+  TORCH_CHECK(k >= 1 && k <= 64, "aggregate_bwd: at most 64 choices per row (the kernel's per-row LDS dot array)");
   if (dgate.has_value() && dgate->defined()) TORCH_CHECK(dgate->numel() == B * k && dgate->scalar_type() == dout.scalar_type());
   if (dfull.has_value() && dfull->defined()) TORCH_CHECK(dfull->numel() == B * n && dfull->scalar_type() == dout.scalar_type());
   auto pe = ptr_list(exps, dout.scalar_type(), cap * D);

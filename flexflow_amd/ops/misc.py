@@ -225,7 +225,8 @@ class Aggregate(OpImpl):
     """inputs: gate_preds [B,k], gate_assign [B,k], true_assign [B,k], full_gate_preds [B,n],
     exp_preds x n ([cap, D]). out[b] = sum_j gate_preds[b,j] * exp_pred[assign[b,j]][row].
     Backward (reference aggregate.cu): expert grads = gate * dout; full-gate grads = dout.exp_pred
-    plus lambda_bal * expert load, made zero-mean per row. AggregateSpec skips the gate product."""
+    plus lambda_bal * n / B * expert load (the reference's scaling, aggregate.cu:194), made zero-mean
+    per row. AggregateSpec skips the gate product."""
 
     @classmethod
     def infer(cls, attrs, in_dims, in_dtypes):
@@ -279,8 +280,9 @@ class Aggregate(OpImpl):
             dexp = [torch.empty_like(x) for x in ex]
             dgate = None if spec else torch.empty((B, k), dtype=dt, device=dout.device)
             dfull = None if spec else torch.empty(tuple(s["full_shape"]), dtype=dt, device=dout.device)
+            lam = float(self.attrs.get("lambda_bal", 0.0)) * n / max(B, 1)  # reference aggregate.cu:194
             K.ext().aggregate_bwd(dout, g, ex, dexp, e, pos, s["assign"], s["true_assign"], load,
-                                  float(self.attrs.get("lambda_bal", 0.0)), dgate, dfull, s["cap"], k)
+                                  lam, dgate, dfull, s["cap"], k)
             gdt, fdt = s["gate_dtype"], s["full_dtype"]
             ctx.saved.clear()
             return [None if dgate is None else dgate.to(gdt), None, None,
@@ -299,7 +301,7 @@ class Aggregate(OpImpl):
         dfull = None
         if not s["spec"]:
             dgate = (dgrow * rows).sum(-1).reshape(B, k).to(s["gate_dtype"])
-            lam = float(self.attrs.get("lambda_bal", 0.0))
+            lam = float(self.attrs.get("lambda_bal", 0.0)) * n / max(B, 1)  # reference aggregate.cu:194
             full = torch.zeros(s["full_shape"], dtype=torch.float32, device=dout.device)
             corr = (s["assign"] == s["true_assign"]).all(-1)
             contrib = (dgrow * rows).sum(-1) * corr.repeat_interleave(k)

@@ -102,7 +102,12 @@ def load_checkpoint(model, path: str, strict: bool = True):
         md = f.metadata() or {}
     if "arenas" not in md:
         # written before per-entry layouts were stored: the old whole-arena copy is safe only when
-        # this job's arenas have exactly the sizes the shard holds (same placement and layout)
+        # this job has the writer's world size and strategy (checked above under strict=True) AND
+        # its arenas have exactly the sizes the shard holds; equal sizes alone do not mean equal
+        # contents (a permuted placement or bucket order gives equal sizes)
+        if not strict:
+            raise ValueError(f"{fn} has no per-entry arena layout (written by an older version); it can only be "
+                             "loaded with strict=True (same world size and strategy)")
         arenas = _arenas(ex)
         if not all(f"arena{i}.master" in tensors and tensors[f"arena{i}.master"].numel() == ar.size
                    for i, ar in arenas):

@@ -86,9 +86,9 @@ class StepGraph:
             return False
         if self.failed or ex.hooks:  # per-op hooks time / inspect individual ops: run eagerly
             return False
-        # multi-rank: captured by default over RCCL (the bucket all-reduces are joined inside the
-        # graph, see step()); the 'auto' timing decision is agreed over all ranks
-        return _collectives_capturable(ex, "1")
+        # multi-rank: captured over RCCL only with FF_GRAPH_COLLECTIVES=1 (the bucket all-reduces
+        # are then joined inside the graph, see step()); every decision is agreed over all ranks
+        return _collectives_capturable(ex, "0")
 
     def step(self):
         m = self.model
@@ -129,8 +129,10 @@ class StepGraph:
                     self.decision = False
             return
         if self.graph is None:
+            import torch.distributed as dist
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
+            err = None
             try:
                 with torch.cuda.graph(g):
                     ex.zero_gradients()
@@ -140,13 +142,20 @@ class StepGraph:
                         # every bucket all-reduce is issued and joined back into the captured
                         # stream, so update() after a replay finds final gradients and no handle
                         ex.bucketer.flush()
-            except Exception as e:  # fall back to eager, loudly
+            except Exception as e:  # noqa: BLE001 - any capture error falls back to eager
+                err = e
+            # capture success is agreed over the world: a rank replaying its graph while a peer
+            # runs eagerly would issue its collectives in a different order
+            ok = _agree(ex, 0.0 if err is not None else 1.0, dist.ReduceOp.MIN) > 0.5
+            if not ok:
                 self.failed = True
-                print(f"[flexflow_amd] hipGraph capture failed ({e}); running eagerly", flush=True)
+                why = err if err is not None else "a peer rank's capture failed"
+                print(f"[flexflow_amd] hipGraph capture failed ({why}); running eagerly", flush=True)
+                del g
                 torch.cuda.synchronize()
                 ex.zero_gradients()
                 ex.forward()
-                ex.backward()
+                ex.backward(overlap_update=ov)
                 ex.update(m.optimizer)
                 return
             self.graph = g

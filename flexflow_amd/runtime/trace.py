@@ -103,8 +103,11 @@ def traced_call(model, name: str, run) -> None:
         st.cur.append(name)
         if len(st.cur) == 1 and st.iters in (1, 2) and _timing_wanted(st):
             _start_timer(st)  # eager iterations 2 and 3 are timed (the first pays autotuning)
-        if st.iters >= 2 and st.seq and len(st.cur) == 1 and name == st.seq[0]:
-            from .graph import capturable
+        # capture in iteration 4 (iters == 3): eager iterations 2 and 3 have both been timed
+        if st.iters >= 3 and st.seq and len(st.cur) == 1 and name == st.seq[0]:
+            import torch.distributed as dist
+
+            from .graph import _agree, capturable
             ex = model.executor
             decision = _decide(st)
             # one graph per update: the row-sparse SGD plan and several backward passes per update
@@ -113,14 +116,19 @@ def traced_call(model, name: str, run) -> None:
                     and not ex._sparse_plan(model.optimizer)):
                 st.ev = None
                 g = torch.cuda.CUDAGraph()
+                err = None
                 try:
                     torch.cuda.synchronize()
                     with torch.cuda.graph(g):
                         for n in st.seq:
                             getattr(model, "_eager_" + n)()
-                except Exception as e:  # fall back to eager, loudly
+                except Exception as e:  # noqa: BLE001 - fall back to eager, loudly
+                    err = e
+                # every rank replays or none does (graph.StepGraph agrees the same way)
+                if _agree(ex, 0.0 if err is not None else 1.0, dist.ReduceOp.MIN) < 0.5:
                     st.off = True
-                    print(f"[flexflow_amd] trace capture failed ({e}); running eagerly", flush=True)
+                    why = err if err is not None else "a peer rank's capture failed"
+                    print(f"[flexflow_amd] trace capture failed ({why}); running eagerly", flush=True)
                     torch.cuda.synchronize()
                     run()
                     return
@@ -172,10 +180,20 @@ def end(cfg, trace_id) -> None:
         return
     st.iters += 1
     ms = _stop_timer(st)
+    if ms is not None:
+        # every rank takes the same decision: the world's slowest timing counts
+        import torch.distributed as dist
+
+        from .graph import _agree
+        ms = _agree(st.model.executor, ms, dist.ReduceOp.MAX)
     if st.graph is not None and st.decision == "trial" and ms is not None:
         st.graph_ms.append(ms)
         if len(st.graph_ms) >= 2:
-            if min(st.graph_ms) < 0.98 * min(st.eager_ms):
+            import torch.distributed as dist
+
+            from .graph import _agree
+            keep = float(min(st.graph_ms) < 0.98 * min(st.eager_ms))
+            if _agree(st.model.executor, keep, dist.ReduceOp.MIN) > 0.5:
                 st.decision = True
             else:  # replay is not faster: eager for good (releases the graph's pool)
                 st.graph, st.off = None, True

@@ -158,8 +158,9 @@ def test_graph_trial_policy_matches_eager():
 
 @pytest.mark.parametrize("model", ["candle_uno", "dlrm"])
 def test_begin_end_trace_replays_hipgraph(model):
-    """FFConfig.begin_trace / end_trace (reference: Legion tracing): from the third iteration the
-    recorded forward / zero_gradients / backward sequence replays as one hipGraph; weights after 6
+    """FFConfig.begin_trace / end_trace (reference: Legion tracing): from the fourth iteration the
+    recorded forward / zero_gradients / backward sequence replays as one hipGraph (captured in the
+    fourth iteration, after two timed eager ones); weights after 6
     iterations match an untraced eager run. DLRM under SGD takes the row-sparse embedding update,
     whose host bookkeeping a replay would skip: its trace runs eagerly (same weights)."""
     from flexflow_amd.core import FFConfig, FFModel, SGDOptimizer
