@@ -174,7 +174,8 @@ def test_model_repository_rejects_path_escape(tmp_path):
 
 def test_checkpoint_without_entry_layout_loads_when_arenas_match(tmp_path):
     """Shards written before the per-entry arena layout existed still load when the arena sizes
-    match this job's; otherwise they are rejected."""
+    match this job's and strict=True checked world size and strategy; otherwise
+    they are rejected."""
     from safetensors.torch import load_file, save_file
     ff, _ = _model(opt="adam")
     ff.train_step()
@@ -184,6 +185,8 @@ def test_checkpoint_without_entry_layout_loads_when_arenas_match(tmp_path):
     save_file(load_file(fn), fn)  # drop the metadata: the old format
     w_ref = [np.asarray(w.get_weights(ff)).copy() for L in ff.layers for w in L.weights]
     ff2, _ = _model(opt="adam")
+    with pytest.raises(ValueError):  # equal sizes alone do not prove equal contents
+        ff2.load_checkpoint(str(ck), strict=False)
     assert ff2.load_checkpoint(str(ck)) == 1
     w2 = [np.asarray(w.get_weights(ff2)).copy() for L in ff2.layers for w in L.weights]
     for a, b in zip(w_ref, w2):
