@@ -25,7 +25,7 @@ struct GemmArgs {
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
-  int impl = 2;  // 5: persistent 4-wave, 4-deep BK=32 ring (gemm_w4q.hip, falls back to 4), 4: persistent 4-wave (gemm_w4p.hip, falls back to 3), 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
+  int impl = 2;  // 6: persistent 8-wave ping-pong (gemm_pp.hip, falls back to 4), 5: persistent 4-wave, 4-deep BK=32 ring (gemm_w4q.hip, falls back to 4), 4: persistent 4-wave (gemm_w4p.hip, falls back to 3), 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
   // Backward-activation epilogue (gemm256 only, see gemm_dact_bf16): C = (alpha*A.B) * act'(zin),
   // zin the producer's bf16 pre-activation in C's layout; colpart (optional) receives per-128-row
   // fp32 column sums of that product, [2 * ceil(M / 256)][N], for the producer's bias gradient.
@@ -48,6 +48,9 @@ bool gemm_w4_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
 bool gemm_w4p_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 // the same walk and epilogue with a 4-slot BK = 32 ring (K-tiles requested 3 steps ahead), gemm_w4q.hip
 bool gemm_w4q_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+// persistent 8-wave ping-pong 256x256x64 kernel, two waves per SIMD alternating MFMA and memory
+// phases (gemm_pp.hip); batch 1, no beta / split-K / activation, K % 64 == 0
+bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 int gemm256_bn(int M, int N, int batch, int splitk);
 // fp32 operands and output on the f32-input MFMA (gemm_f32.hip): any shape / layout, batch strides,
 // alpha / beta / bias / activation / pre-activation epilogue (A, B, C, Z reinterpreted as float)

@@ -351,7 +351,7 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // tile count of the kernel that will run
   int64_t tiles;
-  if (impl == 4 || impl == 5 || impl >= 40) return 1;  // persistent: every CU busy whatever the tile count
+  if (impl == 4 || impl == 5 || impl == 6 || impl >= 40) return 1;  // persistent: every CU busy whatever the tile count
   if (impl == 3 && K % 128 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
   } else if (impl == 2 && K % 32 == 0) {
@@ -386,6 +386,7 @@ static bool try_large(const GemmArgs& p, bool a_al, bool b_al, hipStream_t strea
     q.impl = 4;
     return gemm_w4p_bf16(q, p.a_bytes, p.b_bytes, stream);
   }
+  if (p.impl == 6 && gemm_pp_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl == 5 && gemm_w4q_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl >= 4 && gemm_w4p_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl >= 3 && gemm_w4_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;

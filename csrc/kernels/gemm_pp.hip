@@ -1,0 +1,486 @@
+// Persistent 8-wave ping-pong bf16 MFMA GEMM: 256 x 256 x 64 tiles, two waves per SIMD.
+//
+// Why (rounds 3-4, gemm_w4*.hip): with ONE wave per SIMD (4 waves of 128 x 128) every LDS-DMA
+// issue and fragment read of the ring sits in the MFMA wave's own instruction stream; ablations
+// priced the DMA issue at ~14 % of the main loop, which kept those kernels 8-14 % behind
+// hipBLASLt. Here each SIMD holds two waves that own different halves of the tile's rows and
+// alternate roles every ~1000 cycles:
+//   * a COMPUTE phase: 64 back-to-back v_mfma_f32_16x16x32_bf16 on fragments already in registers
+//     (128 x 64 outputs per wave, 128 AGPR accumulators);
+//   * a MEMORY phase: this group's share of the LDS-DMA for the next K-tiles, the 24 fragment
+//     reads for its next compute phase and, at a tile boundary, the previous tile's epilogue.
+// Group 0 (waves 0-3: tile rows 0-127) runs one phase ahead of group 1 (waves 4-7: rows
+// 128-255); wave w and wave w+4 share a SIMD (cyclic dealing), so while one of them computes the
+// other's memory work issues beside it — the MFMA pipe of every SIMD is fed from one wave while
+// the other pays the issue cost. Phase p: group 0 reads / computes stage p/2, group 1 stage
+// (p-1)/2; one s_barrier closes every phase (group 1 executes one extra barrier first).
+//
+// Every DMA offset is in the VGPR operand (the buffer range check does not cover soffset), so rows
+// past the end of a K-contiguous operand read as zeros instead of past the allocation.
+// Two-slot LDS ring (2 x 64 KiB). Stage u = (tile, K-tile) in this workgroup's tile walk; the
+// K-tiles of consecutive tiles follow each other, so the ring never drains between tiles. Who
+// stages what (each piece = one 1-KiB buffer_load ... lds; slot lifetimes in phases):
+//   * A-rows-128..255 of u+1 (16) and the first half of every B quarter of u+1 (16): group 0 in its
+//     memory phase 2u (their slot was last read by group 1 in phase 2u-1);
+//   * A-rows-0..127 of u+2 (16) and the second half of every B quarter (16): group 1 in its memory
+//     phase 2u+1 (A slot last read in 2u; a B quarter is read only by waves j and j+4, so wave j+4
+//     refills it right behind its own reads). Eight pieces per wave per memory phase.
+// Every piece has ~2 phases (~1 us) to land; each issuing wave retires its pieces with a counted
+// vmcnt before the barrier that precedes their first read (never vmcnt(0) in steady state).
+// The MFMAs are inline asm on "+a" accumulators, the first K-step of a tile uses a zero C operand
+// (no accumulator clearing), and all LDS reads are inline asm (hipcc otherwise waits for the
+// LDS-DMA in flight before each read).
+//
+// Epilogue: alpha, bias (fp32 / bf16), bf16 or fp32 output, through a wave-private LDS image into
+// whole-row range-checked buffer stores (see epilogue()). Requires batch 1, beta 0, no activation, K % 64 == 0, 16-B aligned operand
+// rows, operands and output < 2 GiB. Image formats / swizzles as gemm_w4_core.h.
+#include "gemm_w4_core.h"
+
+namespace ffk {
+namespace pp {
+using namespace w4;
+
+constexpr int NTHR = 512;
+constexpr int NFB = 4;     // 16-column B fragments per wave (64 columns)
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// No AGPRs anywhere in this kernel: when a function uses AGPRs, LLVM splits the 256-register budget
+// of two waves per SIMD 128 / 128 between VGPRs and AGPRs, and 128 accumulators + 96 fragment
+// registers + addressing do not fit the halves (hipcc spilled 100-300 registers). In VGPR form the
+// MFMAs read and write the one 256-register pool, and the epilogue needs no AGPR -> VGPR copies.
+template <int OFF>
+__device__ __forceinline__ bf16x8 ds128(unsigned a) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+template <bool ZERO>
+__device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  if constexpr (ZERO) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=v"(acc) : "v"(b), "v"(a));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(b), "v"(a));
+}
+template <int OFF>
+__device__ __forceinline__ v4s dstr(unsigned a) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+__device__ __forceinline__ bf16x8 join(v4s lo, v4s hi) {
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// counted wait with a run-time count (the counts differ at tile boundaries and at the end)
+template <int EPI>
+__device__ __forceinline__ void vmcnt_rt(int n) {
+  switch (n) {
+    case 8: vmcnt<8>(); break;
+    case EPI: vmcnt<EPI>(); break;
+    case EPI + 8: vmcnt<EPI + 8>(); break;
+    default: vmcnt<0>(); break;
+  }
+}
+
+// The lane id, opaque to the optimiser: every lane-dependent address is re-derived from it where it
+// is used (a few VALU per phase) instead of being hoisted into long-lived registers, which this
+// kernel does not have (224 of its 256 VGPRs are accumulators and fragments).
+__device__ __forceinline__ int opaque_lane() {
+  int l = (int)(threadIdx.x & 63);
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+// VMEM ops of one epilogue: 2 bias loads (one wasted for a bf16 bias keeps the count fixed) + 16 row
+// stores (bf16) or 32 (fp32)
+template <bool F32OUT>
+constexpr int epi_ops() { return 2 + (F32OUT ? 32 : 16); }
+
+template <bool A_K, bool B_K, bool F32OUT>
+__global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
+gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
+  constexpr int EPI = epi_ops<F32OUT>();
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wj = wave & 3;  // grp: rows grp*128.. of the tile; wj: columns wj*64..
+  const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
+  const int total = tm * tn;
+  const int nk = p.K / BK;
+  const int first = blockIdx.x;
+  if (first >= total || nk <= 0) return;
+  const int ntiles = (total - 1 - first) / (int)gridDim.x + 1;
+  const int U = ntiles * nk;  // stages of this workgroup
+
+  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)min(a_bytes, (int64_t)0x7fffffff), 0x00020000);
+  __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)min(b_bytes, (int64_t)0x7fffffff), 0x00020000);
+
+  // ---- LDS-DMA: per-lane (tile independent) source offsets; the tile / K-tile part is scalar and
+  // added to them per issue.
+  // VGPRs are scarce (128 AGPR accumulators + 96 fragment registers of the 256): a K-contiguous
+  // operand needs one offset register (piece_lane_off does not depend on the piece there), an
+  // MN-contiguous one two (q enters as an XOR of the 16-B chunk: off(q) = base + (x ^ 16 q)).
+  const int gsA = piece_gstride<A_K>(p.lda), gsB = piece_gstride<true>(p.ldb);
+  const int awl = grp ^ 1;  // A half this wave stages: group 0 stages rows 128.., group 1 rows 0..
+  // per-lane DMA source offset = base + chunk: for an MN-contiguous operand the piece's q = g & 3
+  // enters as an XOR of the chunk part only (bits 4-5 of the base need not be zero)
+  auto voff = [&](bool is_a, int& base, int& chunk) __attribute__((always_inline)) {
+    const int l = opaque_lane();
+    const bool kc = A_K;
+    const int64_t ld = p.lda;
+    const int wl = awl;
+    if (kc) {
+      base = piece_lane_off<true>(ld, 0, 0, wl, 0, l);
+      chunk = 0;
+    } else {
+      base = (int)(((l >> 4) * (int)ld + wl * 128) * 2);
+      chunk = ((l & 15) ^ (((l >> 4) & 3) << 2)) * 16;
+    }
+  };
+  // Each wave stages an increasing sequence of stages (group 0: 0, 1, 2, ...; group 1 the A rows
+  // 0..127 of 0, 1, 2, ...), so the scalar source bases are kept in a cursor that adds one K-step
+  // per stage and re-derives the tile coordinates only when it crosses into the next tile.
+  const int ka = A_K ? BK * 2 : BK * (int)p.lda * 2, kb = B_K ? BK * 2 : BK * (int)p.ldb * 2;
+  int c_kt = 0, c_tl = 0, c_sa = 0, c_sb = 0;
+  auto cursor_tile = [&]() __attribute__((always_inline)) {
+    int tmi, tni;
+    tile_coords(first + c_tl * (int)gridDim.x, tm, tn, tmi, tni);
+    const int m0 = tmi * BM, n0 = tni * BN;
+    c_sa = __builtin_amdgcn_readfirstlane(A_K ? (int)((int64_t)m0 * p.lda * 2) : m0 * 2);
+    c_sb = __builtin_amdgcn_readfirstlane(B_K ? (int)((int64_t)n0 * p.ldb * 2) : n0 * 2);
+  };
+  auto cursor_next = [&]() __attribute__((always_inline)) {
+    if (++c_kt == nk) {
+      c_kt = 0;
+      if (++c_tl < ntiles) cursor_tile();
+    } else {
+      c_sa += ka;
+      c_sb += kb;
+    }
+  };
+  cursor_tile();
+  // A pieces of half `awl`, g = 4 wj + t (4 per wave)
+  auto dma_a = [&](int u) __attribute__((always_inline)) {
+    const int sa = c_sa;
+    char* dst = smem + (u & 1) * STAGE + awl * 16 * 1024;
+    int vb, vc;
+    voff(true, vb, vc);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int g = wj * 4 + t;
+      const int vo = (A_K ? vb : vb + (vc ^ (16 * t))) + (sa + g * gsA);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(dst + g * 1024), 16, vo, 0, 0, 0);
+    }
+  };
+  // B pieces of this wave's 64-column quarter (8 per stage: group 0 issues 0..3 of stage u + 1,
+  // group 1 pieces 4..7 of stage u + 2). Only wave j and wave j + 4 read quarter j, so a group-1
+  // wave may refill it as soon as its own reads of the stage are done. K-contiguous: piece t =
+  // rows 64 j + 8 t .. + 7 (128-B rows). MN-contiguous: the quarter is its own [64 k][64 n] image
+  // (128-B k-rows, 16-B chunk c stored at c ^ s(k), s(k) = (k & 2) | ((k >> 1) & 4)); piece t =
+  // k-rows 8 t .. 8 t + 7.
+  auto dma_b = [&](int u, int t0) __attribute__((always_inline)) {
+    const int sb = c_sb;
+    const int l = opaque_lane();
+    char* dst = smem + (u & 1) * STAGE + A_BYTES + wj * (B_K ? 8 * 1024 : 8192);
+    if constexpr (B_K) {
+      const int vb = piece_lane_off<true>(p.ldb, 0, 0, 0, 0, l) + sb + wj * 64 * (int)p.ldb * 2;
+#pragma unroll
+      for (int t = t0; t < t0 + 4; ++t)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(dst + t * 1024), 16, vb + t * gsB, 0, 0, 0);
+    } else {
+      const int vb = (l >> 3) * (int)p.ldb * 2 + sb + wj * 128;
+      const int x = ((l & 7) ^ ((l >> 3) & 2)) * 16;
+#pragma unroll
+      for (int t = t0; t < t0 + 4; ++t)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(dst + t * 1024), 16,
+                                                 vb + (x ^ (64 * (t & 1))) + t * 8 * (int)p.ldb * 2, 0, 0, 0);
+    }
+  };
+
+  // ---- fragment reads: per-lane LDS addresses, derived per phase (slot 1 adds STAGE)
+  const unsigned sbase = (unsigned)(uintptr_t)smem;
+  // K-contiguous images: 128-B rows, chunk ^ (row & 7); fragment i of a 16-row block at +2048 i,
+  // and the kk = 1 chunk is the kk = 0 one with bit 2 flipped (address ^ 64).
+  // MN-contiguous images (128-wide halves of 256-B k-rows, chunk ^ swz_mn(krow)), read by
+  // ds_read_b64_tr_b16: lane (g, q, pp) reads k-row 8g + q (+4 for the second read) at chunk
+  // (rr >> 3) + (pp >> 1); with rr = 16 i (+ 64 for odd B waves) the XOR'd chunk is
+  // (2 i [+ 8]) ^ (swz ^ (pp >> 1)), so a read costs one v_xor + v_add off per-lane constants
+  bf16x8 af[2][8], bfr[2][NFB];
+  auto read_frags = [&](int slot) __attribute__((always_inline)) {
+    const unsigned so = slot ? (unsigned)STAGE : 0u;
+    const int lane = opaque_lane();
+    const int l16 = lane & 15, lg = lane >> 4;
+    const unsigned aK = sbase + (grp * 128 + l16) * 128 + ((lg ^ (lane & 7)) << 4);
+    const unsigned bK = sbase + A_BYTES + (wj * 64 + l16) * 128 + ((lg ^ (lane & 7)) << 4);
+    const int q4 = l16 >> 2, pp = l16 & 3;
+    const int kr = 8 * lg + q4;
+    const unsigned aM = sbase + grp * (BK * 256) + kr * 256 + 8 * (pp & 1);
+    const unsigned T0 = (unsigned)((swz_mn(kr) ^ (pp >> 1)) << 4);
+    const unsigned T1 = (unsigned)((swz_mn(kr + 4) ^ (pp >> 1)) << 4);
+    // B quarter image (see dma_b): k-row kr at kr * 128, chunk 2 jj + (pp >> 1) stored at
+    // ^ s(kr), s(kr) = (q4 & 2) | ((lg & 1) << 2) for kr = 8 lg + q4 (also for kr + 4, kr + 32):
+    // address = bQ + ((32 jj) ^ TQ), the k + 4 and kk = 1 reads at +512 / +4096
+    const unsigned bQ = sbase + A_BYTES + wj * 8192 + kr * 128 + 16 * (pp >> 1) + 8 * (pp & 1);
+    const unsigned TQ = (unsigned)(((q4 & 2) | ((lg & 1) << 2)) << 4);
+    if constexpr (B_K) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const unsigned a = (bK + so) ^ (kk * 64);
+        bfr[kk][0] = ds128<0>(a);
+        bfr[kk][1] = ds128<2048>(a);
+        bfr[kk][2] = ds128<4096>(a);
+        bfr[kk][3] = ds128<6144>(a);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < NFB; ++jj) {
+        const unsigned a0 = bQ + so + ((32u * jj) ^ TQ);
+        bfr[0][jj] = join(dstr<0>(a0), dstr<512>(a0));
+        bfr[1][jj] = join(dstr<4096>(a0), dstr<4096 + 512>(a0));
+      }
+    }
+    if constexpr (A_K) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const unsigned a = (aK + so) ^ (kk * 64);
+        af[kk][0] = ds128<0>(a);
+        af[kk][1] = ds128<2048>(a);
+        af[kk][2] = ds128<4096>(a);
+        af[kk][3] = ds128<6144>(a);
+        af[kk][4] = ds128<8192>(a);
+        af[kk][5] = ds128<10240>(a);
+        af[kk][6] = ds128<12288>(a);
+        af[kk][7] = ds128<14336>(a);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const unsigned c = 32 * i;
+        const unsigned a0 = aM + so + (c ^ T0), a1 = aM + so + (c ^ T1);
+        af[0][i] = join(dstr<0>(a0), dstr<1024>(a1));
+        af[1][i] = join(dstr<8192>(a0), dstr<8192 + 1024>(a1));
+      }
+    }
+  };
+
+  f32x4 acc[8][NFB];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NFB; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](auto zero_c) __attribute__((always_inline)) {
+    constexpr bool Z = decltype(zero_c)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NFB; ++jj) mfma<Z>(acc[i][jj], bfr[0][jj], af[0][i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NFB; ++jj) mfma<false>(acc[i][jj], bfr[1][jj], af[1][i]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- epilogue
+  typedef typename std::conditional<F32OUT, float, bf16_t>::type OutT;
+  const int64_t c_bytes = (int64_t)p.M * p.ldc * (int64_t)sizeof(OutT);
+  __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, (int)min(c_bytes, (int64_t)0x7fffffff), 0x00020000);
+  const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
+  __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
+  const float alpha = p.alpha;
+  // Epilogue through a wave-private fp32 staging image (16 rows x 64 columns, 4 KiB, outside the
+  // ring): the accumulator layout puts 4 consecutive columns of one row in a lane, so direct 8-B
+  // stores leave a wave as 16 scattered 32-B row pieces per instruction, store-issue bound at
+  // ~7 B/clk/CU (MI355X_MICROARCH.md, epilogue store tail). Here each 16-row block is written to
+  // the image (16-B chunk c of row r at c ^ r: conflict-free), read back as 8 consecutive columns
+  // per lane and stored as whole 128-B (bf16) / 256-B (fp32) row segments, with bias and alpha.
+  // A wave's LDS operations execute in order, so the read-back needs no wait behind the writes.
+  auto epilogue = [&](int tl) __attribute__((always_inline)) {
+    int tmi, tni;
+    tile_coords(first + tl * (int)gridDim.x, tm, tn, tmi, tni);
+    const int lane = opaque_lane();
+    const int cc = lane & 7;
+    const unsigned st = sbase + 2 * STAGE + wj * 4096;
+    const int m0 = tmi * BM + grp * 128;
+    const int n = tni * BN + wj * 64 + 8 * cc;  // this lane's 8 read-back columns
+    const bool nin = n < p.N;
+    float bb[8];
+    if (p.bias_bf16) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bb[2 * e] = __uint_as_float(v[e] << 16);
+        bb[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+      }
+    } else {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 : -16, 0, 0);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 + 16 : -16, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bb[e] = __uint_as_float(v0[e]);
+        bb[4 + e] = __uint_as_float(v1[e]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      // addresses re-derived per pass (kept across the 8 passes they cost registers the
+      // allocator does not have next to the 128 accumulators)
+      const int ln = opaque_lane();
+      const int w16 = ln & 15, wg = ln >> 4, rc8 = ln & 7, rr8 = ln >> 3;
+#pragma unroll
+      for (int jj = 0; jj < NFB; ++jj) {
+        const unsigned a = st + w16 * 256 + (((4 * jj + wg) ^ w16) << 4);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(acc[i][jj]) : "memory");
+      }
+      f32x4 lo[2], hi[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = rr8 + 8 * h;
+        const unsigned a0 = st + rr * 256 + (((2 * rc8) ^ rr) << 4);
+        const unsigned a1 = st + rr * 256 + (((2 * rc8 + 1) ^ rr) << 4);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(lo[h]), "=&v"(hi[h]) : "v"(a0), "v"(a1) : "memory");
+      }
+      lgkm0();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = m0 + 16 * i + rr8 + 8 * h;
+        const bool in = m < p.M && nin;
+        const int off = in ? (int)(((int64_t)m * p.ldc + n) * (int64_t)sizeof(OutT)) : -16;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = __builtin_fmaf(lo[h][e], alpha, bb[e]);
+          x[4 + e] = __builtin_fmaf(hi[h][e], alpha, bb[4 + e]);
+        }
+        if constexpr (F32OUT) {
+          const u32x4 o0 = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+          const u32x4 o1 = {__float_as_uint(x[4]), __float_as_uint(x[5]), __float_as_uint(x[6]), __float_as_uint(x[7])};
+          __builtin_amdgcn_raw_buffer_store_b128(o0, rc, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(o1, rc, in ? off + 16 : off, 0, 0);
+        } else {
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (uint32_t)f2bf(x[2 * e]) | ((uint32_t)f2bf(x[2 * e + 1]) << 16);
+          __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: stage 0 (all of it) and A rows 0..127 of stage 1 land before the first phase
+  if (grp == 0) {
+    dma_b(0, 0);
+    dma_a(0);
+    cursor_next();
+  } else {
+    dma_a(0);
+    dma_b(0, 4);
+    cursor_next();
+    if (U > 1) {
+      dma_a(1);
+      dma_b(1, 4);
+      cursor_next();
+    }
+  }
+  vmcnt<0>();
+  barrier();
+  if (grp == 1) barrier();  // group 1 runs one phase behind
+
+  // memory phase of stage u (epi: the previous tile's epilogue first)
+  auto mem_phase = [&](int u, bool epi, int tl_prev) __attribute__((always_inline)) {
+    if (epi) epilogue(tl_prev);
+    int after;  // VMEM ops issued after the piece this wave retires at the end of the phase
+    if (grp == 0) {
+      const bool iss = u + 1 < U;
+      if (iss) {
+        dma_b(u + 1, 0);  // first: the compute phase's vmcnt(4) retires these and leaves the A rows
+        dma_a(u + 1);
+        cursor_next();
+      }
+      after = (epi ? EPI : 0) + (iss ? 8 : 0);  // retires A rows 128.. of stage u
+    } else {
+      const bool iss = u + 2 < U;
+      if (iss) dma_a(u + 2);
+      after = (epi ? EPI : 0) + (iss ? 8 : 0);  // retires A rows 0..127 / B 4..7 of stage u + 1
+    }
+    read_frags(u & 1);
+    lgkm0();
+    if (grp == 1 && u + 2 < U) {
+      // this wave's B quarter of slot u & 1 is free only now: its partner (wave j) read it in the
+      // previous phase, and this wave's own reads just completed
+      dma_b(u + 2, 4);
+      cursor_next();
+    }
+    vmcnt_rt<EPI>(after);
+    barrier();
+  };
+  auto compute_phase = [&](int u, auto zero_c) __attribute__((always_inline)) {
+    compute(zero_c);
+    if (grp == 0 && u + 1 < U) vmcnt<4>();  // B of stage u + 1 (its A rows 128.. may still fly)
+    barrier();
+  };
+
+  int u = 0;
+  mem_phase(0, false, 0);
+  for (int tl = 0; tl < ntiles; ++tl) {
+    compute_phase(u, std::true_type());
+    for (int kt = 1; kt < nk; ++kt) {
+      mem_phase(u + 1, false, 0);
+      ++u;
+      compute_phase(u, std::false_type());
+    }
+    ++u;
+    // MFMA -> accumulator read distance before the epilogue (inline asm: hipcc pads nothing)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3");
+    if (tl + 1 < ntiles) {
+      mem_phase(u, true, tl);
+    } else {
+      epilogue(tl);
+      if (grp == 0) barrier();  // balance the barrier count of the two groups
+    }
+  }
+}
+
+template <bool F32OUT>
+static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+}
+
+}  // namespace pp
+
+static int g_pp_cus = 0;
+
+bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+  using namespace pp;
+  if (p.dact || p.Z || p.act != ACT_NONE || p.beta != 0.f || p.batch != 1 || (p.splitk > 1 && p.ws) || p.K % BK != 0 ||
+      p.K <= 0 || a_bytes > 0x7fffffffLL || b_bytes > 0x7fffffffLL || a_bytes <= 0 || b_bytes <= 0)
+    return false;
+  if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15) || p.lda % 8 || p.ldb % 8) return false;
+  if ((int64_t)p.M * p.ldc * (p.out_f32 ? 4 : 2) > 0x7fffff00LL) return false;  // buffer-store offsets
+  if (!p.a_kcontig && p.M % 8) return false;
+  if (!p.b_kcontig && p.N % 8) return false;
+  if (!p.a_kcontig && !p.b_kcontig) return false;  // both transposed: 96 fragment VGPRs do not fit
+  if (p.N % 8 || p.ldc % 8 || ((uintptr_t)p.C & 15)) return false;  // whole 8-column row stores
+  if (p.bias && ((uintptr_t)p.bias & 15)) return false;
+  if (g_pp_cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_pp_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_pp_cus <= 0) g_pp_cus = 256;
+  }
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  dim3 grid(std::min(tiles, g_pp_cus));
+  if (p.out_f32) launch<true>(p, grid, stream, a_bytes, b_bytes);
+  else launch<false>(p, grid, stream, a_bytes, b_bytes);
+  return true;
+}
+
+}  // namespace ffk

@@ -72,7 +72,7 @@ import os as _os
 
 _TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
 # our kernels: 256-row ping-pong (csrc/kernels/gemm256.hip), 256x128 LDS-DMA (gemm_big.hip), 128x128
-IMPLS = {"w4q": 5, "w4p": 4, "w4": 3, "k256": 2, "big": 1, "128": 0}
+IMPLS = {"pp": 6, "w4q": 5, "w4p": 4, "w4": 3, "k256": 2, "big": 1, "128": 0}
 IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []

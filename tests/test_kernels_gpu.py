@@ -28,7 +28,7 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
                                    (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
-@pytest.mark.parametrize("impl", [5, 4, 3, 2, 1, 0])
+@pytest.mark.parametrize("impl", [6, 5, 4, 3, 2, 1, 0])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -63,7 +63,7 @@ def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
     assert _rel(C32, ref + 1.0) < 1e-3
 
 
-@pytest.mark.parametrize("impl", [4, 5])
+@pytest.mark.parametrize("impl", [4, 5, 6])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (8200, 2056, 512), (16384, 1024, 256), (3000, 1000, 1152),
                                    (2048, 768, 128)])
@@ -98,7 +98,7 @@ def test_gemm_persistent(ffC, a_k, b_k, M, N, K, out, bias, impl):
         assert torch.equal(C, first)
 
 
-@pytest.mark.parametrize("impl", [3, 4, 5])
+@pytest.mark.parametrize("impl", [3, 4, 5, 6])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(512, 512, 512, 1), (512, 512, 512, 2), (1024, 768, 1024, 1)])
 def test_gemm_repeat_bitwise(ffC, impl, a_k, b_k, M, N, K, splitk):
