@@ -76,7 +76,7 @@ void gemm(Tensor A, Tensor B, Tensor C, optional<Tensor> bias, optional<Tensor> 
 
 // C = (A.B) * act'(zin) [+ dbias += colsum] in one 256-row MFMA GEMM; false if the shape does not fit
 bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias, int64_t M, int64_t N, int64_t K,
-               int64_t lda, int64_t ldb, int64_t ldc, bool a_k, bool b_k, int64_t act) {
+               int64_t lda, int64_t ldb, int64_t ldc, bool a_k, bool b_k, int64_t act, int64_t impl) {
   check_dev(A, "A"); check_dev(B, "B"); check_dev(C, "C"); check_dev(zin, "zin");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
               C.scalar_type() == at::kBFloat16 && zin.scalar_type() == at::kBFloat16, "gemm_dact: bf16 operands");
@@ -101,7 +101,15 @@ bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias,
     part = at::empty({rows * N}, C.options().dtype(at::kFloat));
     p.colpart = part.data_ptr<float>();
   }
-  if (!ffk::gemm_dact_bf16(p, cur_stream())) return false;
+  bool ok = false;
+  if (impl == 6) {  // persistent ping-pong kernel: act must be ACT_GRADMUL (zin holds the stored act')
+    ffk::GemmArgs q = p;
+    q.dact = true;
+    ok = ffk::gemm_pp_bf16(q, q.a_bytes, q.b_bytes, cur_stream());
+  } else {
+    ok = ffk::gemm_dact_bf16(p, cur_stream());
+  }
+  if (!ok) return false;
   if (has_db) ffk::col_reduce_add(p.colpart, dbias->data_ptr<float>(), (int)rows, (int)N, cur_stream());
   return true;
 }

@@ -108,7 +108,10 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // Activation codes (match flexflow_amd.type.ActiMode numeric values).
-enum Act : int { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13, ACT_GELU = 14 };
+// ACT_GRADMUL (kernel-internal): the 'pre-activation' operand already holds act'(z), stored by the
+// producer's forward (bias_act_fwd with ACT_STORE_GRAD), so the backward multiplies by it.
+enum Act : int { ACT_NONE = 10, ACT_RELU = 11, ACT_SIGMOID = 12, ACT_TANH = 13, ACT_GELU = 14, ACT_GRADMUL = 15 };
+constexpr int ACT_STORE_GRAD = 0x100;  // bias_act_fwd flag: write act'(z) to zout instead of z
 
 // erf with |error| < 1.5e-7 (Abramowitz & Stegun 7.1.26): one v_rcp, one v_exp and five FMAs
 // instead of libm erff's branchy polynomial — the GELU epilogues evaluate it per output element.
@@ -139,12 +142,14 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
     default: return x;
   }
 }
+// y = act(x) and g = act'(x) together (GELU: one erf / exp for both)
 // derivative wrt pre-activation x
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
     case ACT_SIGMOID: { float s = fast_rcp(1.f + __expf(-x)); return s * (1.f - s); }
     case ACT_TANH: { float t = tanhf(x); return 1.f - t * t; }
+    case ACT_GRADMUL: return x;
     case ACT_GELU: {
       // Phi(x) + x phi(x); erf(x / sqrt 2) and phi share one exp(-x^2 / 2)
       const float au = fabsf(x) * 0.70710678118654752f;
@@ -156,6 +161,20 @@ __device__ __forceinline__ float act_grad(int act, float x) {
     }
     default: return 1.f;
   }
+}
+__device__ __forceinline__ void act_fwd_grad(int act, float x, float& y, float& g) {
+  if (act == ACT_GELU) {
+    const float au = fabsf(x) * 0.70710678118654752f;
+    const float t = fast_rcp(__builtin_fmaf(0.3275911f, au, 1.f));
+    const float e = __expf(-au * au);
+    const float erf_abs = 1.f - erf_poly_t(t) * e;
+    const float cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
+    y = x * cdf;
+    g = __builtin_fmaf(x * 0.3989422804014327f, e, cdf);
+    return;
+  }
+  y = act_fwd(act, x);
+  g = act_grad(act, x);
 }
 
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 "XCD swizzle

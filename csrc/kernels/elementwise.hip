@@ -505,8 +505,14 @@ int bias_act_bwd_chunks(int rows, int cols) {
 
 // Epilogue pass for library GEMMs: zb = z + bias[col] (stored back if zout), y = act(zb).
 // bf16, cols % 8 == 0: one 16-B vector per thread-step. In place (y == z) is allowed.
+// Epilogue pass for library GEMMs: zb = z + bias[col] (stored back if zout), y = act(zb). With
+// ACT_STORE_GRAD in act, zout receives act'(zb) instead (the consumer's dgrad epilogue then only
+// multiplies by it; zout may alias z). bf16, cols % 8 == 0: one 16-B vector per thread-step. In
+// place (y == z) is allowed.
 __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __restrict__ bias, int bias_bf16,
                                     bf16_t* zout, bf16_t* y, int64_t rows, int cols, int act) {
+  const bool sg = (act & ACT_STORE_GRAD) != 0 && zout != nullptr;
+  act &= 0xff;
   const int64_t nv = rows * (int64_t)cols / 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -517,10 +523,21 @@ __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __
       float x0[8], x1[8];
       load16(z + v * 8, x0);
       load16(z + (v + stride) * 8, x1);
+      if (sg) {
+        float g0[8], g1[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        x0[j] = act_fwd(act, x0[j]);
-        x1[j] = act_fwd(act, x1[j]);
+        for (int j = 0; j < 8; ++j) {
+          act_fwd_grad(act, x0[j], x0[j], g0[j]);
+          act_fwd_grad(act, x1[j], x1[j], g1[j]);
+        }
+        store16(zout + v * 8, g0);
+        store16(zout + (v + stride) * 8, g1);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          x0[j] = act_fwd(act, x0[j]);
+          x1[j] = act_fwd(act, x1[j]);
+        }
       }
       store16(y + v * 8, x0);
       store16(y + (v + stride) * 8, x1);
@@ -543,10 +560,17 @@ __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __
         x[0] += b0.x; x[1] += b0.y; x[2] += b0.z; x[3] += b0.w;
         x[4] += b1.x; x[5] += b1.y; x[6] += b1.z; x[7] += b1.w;
       }
-      if (zout) store16(zout + e, x);
+      if (zout && !sg) store16(zout + e, x);
     }
+    if (sg) {
+      float g[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = act_fwd(act, x[j]);
+      for (int j = 0; j < 8; ++j) act_fwd_grad(act, x[j], x[j], g[j]);
+      store16(zout + e, g);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = act_fwd(act, x[j]);
+    }
     store16(y + e, x);
   }
 }

@@ -351,7 +351,7 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // tile count of the kernel that will run
   int64_t tiles;
-  if (impl == 4 || impl == 5 || impl == 6 || impl >= 40) return 1;  // persistent: every CU busy whatever the tile count
+  if (impl == 4 || impl == 5 || impl == 6 || impl >= 40) return 1;  // persistent kernels and their ablations  // persistent: every CU busy whatever the tile count
   if (impl == 3 && K % 128 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
   } else if (impl == 2 && K % 32 == 0) {
@@ -374,6 +374,12 @@ int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
 
 static bool try_large(const GemmArgs& p, bool a_al, bool b_al, hipStream_t stream) {
   if (!(a_al && b_al && p.a_bytes > 0)) return false;
+  if (p.impl >= 60 && p.impl < 70) {  // ablation of gemm_pp (timing only): 61 no loop DMA
+    GemmArgs q = p;
+    q.ablate = p.impl - 60;
+    q.impl = 6;
+    return gemm_pp_bf16(q, p.a_bytes, p.b_bytes, stream);
+  }
   if (p.impl >= 50) {  // ablations of gemm_w4q (timing only): 51 no stores, 53 + no loop DMA, 57 + no barrier
     GemmArgs q = p;
     q.ablate = p.impl - 50;

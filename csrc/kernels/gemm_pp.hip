@@ -93,15 +93,16 @@ __device__ __forceinline__ int opaque_lane() {
 }
 
 // VMEM ops of one epilogue: 2 bias loads (one wasted for a bf16 bias keeps the count fixed) + 16 row
-// stores (bf16) or 32 (fp32)
-template <bool F32OUT>
-constexpr int epi_ops() { return 2 + (F32OUT ? 32 : 16); }
+// stores (bf16) or 32 (fp32); DACT (no bias) has 16 loads of the stored act' and 2 column-sum
+// stores instead of the bias loads
+template <bool F32OUT, bool DACT>
+constexpr int epi_ops() { return (F32OUT ? 32 : 16) + (DACT ? 18 : 2); }
 
-template <bool A_K, bool B_K, bool F32OUT>
+template <bool A_K, bool B_K, bool F32OUT, bool DACT>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
-  constexpr int EPI = epi_ops<F32OUT>();
+  constexpr int EPI = epi_ops<F32OUT, DACT>();
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -292,6 +293,11 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
   __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
   const float alpha = p.alpha;
+  __amdgpu_buffer_rsrc_t rzin = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT ? p.zin : p.A), (short)0,
+                                                                  DACT ? (int)min(c_bytes, (int64_t)0x7fffffff) : 0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rcol = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT && p.colpart ? (void*)p.colpart : (void*)p.A), (short)0,
+                                                                  DACT && p.colpart ? (int)min((int64_t)2 * tm * p.N * 4, (int64_t)0x7fffffff) : 0,
+                                                                  0x00020000);
   // Epilogue through a wave-private fp32 staging image (16 rows x 64 columns, 4 KiB, outside the
   // ring): the accumulator layout puts 4 consecutive columns of one row in a lane, so direct 8-B
   // stores leave a wave as 16 scattered 32-B row pieces per instruction, store-issue bound at
@@ -308,23 +314,42 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
     const int m0 = tmi * BM + grp * 128;
     const int n = tni * BN + wj * 64 + 8 * cc;  // this lane's 8 read-back columns
     const bool nin = n < p.N;
-    float bb[8];
-    if (p.bias_bf16) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
+    float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (!DACT) {
+      if (p.bias_bf16) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bb[2 * e] = __uint_as_float(v[e] << 16);
-        bb[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
-      }
-    } else {
-      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 : -16, 0, 0);
-      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 + 16 : -16, 0, 0);
+        for (int e = 0; e < 4; ++e) {
+          bb[2 * e] = __uint_as_float(v[e] << 16);
+          bb[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+        }
+      } else {
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 : -16, 0, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 + 16 : -16, 0, 0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bb[e] = __uint_as_float(v0[e]);
-        bb[4 + e] = __uint_as_float(v1[e]);
+        for (int e = 0; e < 4; ++e) {
+          bb[e] = __uint_as_float(v0[e]);
+          bb[4 + e] = __uint_as_float(v1[e]);
+        }
       }
     }
+    // DACT: the producer's stored act'(z), one pass ahead of its use: a pass's loads are issued
+    // before the previous pass's stores, so the wait hipcc puts in front of their use never covers
+    // the most recent stores (all up front would hold 64 more VGPRs)
+    u32x4 gz[DACT ? 16 : 1];
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int i) __attribute__((always_inline)) {
+      if constexpr (DACT) {
+        const int rr8 = opaque_lane() >> 3;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int m = m0 + 16 * i + rr8 + 8 * h;
+          const bool in = m < p.M && nin;
+          gz[2 * i + h] = __builtin_amdgcn_raw_buffer_load_b128(rzin, in ? (int)(((int64_t)m * p.ldc + n) * 2) : -16, 0, 0);
+        }
+      }
+    };
+    gload(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_barrier(0);
@@ -337,6 +362,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
         const unsigned a = st + w16 * 256 + (((4 * jj + wg) ^ w16) << 4);
         asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(acc[i][jj]) : "memory");
       }
+      if (i + 1 < 8) gload(i + 1);
       f32x4 lo[2], hi[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -358,6 +384,18 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           x[e] = __builtin_fmaf(lo[h][e], alpha, bb[e]);
           x[4 + e] = __builtin_fmaf(hi[h][e], alpha, bb[4 + e]);
         }
+        if constexpr (DACT) {
+          // consumer dgrad (rounded to bf16 first, as the unfused GEMM + pass pair does) times the
+          // producer's act'(z); the column sums feed the producer's bias gradient
+          const u32x4 gv = gz[2 * i + h];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            x[2 * e] = bf2f(f2bf(x[2 * e])) * __uint_as_float(gv[e] << 16);
+            x[2 * e + 1] = bf2f(f2bf(x[2 * e + 1])) * __uint_as_float(gv[e] & 0xffff0000u);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += x[e];
+        }
         if constexpr (F32OUT) {
           const u32x4 o0 = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
           const u32x4 o1 = {__float_as_uint(x[4]), __float_as_uint(x[5]), __float_as_uint(x[6]), __float_as_uint(x[7])};
@@ -370,6 +408,21 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
         }
       }
+    }
+    if constexpr (DACT) {
+      // fold the 8 lanes that share this lane's 8 columns (lane bits 3-5), then lanes 0-7 store
+      // the wave's 128-row partial into row 2 tile_m + grp of the [2 tm][N] slab (every lane
+      // issues the two stores: the other lanes' go out of range, so the VMEM count stays fixed)
+#pragma unroll
+      for (int sh = 8; sh < 64; sh <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], sh);
+      const bool wr = lane < 8 && nin;
+      const int off = wr ? (int)(((int64_t)(2 * tmi + grp) * p.N + n) * 4) : -16;
+      const u32x4 o0 = {__float_as_uint(cs[0]), __float_as_uint(cs[1]), __float_as_uint(cs[2]), __float_as_uint(cs[3])};
+      const u32x4 o1 = {__float_as_uint(cs[4]), __float_as_uint(cs[5]), __float_as_uint(cs[6]), __float_as_uint(cs[7])};
+      __builtin_amdgcn_raw_buffer_store_b128(o0, rcol, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(o1, rcol, wr ? off + 16 : off, 0, 0);
     }
   };
 
@@ -397,7 +450,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
     if (epi) epilogue(tl_prev);
     int after;  // VMEM ops issued after the piece this wave retires at the end of the phase
     if (grp == 0) {
-      const bool iss = u + 1 < U;
+      const bool iss = u + 1 < U && !(p.ablate & 1);
       if (iss) {
         dma_b(u + 1, 0);  // first: the compute phase's vmcnt(4) retires these and leaves the A rows
         dma_a(u + 1);
@@ -405,13 +458,13 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
       }
       after = (epi ? EPI : 0) + (iss ? 8 : 0);  // retires A rows 128.. of stage u
     } else {
-      const bool iss = u + 2 < U;
+      const bool iss = u + 2 < U && !(p.ablate & 1);
       if (iss) dma_a(u + 2);
       after = (epi ? EPI : 0) + (iss ? 8 : 0);  // retires A rows 0..127 / B 4..7 of stage u + 1
     }
     read_frags(u & 1);
     lgkm0();
-    if (grp == 1 && u + 2 < U) {
+    if (grp == 1 && u + 2 < U && !(p.ablate & 1)) {
       // this wave's B quarter of slot u & 1 is free only now: its partner (wave j) read it in the
       // previous phase, and this wave's own reads just completed
       dma_b(u + 2, 4);
@@ -422,7 +475,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   };
   auto compute_phase = [&](int u, auto zero_c) __attribute__((always_inline)) {
     compute(zero_c);
-    if (grp == 0 && u + 1 < U) vmcnt<4>();  // B of stage u + 1 (its A rows 128.. may still fly)
+    if (grp == 0 && u + 1 < U && !(p.ablate & 1)) vmcnt<4>();  // B of stage u + 1 (its A rows 128.. may still fly)
     barrier();
   };
 
@@ -447,11 +500,11 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   }
 }
 
-template <bool F32OUT>
+template <bool F32OUT, bool DACT>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
-  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
 }  // namespace pp
@@ -460,7 +513,14 @@ static int g_pp_cus = 0;
 
 bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
   using namespace pp;
-  if (p.dact || p.Z || p.act != ACT_NONE || p.beta != 0.f || p.batch != 1 || (p.splitk > 1 && p.ws) || p.K % BK != 0 ||
+  if (p.dact) {
+    // dgrad with the producer's stored act'(z) (act ACT_GRADMUL): bf16 C, no bias / beta / Z
+    if (p.act != ACT_GRADMUL || !p.zin || p.out_f32 || p.bias || p.Z || p.beta != 0.f) return false;
+    if (((uintptr_t)p.zin & 15) || (p.colpart && ((uintptr_t)p.colpart & 15))) return false;
+  } else if (p.Z || p.act != ACT_NONE) {
+    return false;
+  }
+  if (p.beta != 0.f || p.batch != 1 || (p.splitk > 1 && p.ws) || p.K % BK != 0 ||
       p.K <= 0 || a_bytes > 0x7fffffffLL || b_bytes > 0x7fffffffLL || a_bytes <= 0 || b_bytes <= 0)
     return false;
   if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15) || p.lda % 8 || p.ldb % 8) return false;
@@ -478,8 +538,9 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   dim3 grid(std::min(tiles, g_pp_cus));
-  if (p.out_f32) launch<true>(p, grid, stream, a_bytes, b_bytes);
-  else launch<false>(p, grid, stream, a_bytes, b_bytes);
+  if (p.dact) launch<false, true>(p, grid, stream, a_bytes, b_bytes);
+  else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
+  else launch<false, false>(p, grid, stream, a_bytes, b_bytes);
   return true;
 }
 

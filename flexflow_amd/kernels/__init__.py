@@ -38,6 +38,10 @@ def native(t: torch.Tensor) -> bool:
 
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_GELU = 10, 11, 12, 13, 14
+# kernel-internal: the 'pre-activation' operand holds act'(z) already (stored by the producer's
+# forward, linear_fwd(store_grad=True)); the backward multiplies by it
+ACT_GRADMUL = 15
+ACT_STORE_GRAD = 0x100  # bias_act_fwd flag: write act'(z) into zout instead of z
 
 
 def act_ref(x, act):
@@ -53,6 +57,8 @@ def act_ref(x, act):
 
 
 def act_grad_ref(z, act):
+    if act == ACT_GRADMUL:
+        return z
     if act == ACT_RELU:
         return (z > 0).to(z.dtype)
     if act == ACT_SIGMOID:
@@ -572,8 +578,8 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
         return C
     X = ext()
 
-    def fused(out=C, dbo=db):
-        return X.gemm_dact(A, B, out, Zp, dbo, M, N, K, lda, ldb, ldc, a_k, b_k, act)
+    def fused(out=C, dbo=db, impl=2):
+        return X.gemm_dact(A, B, out, Zp, dbo, M, N, K, lda, ldb, ldc, a_k, b_k, act, impl)
 
     def unfused(out=C, dbo=db):
         gemm(A, B, out, M, N, K, a_k, b_k, lda, ldb, ldc)
@@ -592,11 +598,18 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
         else:
             scratch = torch.empty_like(C)
             dbs = torch.zeros_like(db) if db is not None else None
-            if not fused(scratch, dbs):
+            cands = {}
+            if fused(scratch, dbs):
+                cands["fused"] = lambda: fused(scratch, dbs)
+            # the persistent ping-pong kernel multiplies by a stored act' (ACT_GRADMUL) in its epilogue
+            if act == ACT_GRADMUL and fused(scratch, dbs, 6):
+                cands["pp"] = lambda: fused(scratch, dbs, 6)
+            if not cands:
                 choice = "unfused"
             else:
                 unfused(scratch, dbs)  # tune the plain GEMM's call site outside the timing
-                times = _time_all({"fused": lambda: fused(scratch, dbs), "unfused": lambda: unfused(scratch, dbs)})
+                cands["unfused"] = lambda: unfused(scratch, dbs)
+                times = _time_all(cands)
                 choice = min(times, key=lambda k: times[k])
                 TUNE_LOG.append({"op": "gemm_dact", "M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "act": act,
                                  "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
@@ -604,24 +617,36 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
         _tuned[key] = choice
     if choice == "fused" and fused():
         return C
+    if choice == "pp" and fused(impl=6):
+        return C
     unfused()
     return C
 
 
-def linear_fwd(x2d, w, bias, act, save_z):
-    """y = act(x.w^T + b) for x2d [M,K], w [N,K]. Returns (y, z_or_None)."""
+def linear_fwd(x2d, w, bias, act, save_z, store_grad=False):
+    """y = act(x.w^T + b) for x2d [M,K], w [N,K]. Returns (y, z_or_None). store_grad: the second
+    value is act'(z) instead of z (the backward then uses ACT_GRADMUL): the consumer's dgrad GEMM
+    multiplies by it in its epilogue instead of evaluating act' per element."""
     M, K = x2d.shape
     N = w.shape[0]
     y = torch.empty(M, N, device=x2d.device, dtype=x2d.dtype)
     z = torch.empty_like(y) if (save_z and act != ACT_NONE) else None
+    if store_grad and z is not None and native(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == x2d.dtype \
+            and N % 8 == 0:
+        # library GEMM (+ bias) into z, then one pass: y = act(z), z <- act'(z) in place
+        _lib_gemm(x2d, w, z, M, N, K, True, True, K, K, N, 1.0, 0.0, bias, 1, 0, 0, 0)
+        ext().bias_act_fwd(z, None, z, y, M, N, act | ACT_STORE_GRAD)
+        return y, z
     if native(x2d) and x2d.dtype in (torch.bfloat16, torch.float32) and w.dtype == x2d.dtype:
         gemm(x2d, w, y, M, N, K, True, True, K, K, N, bias=bias, Z=z, act=act)
+        if store_grad and z is not None:
+            z.copy_(act_grad_ref(z.float(), act).to(z.dtype))
         return y, z
     r = x2d.float() @ w.float().t()
     if bias is not None:
         r = r + bias.float()
     if z is not None:
-        z.copy_(r)
+        z.copy_(act_grad_ref(r, act) if store_grad else r)
     y.copy_(act_ref(r, act))
     return y, z
 

@@ -13,6 +13,7 @@ Reference: src/ops/linear.cc, src/ops/kernels/linear_kernels.cu.
 from __future__ import annotations
 
 import math
+import os
 
 from .. import kernels as K
 from ..type import ActiMode, DataType, OperatorType
@@ -74,10 +75,15 @@ class Linear(OpImpl):
             b = None
         Kl = x.shape[-1]
         x2 = x.reshape(-1, Kl)
-        y, z = K.linear_fwd(x2, w, b, self.act, save_z=ctx.training)
+        # when the consumer's dgrad GEMM applies this op's act' (Executor._plan_dact_fusion), the
+        # forward stores act'(z) instead of z: the fused epilogue then multiplies by it
+        sg = bool(ctx.training and ctx.extra.get("dact_fused") and self.act != K.ACT_NONE
+                  and os.environ.get("FF_DACT_STORE_GRAD", "1") == "1")
+        y, z = K.linear_fwd(x2, w, b, self.act, save_z=ctx.training, store_grad=sg)
         if ctx.training:
             ctx.saved["x"] = x2
             ctx.saved["z"] = z
+            ctx.saved["z_is_grad"] = sg
             ctx.saved["w"] = w
             ctx.saved["has_b"] = b is not None
         return [y.reshape(tuple(x.shape[:-1]) + (w.shape[0],))]
@@ -104,6 +110,8 @@ class Linear(OpImpl):
             pdb = None
             if len(pctx.wgrads) > 1 and pctx.saved.get("has_b") and not pctx.extra.get("bias_grad_fused"):
                 pdb = pctx.wgrads[1]
+            if pctx.saved.get("z_is_grad"):
+                pact = K.ACT_GRADMUL
             dact = (pctx.saved["z"].reshape(-1, x2.shape[1]), pact, pdb)
         ready = ctx.extra.get("dx_ready")
         out_shape = tuple(dy.shape[:-1]) + (x2.shape[1],)
