@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="default 32 for BERT (HBM-sized: 288 GB/GPU), 64 for the other models")
     ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--pad-vocab", type=int, default=64,
+                    help="BERT: pad the MLM decoder width to a multiple of this with masked logits (0: off)")
     ap.add_argument("--search", default="unity", help="unity | mcmc | dp")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
@@ -78,6 +80,9 @@ def build(args, search):
         bc = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "bert-tiny": BertConfig.tiny}[args.model](args.seq)
         bc.seq = args.seq
         bc.max_pos = max(bc.max_pos, args.seq)
+        # MLM decoder width padded to a multiple of 64 (30522 -> 30528) with masked (-1e9 bias)
+        # columns: identical loss / gradients, every vocab GEMM on aligned tiles
+        bc.pad_vocab_multiple = args.pad_vocab
         ids, pos, out = build_bert(ff, gb, bc)
         ff.optimizer = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)
         ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
@@ -85,7 +90,8 @@ def build(args, search):
         pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (gb, 1)))
         ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (gb, bc.seq, 1), dtype=np.int32))
         info = {"seq": bc.seq, "flops_per_sample": bc.train_flops_per_seq(), "params": bc.params(),
-                "extra": {"hidden": bc.hidden, "layers": bc.layers, "heads": bc.heads, "vocab": bc.vocab}}
+                "extra": {"hidden": bc.hidden, "layers": bc.layers, "heads": bc.heads, "vocab": bc.vocab,
+                          "vocab_padded": bc.padded_vocab()}}
         return ff, gb, info
     inputs, out, loss, mets, make_batch = build_model(args.model, ff, gb)
     ff.optimizer = AdamOptimizer(ff, 1e-4) if args.optimizer == "adam" else SGDOptimizer(ff, 1e-3)

@@ -38,11 +38,12 @@ class Initializer:
 
 
 class GlorotUniformInitializer(Initializer):
-    def __init__(self, seed=0):
-        self.seed = seed
+    def __init__(self, seed=0, fans=None):
+        self.seed = seed  # None: the model-local default seed of the weight (Executor.init_weights)
+        self.fans = fans  # (fan_in, fan_out) override, e.g. a padded weight's logical shape
 
     def fill_full(self, t, shape):
-        fin, fout = _fans(shape)
+        fin, fout = self.fans if self.fans is not None else _fans(shape)
         sc = math.sqrt(6.0 / (fin + fout))
         K.init_uniform(t, -sc, sc, self.seed)
 
@@ -50,6 +51,23 @@ class GlorotUniformInitializer(Initializer):
 class ZeroInitializer(Initializer):
     def fill_full(self, t, shape):
         K.fill(t, 0.0)
+
+
+class MaskedTailInitializer(Initializer):
+    """Zeros for the first `valid` entries of a 1-D weight and `fill` after them: the bias of an
+    output projection padded past its logical width (BERT's MLM decoder, vocab 30522 padded to a
+    multiple of 64 so that every GEMM of the vocab projection runs on aligned tiles). A large
+    negative fill makes the padded logits vanish under the softmax (probability 0, gradient 0),
+    so the loss, accuracy and every real gradient equal the unpadded model's."""
+
+    def __init__(self, valid, fill=-1e9):
+        self.valid = int(valid)
+        self.fill = float(fill)
+
+    def fill_full(self, t, shape):
+        K.fill(t, 0.0)
+        if t.numel() > self.valid:
+            t.view(-1)[self.valid:].fill_(self.fill)
 
 
 class ConstantInitializer(Initializer):

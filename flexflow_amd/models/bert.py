@@ -20,6 +20,9 @@ class BertConfig:
     layers: int = 24
     ffn: int = 4096
     vocab: int = 30522
+    # pad the MLM decoder's output width to a multiple of this (0: no padding); the padded logits
+    # carry a -1e9 bias (MaskedTailInitializer), so the model computes exactly the unpadded loss
+    pad_vocab_multiple: int = 0
     max_pos: int = 512
     seq: int = 512
     dropout: float = 0.0
@@ -36,6 +39,10 @@ class BertConfig:
     @staticmethod
     def tiny(seq=64):
         return BertConfig(hidden=128, heads=2, layers=2, ffn=256, vocab=1000, max_pos=seq, seq=seq)
+
+    def padded_vocab(self) -> int:
+        m = int(self.pad_vocab_multiple or 0)
+        return (self.vocab + m - 1) // m * m if m > 1 else self.vocab
 
     def params(self) -> int:
         h, f = self.hidden, self.ffn
@@ -74,7 +81,14 @@ def build_bert(ff, batch: int, cfg: BertConfig):
     if cfg.mlm_head:
         t = ff.dense(x, H, ActiMode.AC_MODE_GELU, name="mlm_transform")
         t = ff.layer_norm(t, [-1], name="mlm_ln")
-        t = ff.dense(t, cfg.vocab, name="mlm_decoder")
+        vp = cfg.padded_vocab()
+        if vp > cfg.vocab:
+            from ..core.initializers import GlorotUniformInitializer, MaskedTailInitializer
+            # the real rows are initialised as in the unpadded model (same values, same fans)
+            t = ff.dense(t, vp, kernel_initializer=GlorotUniformInitializer(seed=None, fans=(H, cfg.vocab)),
+                         bias_initializer=MaskedTailInitializer(cfg.vocab), name="mlm_decoder")
+        else:
+            t = ff.dense(t, cfg.vocab, name="mlm_decoder")
     else:
         t = ff.dense(x, 2, name="cls")
     out = ff.softmax(t, name="mlm_softmax")

@@ -301,8 +301,12 @@ class Executor:
             # independent of how many models were built before. Graph rewrites stamp the slot of
             # the graph as written (w._init_slot) so that rewritten graphs initialise identically.
             slot = getattr(w, "_init_slot", None) or (li, i)
-            init = w.initializer or default_initializer(getattr(w, "short_name", w.name),
-                                                        seed_base + 1009 * slot[0] + slot[1])
+            seed = seed_base + 1009 * slot[0] + slot[1]
+            init = w.initializer or default_initializer(getattr(w, "short_name", w.name), seed)
+            if getattr(init, "seed", 0) is None:  # an explicit initializer asking for the model-local seed
+                import copy
+                init = copy.copy(init)
+                init.seed = seed
             if isinstance(init, BlockInitializer):
                 init.resolve = resolve
             return init

@@ -331,7 +331,7 @@ def test_flash_attention_strided_qkv(ffC):
     assert _rel(o.permute(0, 2, 1, 3), ref) < 2e-2
 
 
-@pytest.mark.parametrize("cols,rows", [(1024, 300), (768, 300), (100, 300), (1024, 8200)])
+@pytest.mark.parametrize("cols,rows", [(1024, 300), (768, 300), (100, 300), (1024, 8200), (1024, 16384)])
 def test_layernorm(ffC, cols, rows):
     torch.manual_seed(5)
     x = torch.randn(rows, cols, device=DEV).bfloat16()
@@ -364,6 +364,25 @@ def test_layernorm(ffC, cols, rows):
     assert torch.equal(dx2, dx)
     assert _rel(dsum - 0.5, dx.float().sum(0)) < 5e-3  # kernel sums the fp32 values before bf16 rounding
     assert _rel(db, 2 * bf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("cols", [1024, 4096, 30528, 1000])
+def test_col_fold_two_level_deterministic(ffC, cols):
+    """The bias-gradient column fold of a BERT-Large-sized gradient (16384 rows: 512 slab rows,
+    two-level deterministic fold with a last-arriving-block finish) against fp32 torch, and
+    bitwise equal over repeated calls (no float atomics, fixed summation order)."""
+    torch.manual_seed(8)
+    rows = 16384
+    dy = torch.randn(rows, cols, device=DEV).bfloat16()
+    ref = dy.float().sum(0)
+    outs = []
+    for _ in range(4):
+        db = torch.full((cols,), 0.25, device=DEV)
+        ffC.bias_act_bwd(dy, None, None, db, rows, cols, 10)
+        outs.append(db.clone())
+    assert _rel(outs[0] - 0.25, ref) < 1e-4
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 def test_softmax_and_xent(ffC):

@@ -232,3 +232,41 @@ def test_sparse_plan_follows_momentum_change():
     assert ff.executor._sparse_plan(ff.optimizer)
     ff.optimizer.momentum = 0.9
     assert not ff.executor._sparse_plan(ff.optimizer)
+
+
+def test_bert_padded_vocab_matches_unpadded():
+    """BertConfig.pad_vocab_multiple: the MLM decoder is padded (1000 -> 1024 columns) with a
+    -1e9 bias on the padded logits and the real rows initialised as in the unpadded model, so the
+    losses of three Adam steps equal the unpadded model's (bench.py pads 30522 -> 30528)."""
+    import numpy as np
+
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(pad):
+        cfg = FFConfig(["--dtype", "fp32"])
+        cfg.batch_size = 2
+        ff = FFModel(cfg)
+        bc = BertConfig(hidden=64, heads=2, layers=1, ffn=128, vocab=1000, max_pos=32, seq=32)
+        bc.pad_vocab_multiple = pad
+        ids, pos, out = build_bert(ff, 2, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        rng = np.random.default_rng(0)
+        ids.set_tensor(ff, rng.integers(0, 1000, (2, 32), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(32, dtype=np.int32), (2, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, 1000, (2, 32, 1), dtype=np.int32))
+        losses = []
+        for _ in range(3):
+            ff.reset_metrics()
+            ff.forward()
+            ff.zero_gradients()
+            ff.backward()
+            ff.update()
+            losses.append(ff.get_perf_metrics().get_loss())
+        return losses, out
+
+    ref, _ = run(0)
+    pad, out = run(64)
+    assert out.dims[-1] == 1024
+    np.testing.assert_allclose(pad, ref, rtol=1e-5)
