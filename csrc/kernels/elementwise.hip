@@ -431,104 +431,6 @@ __global__ void __launch_bounds__(1024) col_reduce_det_kernel(const float* __res
   }
 }
 
-// Two-level deterministic fold: grid (C / 32 column chunks, outputs, S row splits). Each block
-// sums its R / S rows of 32 columns (32 row lanes x 8 loads in flight) into a second-level partial
-// [S][32] of its column chunk, then the block that arrives last at the chunk's counter adds the S
-// partials in split order (deterministic) into out. One launch of 8-16x the blocks of the
-// single-level kernel above, which left 160 of 256 CUs idle on the LayerNorm folds (C = 1024:
-// 96 blocks reading 12 MB, ~15 us per fold, 1.5 ms of the BERT-Large step). Hand-off per
-// MI355X_MICROARCH.md (inter-workgroup visibility): plain partial stores, every wave's
-// vmcnt(0), barrier, one agent release fence before the counter add; the last arriver acquires
-// once before reading. The counter is reset by the last arriver (zeroed once at allocation).
-__global__ void __launch_bounds__(1024) col_reduce_det2_kernel(const float* __restrict__ part, Outs3 o, int R, int C,
-                                                                float* __restrict__ l2, unsigned* __restrict__ cnt) {
-  constexpr int CW = 32, RL = 32, U = 8;
-  __shared__ float red[RL][CW + 1];
-  __shared__ unsigned last;
-  const int k = o.which[blockIdx.y];
-  const int S = gridDim.z, sp = blockIdx.z;
-  const float* p = part + (int64_t)k * R * C;
-  float* out = o.p[k];
-  const int c = blockIdx.x * CW + (threadIdx.x % CW);
-  const int rl = threadIdx.x / CW;
-  const int rpb = (R + S - 1) / S;
-  const int r0 = sp * rpb, r1 = min(R, r0 + rpb);
-  float acc[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) acc[u] = 0.f;
-  if (c < C) {
-    int r = r0 + rl;
-    for (; r + (U - 1) * RL < r1; r += U * RL) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(r + u * RL) * C + c];
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] += v[u];
-    }
-    for (; r < r1; r += RL) acc[0] += p[(int64_t)r * C + c];
-  }
-  float t0 = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u) t0 += acc[u];
-  red[rl][threadIdx.x % CW] = t0;
-  __syncthreads();
-  // this chunk's second-level partials: l2[(y * gx + x) * S + sp][32]
-  float* lp = l2 + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * S) * CW;
-  if (rl == 0) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < RL; ++i) t += red[i][threadIdx.x];
-    lp[sp * CW + threadIdx.x] = t;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned* ct = cnt + blockIdx.y * gridDim.x + blockIdx.x;
-    const unsigned prev = __hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(S - 1);
-    if (last) {
-      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (last && rl == 0 && c < C) {
-    float t = 0.f;
-    for (int i = 0; i < S; ++i) t += lp[i * CW + threadIdx.x];
-    out[c] += t;
-  }
-}
-
-// second-level partials + counters of the two-level fold, one pool per device; a launch takes the
-// next of FOLD_SLOTS slices so folds on different streams (overlapped update) never share counters
-constexpr int FOLD_SLOTS = 16;
-struct FoldPool { float* l2 = nullptr; unsigned* cnt = nullptr; int64_t l2n = 0, cn = 0; unsigned next = 0; };
-static FoldPool g_fold[16];
-static bool fold_pool(int64_t l2n, int64_t cn, float*& l2, unsigned*& cnt, hipStream_t st) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return false;
-  FoldPool& fp = g_fold[dev];
-  if (fp.l2n < l2n || fp.cn < cn) {
-    // grown on the host thread that launches; a capture in progress cannot allocate: single-level
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-    if (fp.l2) { (void)hipDeviceSynchronize(); (void)hipFree(fp.l2); (void)hipFree(fp.cnt); }
-    fp.l2n = std::max<int64_t>(l2n, 1 << 16);
-    fp.cn = std::max<int64_t>(cn, 1 << 12);
-    if (hipMalloc(&fp.l2, fp.l2n * FOLD_SLOTS * sizeof(float)) != hipSuccess) { fp.l2 = nullptr; fp.l2n = fp.cn = 0; return false; }
-    if (hipMalloc(&fp.cnt, fp.cn * FOLD_SLOTS * sizeof(unsigned)) != hipSuccess) { (void)hipFree(fp.l2); fp.l2 = nullptr; fp.l2n = fp.cn = 0; return false; }
-    (void)hipMemset(fp.cnt, 0, fp.cn * FOLD_SLOTS * sizeof(unsigned));
-    (void)hipDeviceSynchronize();
-  }
-  const unsigned slot = fp.next++ % FOLD_SLOTS;
-  l2 = fp.l2 + (int64_t)slot * fp.l2n;
-  cnt = fp.cnt + (int64_t)slot * fp.cn;
-  return true;
-}
-
 // row chunks per column block (atomic adders per output address); 0 = the deterministic kernel
 // above (default); FF_COLRED_GY / col_reduce_set_gy
 static int g_cr_gy = -1;
@@ -549,16 +451,7 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
     if (o.p[k]) o.which[nz++] = k;
   if (!nz) return;
   if (col_reduce_gy() == 0) {
-    const int gx = (C + 31) / 32;
-    // row splits: ~1024 blocks where the rows allow, >= 128 rows (4 load rounds) per split
-    const int S = std::max(1, std::min(std::min(16, (1024 + gx * nz - 1) / (gx * nz)), R / 128));
-    float* l2 = nullptr;
-    unsigned* cnt = nullptr;
-    if (S > 1 && fold_pool((int64_t)gx * nz * S * 32, (int64_t)gx * nz, l2, cnt, st)) {
-      hipLaunchKernelGGL(col_reduce_det2_kernel, dim3(gx, nz, S), dim3(1024), 0, st, part, o, R, C, l2, cnt);
-      return;
-    }
-    hipLaunchKernelGGL(col_reduce_det_kernel, dim3(gx, nz), dim3(1024), 0, st, part, o, R, C);
+    hipLaunchKernelGGL(col_reduce_det_kernel, dim3((C + 31) / 32, nz), dim3(1024), 0, st, part, o, R, C);
     return;
   }
   const int gy = std::max(1, std::min(col_reduce_gy(), R / 8));
