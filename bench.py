@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="default 32 for BERT (HBM-sized: 288 GB/GPU), 64 for the other models")
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--pad-vocab", type=int, default=64,
+    ap.add_argument("--pad-vocab", type=int, default=int(os.environ.get("FF_PAD_VOCAB", "64")),
                     help="BERT: pad the MLM decoder width to a multiple of this with masked logits (0: off)")
     ap.add_argument("--search", default="unity", help="unity | mcmc | dp")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])

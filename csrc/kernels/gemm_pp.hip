@@ -108,12 +108,23 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wj = wave & 3;  // grp: rows grp*128.. of the tile; wj: columns wj*64..
   const int tm = (p.M + BM - 1) / BM, tn = (p.N + BN - 1) / BN;
-  const int total = tm * tn;
-  const int nk = p.K / BK;
+  // work units: output tiles x split-K slices (unit = tile * S + slice; slices write fp32 slabs
+  // ws[slice][M][N] that slab_sum folds; S = 1: the tile's output straight into C)
+  // slice s of a tile covers K-tiles [s nkt / S, (s + 1) nkt / S) (any S <= nkt: S is chosen so
+  // that the units fill the CUs, e.g. 48 tiles x 5 slices)
+  const int S = (p.splitk > 1 && p.ws) ? p.splitk : 1;
+  const int total = tm * tn * S;
+  const int nkt = p.K / BK;
   const int first = blockIdx.x;
-  if (first >= total || nk <= 0) return;
+  if (first >= total || nkt < S) return;
   const int ntiles = (total - 1 - first) / (int)gridDim.x + 1;
-  const int U = ntiles * nk;  // stages of this workgroup
+  auto unit_nk = [&](int unit) __attribute__((always_inline)) {
+    if (S == 1) return nkt;
+    const int sl = unit % S;
+    return (sl + 1) * nkt / S - sl * nkt / S;
+  };
+  int U = 0;  // stages of this workgroup
+  for (int tl = 0; tl < ntiles; ++tl) U += unit_nk(first + tl * (int)gridDim.x);
 
   __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)min(a_bytes, (int64_t)0x7fffffff), 0x00020000);
   __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)min(b_bytes, (int64_t)0x7fffffff), 0x00020000);
@@ -140,20 +151,26 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
       chunk = ((l & 15) ^ (((l >> 4) & 3) << 2)) * 16;
     }
   };
+  auto unit_coords = [&](int unit, int& tmi, int& tni, int& sl) __attribute__((always_inline)) {
+    const int t = S > 1 ? unit / S : unit;
+    sl = S > 1 ? unit - t * S : 0;
+    tile_coords(t, tm, tn, tmi, tni);
+  };
   // Each wave stages an increasing sequence of stages (group 0: 0, 1, 2, ...; group 1 the A rows
   // 0..127 of 0, 1, 2, ...), so the scalar source bases are kept in a cursor that adds one K-step
   // per stage and re-derives the tile coordinates only when it crosses into the next tile.
   const int ka = A_K ? BK * 2 : BK * (int)p.lda * 2, kb = B_K ? BK * 2 : BK * (int)p.ldb * 2;
-  int c_kt = 0, c_tl = 0, c_sa = 0, c_sb = 0;
+  int c_kt = 0, c_tl = 0, c_sa = 0, c_sb = 0, c_nk = 0;
   auto cursor_tile = [&]() __attribute__((always_inline)) {
-    int tmi, tni;
-    tile_coords(first + c_tl * (int)gridDim.x, tm, tn, tmi, tni);
-    const int m0 = tmi * BM, n0 = tni * BN;
-    c_sa = __builtin_amdgcn_readfirstlane(A_K ? (int)((int64_t)m0 * p.lda * 2) : m0 * 2);
-    c_sb = __builtin_amdgcn_readfirstlane(B_K ? (int)((int64_t)n0 * p.ldb * 2) : n0 * 2);
+    int tmi, tni, sl;
+    unit_coords(first + c_tl * (int)gridDim.x, tmi, tni, sl);
+    const int m0 = tmi * BM, n0 = tni * BN, k0 = (sl * nkt / S) * BK;
+    c_nk = unit_nk(first + c_tl * (int)gridDim.x);
+    c_sa = __builtin_amdgcn_readfirstlane(A_K ? (int)(((int64_t)m0 * p.lda + k0) * 2) : (int)(((int64_t)k0 * p.lda + m0) * 2));
+    c_sb = __builtin_amdgcn_readfirstlane(B_K ? (int)(((int64_t)n0 * p.ldb + k0) * 2) : (int)(((int64_t)k0 * p.ldb + n0) * 2));
   };
   auto cursor_next = [&]() __attribute__((always_inline)) {
-    if (++c_kt == nk) {
+    if (++c_kt == c_nk) {
       c_kt = 0;
       if (++c_tl < ntiles) cursor_tile();
     } else {
@@ -290,6 +307,10 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   typedef typename std::conditional<F32OUT, float, bf16_t>::type OutT;
   const int64_t c_bytes = (int64_t)p.M * p.ldc * (int64_t)sizeof(OutT);
   __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, (int)min(c_bytes, (int64_t)0x7fffffff), 0x00020000);
+  // split-K: one range-checked descriptor over all slabs ([S][M][N] fp32, ldc = N)
+  const int64_t ws_bytes = (int64_t)S * p.M * p.N * 4;
+  if (S > 1) rc = __builtin_amdgcn_make_buffer_rsrc(p.ws, (short)0, (int)min(ws_bytes, (int64_t)0x7fffffff), 0x00020000);
+  const int64_t ldo = S > 1 ? p.N : p.ldc;
   const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
   __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
   const float alpha = p.alpha;
@@ -306,8 +327,8 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   // per lane and stored as whole 128-B (bf16) / 256-B (fp32) row segments, with bias and alpha.
   // A wave's LDS operations execute in order, so the read-back needs no wait behind the writes.
   auto epilogue = [&](int tl) __attribute__((always_inline)) {
-    int tmi, tni;
-    tile_coords(first + tl * (int)gridDim.x, tm, tn, tmi, tni);
+    int tmi, tni, sl;
+    unit_coords(first + tl * (int)gridDim.x, tmi, tni, sl);
     const int lane = opaque_lane();
     const int cc = lane & 7;
     const unsigned st = sbase + 2 * STAGE + wj * 4096;
@@ -377,7 +398,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
       for (int h = 0; h < 2; ++h) {
         const int m = m0 + 16 * i + rr8 + 8 * h;
         const bool in = m < p.M && nin;
-        const int off = in ? (int)(((int64_t)m * p.ldc + n) * (int64_t)sizeof(OutT)) : -16;
+        const int off = in ? (int)(((int64_t)sl * p.M * p.N + (int64_t)m * ldo + n) * (int64_t)sizeof(OutT)) : -16;
         float x[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -483,6 +504,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   mem_phase(0, false, 0);
   for (int tl = 0; tl < ntiles; ++tl) {
     compute_phase(u, std::true_type());
+    const int nk = unit_nk(first + tl * (int)gridDim.x);
     for (int kt = 1; kt < nk; ++kt) {
       mem_phase(u + 1, false, 0);
       ++u;
@@ -504,7 +526,8 @@ template <bool F32OUT, bool DACT>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
   if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
   else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if constexpr (!DACT) hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
 }  // namespace pp
@@ -520,14 +543,17 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   } else if (p.Z || p.act != ACT_NONE) {
     return false;
   }
-  if (p.beta != 0.f || p.batch != 1 || (p.splitk > 1 && p.ws) || p.K % BK != 0 ||
+  const bool split = p.splitk > 1 && p.ws;
+  if (split && (p.dact || !p.out_f32 || p.bias || p.alpha != 1.f || p.K / BK < p.splitk ||
+                (int64_t)p.splitk * p.M * p.N * 4 > 0x7fffff00LL))
+    return false;
+  if ((p.beta != 0.f && !split) || p.batch != 1 || p.K % BK != 0 ||
       p.K <= 0 || a_bytes > 0x7fffffffLL || b_bytes > 0x7fffffffLL || a_bytes <= 0 || b_bytes <= 0)
     return false;
   if (((uintptr_t)p.A & 15) || ((uintptr_t)p.B & 15) || p.lda % 8 || p.ldb % 8) return false;
   if ((int64_t)p.M * p.ldc * (p.out_f32 ? 4 : 2) > 0x7fffff00LL) return false;  // buffer-store offsets
   if (!p.a_kcontig && p.M % 8) return false;
   if (!p.b_kcontig && p.N % 8) return false;
-  if (!p.a_kcontig && !p.b_kcontig) return false;  // both transposed: 96 fragment VGPRs do not fit
   if (p.N % 8 || p.ldc % 8 || ((uintptr_t)p.C & 15)) return false;  // whole 8-column row stores
   if (p.bias && ((uintptr_t)p.bias & 15)) return false;
   if (g_pp_cus == 0) {
@@ -536,8 +562,9 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
     hipDeviceGetAttribute(&g_pp_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (g_pp_cus <= 0) g_pp_cus = 256;
   }
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * (split ? p.splitk : 1);
   dim3 grid(std::min(tiles, g_pp_cus));
+  if (p.dact && !p.a_kcontig && !p.b_kcontig) return false;
   if (p.dact) launch<false, true>(p, grid, stream, a_bytes, b_bytes);
   else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
   else launch<false, false>(p, grid, stream, a_bytes, b_bytes);

@@ -480,10 +480,15 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                 scratch = torch.zeros_like(C)
                 cands = {k: (lambda i=i: ours(i, scratch)) for k, i in IMPLS.items()}
                 if C.dtype == torch.float32 and batch == 1 and K >= 8192 and splitk is None:
-                    # weight gradients: the 4-wave kernel's split-K factor is tuned like the library's
+                    # weight gradients: the split-K factor of the 4-wave and the ping-pong kernels is
+                    # tuned like the library's (fp32 slabs folded by slab_sum)
                     for S in (2, 4, 8, 16):
                         if K % (S * 128) == 0:
                             cands[f"w4_sk{S}"] = (lambda S=S: ours(IMPLS["w4"], scratch, S))
+                    # the ping-pong kernel takes uneven K slices: S that fill the CUs (48 tiles x 5)
+                    for S in (2, 3, 4, 5, 6, 8, 16):
+                        if K % 64 == 0 and K // 64 >= S:
+                            cands[f"pp_sk{S}"] = (lambda S=S: ours(IMPLS["pp"], scratch, S))
                 if plain:
                     cands["lib"] = lambda: _lib_gemm(A, B, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta,
                                                      bias, batch, sA, sB, sC)
@@ -519,6 +524,8 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
         elif isinstance(choice, str) and choice.startswith("w4_sk"):
             ours(IMPLS["w4"], sk=int(choice[5:]))
+        elif isinstance(choice, str) and choice.startswith("pp_sk"):
+            ours(IMPLS["pp"], sk=int(choice[5:]))
         elif isinstance(choice, str) and choice.startswith("lib_sk"):
             _lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, beta, int(choice[6:]))
         elif choice == "lib":

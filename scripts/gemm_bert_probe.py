@@ -45,8 +45,14 @@ def runner(impl, A, B, C, M, N, K, a_k, b_k):
     ldb = K if b_k else N
     if impl == "lib":
         return lambda: Kn._lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, N, 1.0, 0.0, None, 1, 0, 0, 0)
-    i = IMP[impl]
-    sk = X.gemm_pick_splitk(M, N, K, 1, i)
+    if impl.startswith("lib_sk"):
+        return lambda: Kn._lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, 0.0, int(impl[6:]))
+    if "_sk" in impl:  # e.g. pp_sk4, w4_sk8: that kernel with a fixed split-K factor
+        i = IMP[impl.split("_sk")[0]]
+        sk = int(impl.split("_sk")[1])
+    else:
+        i = IMP[impl]
+        sk = X.gemm_pick_splitk(M, N, K, 1, i)
     ws = torch.empty(M * N * sk, device=dev) if sk > 1 else None
     return lambda: X.gemm(A, B, C, None, None, M, N, K, lda, ldb, N, 0, 0, 0, 1, a_k, b_k, 1.0, 0.0, 10, sk, ws, i)
 

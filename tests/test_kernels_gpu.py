@@ -43,8 +43,8 @@ def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
 
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 4096, 1), (8192, 3072, 1024, 2), (1024, 4096, 8192, 4),
-                                          (1000, 600, 1056, 1), (2048, 2048, 2048, 3)])
-@pytest.mark.parametrize("impl", [5, 4, 3, 2])
+                                          (1000, 600, 1056, 1), (2048, 2048, 2048, 3), (3072, 1024, 16384, 5)])
+@pytest.mark.parametrize("impl", [6, 5, 4, 3, 2])
 def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
     """256-row kernels (3: 4-wave 256x256x64, 128x128 per wave; 2: 8-wave ping-pong): BERT-Large shapes,
     split-K slabs, edge tiles."""
