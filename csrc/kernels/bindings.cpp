@@ -101,15 +101,8 @@ bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias,
     part = at::empty({rows * N}, C.options().dtype(at::kFloat));
     p.colpart = part.data_ptr<float>();
   }
-  bool ok = false;
-  if (impl == 6) {  // persistent ping-pong kernel: act must be ACT_GRADMUL (zin holds the stored act')
-    ffk::GemmArgs q = p;
-    q.dact = true;
-    ok = ffk::gemm_pp_bf16(q, q.a_bytes, q.b_bytes, cur_stream());
-  } else {
-    ok = ffk::gemm_dact_bf16(p, cur_stream());
-  }
-  if (!ok) return false;
+  (void)impl;  // one fused-dgrad kernel (gemm_dact.hip); the argument stays for call-site stability
+  if (!ffk::gemm_dact_bf16(p, cur_stream())) return false;
   if (has_db) ffk::col_reduce_add(p.colpart, dbias->data_ptr<float>(), (int)rows, (int)N, cur_stream());
   return true;
 }

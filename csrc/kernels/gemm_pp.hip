@@ -93,16 +93,20 @@ __device__ __forceinline__ int opaque_lane() {
 }
 
 // VMEM ops of one epilogue: 2 bias loads (one wasted for a bf16 bias keeps the count fixed) + 16 row
-// stores (bf16) or 32 (fp32); DACT (no bias) has 16 loads of the stored act' and 2 column-sum
-// stores instead of the bias loads
-template <bool F32OUT, bool DACT>
-constexpr int epi_ops() { return (F32OUT ? 32 : 16) + (DACT ? 18 : 2); }
+// stores (bf16) or 32 (fp32).
+// (A fused-dgrad variant — the producer's stored act'(z) multiplied in here, bias-gradient column
+// sums beside it — was tried in round 5 and removed: its 16 extra loads and column sums spilled
+// ~150 VGPRs into scratch, the spill traffic forced vmcnt(0) into every memory phase, and it was
+// numerically wrong in the last row pass; gemm_dact's impl-2 kernel and the library GEMM + pass
+// pair cover that op.)
+template <bool F32OUT>
+constexpr int epi_ops() { return (F32OUT ? 32 : 16) + 2; }
 
-template <bool A_K, bool B_K, bool F32OUT, bool DACT>
+template <bool A_K, bool B_K, bool F32OUT>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
-  constexpr int EPI = epi_ops<F32OUT, DACT>();
+  constexpr int EPI = epi_ops<F32OUT>();
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -314,11 +318,6 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
   __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
   const float alpha = p.alpha;
-  __amdgpu_buffer_rsrc_t rzin = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT ? p.zin : p.A), (short)0,
-                                                                  DACT ? (int)min(c_bytes, (int64_t)0x7fffffff) : 0, 0x00020000);
-  __amdgpu_buffer_rsrc_t rcol = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT && p.colpart ? (void*)p.colpart : (void*)p.A), (short)0,
-                                                                  DACT && p.colpart ? (int)min((int64_t)2 * tm * p.N * 4, (int64_t)0x7fffffff) : 0,
-                                                                  0x00020000);
   // Epilogue through a wave-private fp32 staging image (16 rows x 64 columns, 4 KiB, outside the
   // ring): the accumulator layout puts 4 consecutive columns of one row in a lane, so direct 8-B
   // stores leave a wave as 16 scattered 32-B row pieces per instruction, store-issue bound at
@@ -336,41 +335,22 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
     const int n = tni * BN + wj * 64 + 8 * cc;  // this lane's 8 read-back columns
     const bool nin = n < p.N;
     float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (!DACT) {
-      if (p.bias_bf16) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
+    if (p.bias_bf16) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bb[2 * e] = __uint_as_float(v[e] << 16);
-          bb[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
-        }
-      } else {
-        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 : -16, 0, 0);
-        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 + 16 : -16, 0, 0);
+      for (int e = 0; e < 4; ++e) {
+        bb[2 * e] = __uint_as_float(v[e] << 16);
+        bb[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+      }
+    } else {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 : -16, 0, 0);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 4 + 16 : -16, 0, 0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bb[e] = __uint_as_float(v0[e]);
-          bb[4 + e] = __uint_as_float(v1[e]);
-        }
+      for (int e = 0; e < 4; ++e) {
+        bb[e] = __uint_as_float(v0[e]);
+        bb[4 + e] = __uint_as_float(v1[e]);
       }
     }
-    // DACT: the producer's stored act'(z), one pass ahead of its use: a pass's loads are issued
-    // before the previous pass's stores, so the wait hipcc puts in front of their use never covers
-    // the most recent stores (all up front would hold 64 more VGPRs)
-    u32x4 gz[DACT ? 16 : 1];
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto gload = [&](int i) __attribute__((always_inline)) {
-      if constexpr (DACT) {
-        const int rr8 = opaque_lane() >> 3;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int m = m0 + 16 * i + rr8 + 8 * h;
-          const bool in = m < p.M && nin;
-          gz[2 * i + h] = __builtin_amdgcn_raw_buffer_load_b128(rzin, in ? (int)(((int64_t)m * p.ldc + n) * 2) : -16, 0, 0);
-        }
-      }
-    };
-    gload(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_barrier(0);
@@ -383,7 +363,6 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
         const unsigned a = st + w16 * 256 + (((4 * jj + wg) ^ w16) << 4);
         asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(acc[i][jj]) : "memory");
       }
-      if (i + 1 < 8) gload(i + 1);
       f32x4 lo[2], hi[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -405,18 +384,6 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           x[e] = __builtin_fmaf(lo[h][e], alpha, bb[e]);
           x[4 + e] = __builtin_fmaf(hi[h][e], alpha, bb[4 + e]);
         }
-        if constexpr (DACT) {
-          // consumer dgrad (rounded to bf16 first, as the unfused GEMM + pass pair does) times the
-          // producer's act'(z); the column sums feed the producer's bias gradient
-          const u32x4 gv = gz[2 * i + h];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x[2 * e] = bf2f(f2bf(x[2 * e])) * __uint_as_float(gv[e] << 16);
-            x[2 * e + 1] = bf2f(f2bf(x[2 * e + 1])) * __uint_as_float(gv[e] & 0xffff0000u);
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cs[e] += x[e];
-        }
         if constexpr (F32OUT) {
           const u32x4 o0 = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
           const u32x4 o1 = {__float_as_uint(x[4]), __float_as_uint(x[5]), __float_as_uint(x[6]), __float_as_uint(x[7])};
@@ -429,21 +396,6 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
         }
       }
-    }
-    if constexpr (DACT) {
-      // fold the 8 lanes that share this lane's 8 columns (lane bits 3-5), then lanes 0-7 store
-      // the wave's 128-row partial into row 2 tile_m + grp of the [2 tm][N] slab (every lane
-      // issues the two stores: the other lanes' go out of range, so the VMEM count stays fixed)
-#pragma unroll
-      for (int sh = 8; sh < 64; sh <<= 1)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], sh);
-      const bool wr = lane < 8 && nin;
-      const int off = wr ? (int)(((int64_t)(2 * tmi + grp) * p.N + n) * 4) : -16;
-      const u32x4 o0 = {__float_as_uint(cs[0]), __float_as_uint(cs[1]), __float_as_uint(cs[2]), __float_as_uint(cs[3])};
-      const u32x4 o1 = {__float_as_uint(cs[4]), __float_as_uint(cs[5]), __float_as_uint(cs[6]), __float_as_uint(cs[7])};
-      __builtin_amdgcn_raw_buffer_store_b128(o0, rcol, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(o1, rcol, wr ? off + 16 : off, 0, 0);
     }
   };
 
@@ -522,12 +474,12 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   }
 }
 
-template <bool F32OUT, bool DACT>
+template <bool F32OUT>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
-  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if constexpr (!DACT) hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, DACT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
 }  // namespace pp
@@ -536,15 +488,9 @@ static int g_pp_cus = 0;
 
 bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
   using namespace pp;
-  if (p.dact) {
-    // dgrad with the producer's stored act'(z) (act ACT_GRADMUL): bf16 C, no bias / beta / Z
-    if (p.act != ACT_GRADMUL || !p.zin || p.out_f32 || p.bias || p.Z || p.beta != 0.f) return false;
-    if (((uintptr_t)p.zin & 15) || (p.colpart && ((uintptr_t)p.colpart & 15))) return false;
-  } else if (p.Z || p.act != ACT_NONE) {
-    return false;
-  }
+  if (p.dact || p.Z || p.act != ACT_NONE) return false;
   const bool split = p.splitk > 1 && p.ws;
-  if (split && (p.dact || !p.out_f32 || p.bias || p.alpha != 1.f || p.K / BK < p.splitk ||
+  if (split && (!p.out_f32 || p.bias || p.alpha != 1.f || p.K / BK < p.splitk ||
                 (int64_t)p.splitk * p.M * p.N * 4 > 0x7fffff00LL))
     return false;
   if ((p.beta != 0.f && !split) || p.batch != 1 || p.K % BK != 0 ||
@@ -564,10 +510,8 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * (split ? p.splitk : 1);
   dim3 grid(std::min(tiles, g_pp_cus));
-  if (p.dact && !p.a_kcontig && !p.b_kcontig) return false;
-  if (p.dact) launch<false, true>(p, grid, stream, a_bytes, b_bytes);
-  else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
-  else launch<false, false>(p, grid, stream, a_bytes, b_bytes);
+  if (p.out_f32) launch<true>(p, grid, stream, a_bytes, b_bytes);
+  else launch<false>(p, grid, stream, a_bytes, b_bytes);
   return true;
 }
 

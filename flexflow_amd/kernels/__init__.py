@@ -608,9 +608,6 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
             cands = {}
             if fused(scratch, dbs):
                 cands["fused"] = lambda: fused(scratch, dbs)
-            # the persistent ping-pong kernel multiplies by a stored act' (ACT_GRADMUL) in its epilogue
-            if act == ACT_GRADMUL and fused(scratch, dbs, 6):
-                cands["pp"] = lambda: fused(scratch, dbs, 6)
             if not cands:
                 choice = "unfused"
             else:
@@ -623,8 +620,6 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
                 _timed.add(key)
         _tuned[key] = choice
     if choice == "fused" and fused():
-        return C
-    if choice == "pp" and fused(impl=6):
         return C
     unfused()
     return C
