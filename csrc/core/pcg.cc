@@ -2,6 +2,9 @@
 #include "pcg.h"
 
 #include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 #include <cmath>
 #include <numeric>
 #include <set>
@@ -142,7 +145,7 @@ static bool is_all_to_all(const Layout& S, const Layout& D) {
   return true;
 }
 
-XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const MachineModel& mm) {
+static XferCost transfer_cost_uncached(const Layout& S, const Layout& D, bool sp, int eb, const MachineModel& mm) {
   XferCost x;
   const bool same_blocks = S.degrees == D.degrees;
   const double lat = mm.latency_us * 1e-3;
@@ -272,6 +275,50 @@ XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const 
   for (auto& kv : egress) worst_dev = std::max(worst_dev, kv.second / (mm.links_per_gpu * mm.link_gbps * 1e6));
   for (auto& kv : ingress) worst_dev = std::max(worst_dev, kv.second / (mm.links_per_gpu * mm.link_gbps * 1e6));
   x.ms = link.empty() ? 0.0 : std::max(worst_link, worst_dev) + lat;
+  return x;
+}
+
+// The joint search costs every rewritten graph with a fresh Problem, and the frontier DP prices
+// (producer config x consumer config) edges lazily: without a shared memo the same layout pairs
+// were priced again per graph (~1 s of a 3 s Inception-v3 N=8 search). Transfer costs depend only
+// on the two layouts, the partial flag, the element size and the machine; the memo is keyed by all
+// of them (the topology by identity) and cleared when it grows past 1 M entries.
+namespace {
+void key_put(std::string& k, int64_t v) { k.append(reinterpret_cast<const char*>(&v), sizeof(v)); }
+void key_put(std::string& k, const Layout& L) {
+  key_put(k, (int64_t)L.shape.size());
+  for (auto v : L.shape) key_put(k, v);
+  for (auto v : L.degrees) key_put(k, v);
+  key_put(k, L.replicas);
+  key_put(k, (int64_t)L.devices.size());
+  for (auto v : L.devices) key_put(k, v);
+  key_put(k, (int64_t)L.halo.size());
+  for (auto v : L.halo) key_put(k, v);
+}
+std::mutex g_xfer_memo_mu;
+std::unordered_map<std::string, XferCost> g_xfer_memo;
+}  // namespace
+
+XferCost transfer_cost(const Layout& S, const Layout& D, bool sp, int eb, const MachineModel& mm) {
+  std::string k;
+  k.reserve(256);
+  key_put(k, S);
+  key_put(k, D);
+  key_put(k, (int64_t)sp * 2 + (int64_t)S.partial);
+  key_put(k, eb);
+  const double mf[] = {mm.link_gbps, mm.links_per_gpu, mm.coll_eff, mm.inter_node_gbps, mm.latency_us, mm.hbm_gbps};
+  k.append(reinterpret_cast<const char*>(mf), sizeof(mf));
+  key_put(k, (int64_t)mm.num_nodes * 4096 + mm.gpus_per_node);
+  key_put(k, (int64_t)(intptr_t)mm.topo.get());
+  {
+    std::lock_guard<std::mutex> g(g_xfer_memo_mu);
+    auto it = g_xfer_memo.find(k);
+    if (it != g_xfer_memo.end()) return it->second;
+  }
+  XferCost x = transfer_cost_uncached(S, D, sp, eb, mm);
+  std::lock_guard<std::mutex> g(g_xfer_memo_mu);
+  if (g_xfer_memo.size() > (1u << 20)) g_xfer_memo.clear();
+  g_xfer_memo.emplace(std::move(k), x);
   return x;
 }
 

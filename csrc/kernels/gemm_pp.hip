@@ -102,7 +102,7 @@ __device__ __forceinline__ int opaque_lane() {
 template <bool F32OUT>
 constexpr int epi_ops() { return (F32OUT ? 32 : 16) + 2; }
 
-template <bool A_K, bool B_K, bool F32OUT>
+template <bool A_K, bool B_K, bool F32OUT, bool SPLIT>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
@@ -116,7 +116,9 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   // ws[slice][M][N] that slab_sum folds; S = 1: the tile's output straight into C)
   // slice s of a tile covers K-tiles [s nkt / S, (s + 1) nkt / S) (any S <= nkt: S is chosen so
   // that the units fill the CUs, e.g. 48 tiles x 5 slices)
-  const int S = (p.splitk > 1 && p.ws) ? p.splitk : 1;
+  // (a template parameter: the run-time form cost the unsplit kernel ~20 SGPRs, spilled to VGPR
+  // lanes and read back in every memory phase)
+  const int S = SPLIT ? p.splitk : 1;
   const int total = tm * tn * S;
   const int nkt = p.K / BK;
   const int first = blockIdx.x;
@@ -313,8 +315,8 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, (int)min(c_bytes, (int64_t)0x7fffffff), 0x00020000);
   // split-K: one range-checked descriptor over all slabs ([S][M][N] fp32, ldc = N)
   const int64_t ws_bytes = (int64_t)S * p.M * p.N * 4;
-  if (S > 1) rc = __builtin_amdgcn_make_buffer_rsrc(p.ws, (short)0, (int)min(ws_bytes, (int64_t)0x7fffffff), 0x00020000);
-  const int64_t ldo = S > 1 ? p.N : p.ldc;
+  if constexpr (SPLIT) rc = __builtin_amdgcn_make_buffer_rsrc(p.ws, (short)0, (int)min(ws_bytes, (int64_t)0x7fffffff), 0x00020000);
+  const int64_t ldo = SPLIT ? p.N : p.ldc;
   const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
   __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
   const float alpha = p.alpha;
@@ -474,12 +476,12 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   }
 }
 
-template <bool F32OUT>
+template <bool F32OUT, bool SPLIT>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
-  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
 }  // namespace pp
@@ -510,8 +512,9 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * (split ? p.splitk : 1);
   dim3 grid(std::min(tiles, g_pp_cus));
-  if (p.out_f32) launch<true>(p, grid, stream, a_bytes, b_bytes);
-  else launch<false>(p, grid, stream, a_bytes, b_bytes);
+  if (split) launch<true, true>(p, grid, stream, a_bytes, b_bytes);  // split-K: fp32 slabs only
+  else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
+  else launch<false, false>(p, grid, stream, a_bytes, b_bytes);
   return true;
 }
 

@@ -22,6 +22,9 @@ layer names plus parameters, so it can be replayed on another process):
     op follow from its config (the executor's transfers are the Repartition/Combine data movement),
     so the xfer pins the op's degree on one axis for every op of the same signature (BERT's 24
     identical FFN layers move together: a coarse move the per-op DP + MCMC rarely reaches).
+  * block pins (combine_inception / combine_concat) and leading_relu_branch_{combine,partition}
+    (substitution.cc:3099-3167, 3463-3540): a fork's branches pinned to one sample degree so the
+    fork tensor is re-laid-out once (or not at all) instead of once per branch.
   * JSON rules (--substitution-json, non-fusion rules) through pcg/substitutions.apply_rule.
 """
 from __future__ import annotations
@@ -29,6 +32,7 @@ from __future__ import annotations
 import heapq
 import math
 import os
+import sys
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -350,6 +354,76 @@ class BlockPin:
         return _pin_layers(model, olds, lambda L: degs[id(L)], f"{self.family}{self.degree}")
 
 
+class LeadingBranch:
+    """leading_relu_branch_combine / leading_relu_branch_partition (substitution.cc:3463-3540,
+    generated at 1839-1841 for num_combines 1..4 on the sample dim). In the reference a tensor that
+    fans out (Inception's ReLU'd tower inputs, a residual fork) feeds one branch through a
+    Repartition and `num` sibling branches through Combines (or one through a Combine and `num`
+    through Repartitions); the rewrite keeps the leading branch's re-layout and turns the `num`
+    siblings' into no-ops, so those branches consume the fork tensor as it is laid out.
+
+    Here a layout change on an edge is implied by the degrees of its two ends, so the two forms
+    become pins on a fork F -> consumers c0 (the leading branch), c1..c_num:
+      * combine[d, num]: c0..c_num all sample-parallel `d` ways — the leading branch's
+        re-layout of F serves every sibling (one transfer of F instead of num + 1);
+      * partition[d, num]: F's producer and c1..c_num sample-parallel `d` ways — the siblings
+        read F where it is produced (no transfer on those edges); c0 keeps its own layout.
+    Forks are ranked by the flops of the ops they pin; at most `max_forks` matches."""
+
+    def __init__(self, family: str, degree: int, num: int, max_forks: int = 2):
+        assert family in ("leading_relu_branch_combine", "leading_relu_branch_partition")
+        self.family = family
+        self.degree = degree
+        self.num = num
+        self.max_forks = max_forks
+        self.name = f"{family}[{degree},{num}]"
+
+    def _degs(self, L):
+        sizes = L.impl.axis_sizes()
+        if not sizes or L.impl.axis_kinds()[0] != "sample" or sizes[0] % self.degree:
+            return None
+        degs = [1] * len(sizes)
+        degs[0] = self.degree
+        return degs if _pin_ok(L, degs) else None
+
+    def _pinned(self, prod, consumers):
+        if self.family == "leading_relu_branch_combine":
+            return consumers[:self.num + 1]
+        return [prod] + consumers[1:self.num + 1]
+
+    def matches(self, model) -> List[tuple]:
+        from ..type import OperatorType as OT
+        pos = {id(L): i for i, L in enumerate(model.layers)}
+        readers: Dict[int, List] = {}
+        for L in model.layers:
+            for t in {t.guid: t for t in L.inputs}.values():
+                readers.setdefault(t.guid, []).append(L)
+        out = []
+        for P in model.layers:
+            if P.op_type == OT.OP_INPUT or not P.outputs:
+                continue
+            cons = readers.get(P.outputs[0].guid, [])
+            if len(cons) < self.num + 1:
+                continue
+            pins = self._pinned(P, cons)
+            if any("pin" in L.attrs or L.op_type == OT.OP_INPUT or self._degs(L) is None for L in pins):
+                continue
+            w = sum(_weight([L]) for L in pins)
+            out.append((w, (self.family, self.degree, self.num, tuple(pos[id(L)] for L in pins))))
+        out.sort(key=lambda m: -m[0])
+        return [m for _, m in out[:self.max_forks]]
+
+    def apply(self, model, match) -> bool:
+        _, _, _, positions = match
+        olds = _at(model, positions)
+        if any(L is None or "pin" in L.attrs for L in olds):
+            return False
+        degs = {id(L): self._degs(L) for L in olds}
+        if any(d is None for d in degs.values()):
+            return False
+        return _pin_layers(model, olds, lambda L: degs[id(L)], f"lrb{self.family[20]}{self.degree}x{self.num}")
+
+
 class LinearReluMerge:
     """create_linear_relu_merge (substitution.cc:1790-1793): Linear (no activation) followed by its
     only consumer ReLU becomes one Linear with a fused ReLU epilogue (same parameters)."""
@@ -430,6 +504,10 @@ def parallel_xfers(cfg) -> List:
                PinAxis("partition_pool2d_combine", [OT.OP_POOL2D], _axis(0), d),
                PinAxis("partition_flat_combine", [OT.OP_FLAT], _axis(0), d),
                BlockPin("combine_inception", d, True), BlockPin("combine_concat", d, False)]
+        # generate_all_pcg_xfers' loop over num_combines 1..4 (substitution.cc:1839-1841)
+        for num in range(1, 5):
+            xs += [LeadingBranch("leading_relu_branch_combine", d, num),
+                   LeadingBranch("leading_relu_branch_partition", d, num)]
         if "attribute" in kinds:  # spatial mappings (halo exchange) only with attribute parallelism
             for ax in (2, 3):
                 xs += [PinAxis(f"partition_conv2d_combine_dim{ax}", [OT.OP_CONV2D], _axis(ax), d),
@@ -492,6 +570,9 @@ def _xfer_from_name(name: str):
     if "[" not in name or not name.endswith("]"):
         return None
     fam, deg = name[:-1].split("[", 1)
+    if fam.startswith("leading_relu_branch_"):
+        d, num = (deg.split(",") + [""])[:2]
+        return LeadingBranch(fam, int(d), int(num)) if d.isdigit() and num.isdigit() else None
     if not deg.isdigit():
         return None
     if fam in ("combine_inception", "combine_concat"):
@@ -596,6 +677,9 @@ def joint_search(model, algo: str = "unity", budget: Optional[int] = None, alpha
                 _, rep = param_search(model, algo, quick=True)
                 evals += 1
                 c = rep["predicted_ms"]
+                if os.environ.get("FF_SEARCH_PROGRESS") == "1":
+                    print(f"[joint] graph {evals}: {x.name} -> {c:.4f} ms (best {best[0]:.4f})", file=sys.stderr,
+                          flush=True)
                 step = (x.name, _tuple(m))
                 tried.append({"xfer": x.name, "match": _jsonable(m), "after": [s_[0] for s_ in seq],
                               "new_ops": [L.name for L in model.layers if id(L) not in cur_ids][:4],

@@ -14,6 +14,7 @@ always; parameter parallelism (channels / heads / reductions / vocab) unless
 from __future__ import annotations
 
 import os
+import sys
 import time
 from types import SimpleNamespace
 
@@ -127,7 +128,12 @@ def build_problem(model, n_devices: int, measure: bool):
     from .strategy import machine_device_sets
     dsets = machine_device_sets(n_devices, prob.machine.gpus_per_node)
     max_cands = int(os.environ.get("FF_MAX_CANDS", "32"))
+    progress = os.environ.get("FF_SEARCH_PROGRESS") == "1"  # long measured searches: a line per 16 ops
+    t_prog = time.perf_counter()
     for i, L in enumerate(layers):
+        if progress and i % 16 == 0:
+            print(f"[search] costing op {i}/{len(layers)} ({time.perf_counter() - t_prog:.1f} s)", file=sys.stderr,
+                  flush=True)
         # candidates and their costs depend only on the op's signature: identical layers (BERT's 24
         # encoder layers) and the unchanged layers of a rewritten graph (joint search) reuse them
         key = (layer_signature(L), n_devices, kinds, cdt, bool(measure), prob.machine.gpus_per_node, max_cands,
@@ -184,8 +190,8 @@ def search(model, algo: str, quick: bool = False):
     budget = cfg.search_budget if cfg.search_budget and cfg.search_budget > 0 else None
 
     def run_search():
-        if quick:
-            return core.search_unity(prob, 4096, 0, cfg.search_alpha, cfg.seed)
+        if quick:  # ranking rewritten graphs (joint search): a narrower frontier, no refinement
+            return core.search_unity(prob, int(os.environ.get("FF_JOINT_BEAM", "512")), 0, cfg.search_alpha, cfg.seed)
         if algo == "mcmc":
             return core.search_mcmc(prob, dp_choice, budget or cfg.mcmc_iterations, cfg.search_alpha, cfg.seed)
         return core.search_unity(prob, 4096, budget if budget is not None else 300, cfg.search_alpha, cfg.seed)

@@ -23,17 +23,17 @@ SHAPES = [
     ("fwd", T, 1024, 1024, True, True, 25, False),
     ("fwd", T, 4096, 1024, True, True, 24, False),
     ("fwd", T, 1024, 4096, True, True, 24, False),
-    ("fwd", T, 30522, 1024, True, True, 1, False),
+    ("fwd", T, 30528, 1024, True, True, 1, False),
     ("dgrad", T, 1024, 3072, True, False, 24, False),
     ("dgrad", T, 1024, 1024, True, False, 25, False),
     ("dgrad", T, 4096, 1024, True, False, 24, False),
     ("dgrad", T, 1024, 4096, True, False, 24, False),
-    ("dgrad", T, 1024, 30522, True, False, 1, False),
+    ("dgrad", T, 1024, 30528, True, False, 1, False),
     ("wgrad", 3072, 1024, T, False, False, 24, True),
     ("wgrad", 1024, 1024, T, False, False, 25, True),
     ("wgrad", 4096, 1024, T, False, False, 24, True),
     ("wgrad", 1024, 4096, T, False, False, 24, True),
-    ("wgrad", 30522, 1024, T, False, False, 1, True),
+    ("wgrad", 30528, 1024, T, False, False, 1, True),
 ]
 IMP = {"pp": 6, "pp_nodma": 61, "w4q": 5, "w4q_nostore": 51, "w4q_nodma": 53, "w4q_nobar": 57, "w4q_samek": 59, "w4q_sc1": 71, "w4q_nt": 72, "w4q_ntsc1": 73, "w4q_sc0": 74, "w4q_glds": 82, "w4p": 4, "w4p_nostore": 40, "w4": 3, "k256": 2, "big": 1, "128": 0}
 dev = "cuda"
