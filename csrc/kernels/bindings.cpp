@@ -107,6 +107,27 @@ bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias,
   return true;
 }
 
+void box_copy(Tensor src, Tensor dst, Tensor desc, int64_t nbox, int64_t max_n, int64_t vec_bytes, bool add) {
+  check_dev(src, "src"); check_dev(dst, "dst"); check_dev(desc, "desc");
+  TORCH_CHECK(desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.numel() >= nbox * ffk::box_words(),
+              "box_copy: descriptors");
+  TORCH_CHECK(nbox >= 0 && nbox <= 65535, "box_copy: at most 65535 boxes per launch");
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type(), "box_copy: one dtype");
+  int dt = 0;
+  if (add) {
+    TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16, "box_copy add: fp32 / bf16");
+    dt = src.scalar_type() == at::kFloat ? ffk::DT_F32 : ffk::DT_BF16;
+  } else {
+    TORCH_CHECK(vec_bytes == 1 || vec_bytes == 2 || vec_bytes == 4 || vec_bytes == 8 || vec_bytes == 16,
+                "box_copy: vector width");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) % vec_bytes) == 0 &&
+                    (reinterpret_cast<uintptr_t>(dst.data_ptr()) % vec_bytes) == 0,
+                "box_copy: pointers not aligned to the vector width");
+  }
+  ffk::box_copy(src.data_ptr(), dst.data_ptr(), desc.data_ptr<int64_t>(), (int)nbox, max_n, (int)vec_bytes,
+                add ? 1 : 0, dt, cur_stream());
+}
+
 int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t impl) {
   return ffk::gemm_pick_splitk(M, N, K, batch, (int)impl);
 }
@@ -708,6 +729,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("sC"), py::arg("batch"), py::arg("a_k"), py::arg("b_k"), py::arg("alpha"), py::arg("beta"),
         py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2, py::arg("skip_reduce") = false);
   m.def("gemm_dact", &gemm_dact);
+  m.def("box_copy", &box_copy);
+  m.def("box_words", []() { return ffk::box_words(); });
+  m.def("box_dims", []() { return ffk::box_dims(); });
   m.def("lstm_fwd_cell", &lstm_fwd_cell);
   m.def("lstm_bwd_cell", &lstm_bwd_cell);
   m.def("lt_plan", &lt_plan);

@@ -45,6 +45,14 @@ int col_reduce_gy();
 void col_reduce_set_gy(int g);
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st);
 
+// transfer.hip: one launch over a list of boxes (pack / unpack / local re-layout of activation
+// shards); desc: device int64 [nbox][box_words()] (see transfer.hip), units of vec_bytes (copy)
+// or elements of dt (add: dst += src)
+int box_words();
+int box_dims();
+void box_copy(const void* src, void* dst, const int64_t* desc, int nbox, int64_t max_n, int vec_bytes, int add,
+              int dt, hipStream_t st);
+
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
 // on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.
 constexpr int kMoeMaxExperts = 64;

@@ -76,21 +76,24 @@ for kind, M, N, K, a_k, b_k, calls, f32 in SHAPES:
     A = (torch.rand((M, K) if a_k else (K, M), device=dev, generator=g) * 2 - 1).bfloat16()
     B = (torch.rand((N, K) if b_k else (K, N), device=dev, generator=g) * 2 - 1).bfloat16()
     C = torch.empty(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
-    fns = {im: runner(im, A, B, C, M, N, K, a_k, b_k) for im in impls}
+    use = [im for im in impls if f32 or "_sk" not in im]  # split-K: fp32 weight gradients only
+    fns = {im: runner(im, A, B, C, M, N, K, a_k, b_k) for im in use}
     best = {}
     for _ in range(rounds):
         for im, fn in fns.items():
             t = timed(fn)
             best[im] = min(best.get(im, t), t)
     fl = 2.0 * M * N * K
-    line = " ".join(f"{im}={best[im] * 1e3:8.1f}us({fl / best[im] / 1e9:6.0f}TF)" for im in impls)
+    line = " ".join(f"{im}={best[im] * 1e3:8.1f}us({fl / best[im] / 1e9:6.0f}TF)" for im in use)
     win = min(best, key=best.get)
     print(f"{kind:5s} M={M:5d} N={N:5d} K={K:5d} x{calls:2d}: {line}  best={win}", flush=True)
-    for im in impls:
+    for im in use:
         summary.setdefault((kind, im), 0.0)
         summary[(kind, im)] += best[im] * calls
     summary.setdefault((kind, "best_ours"), 0.0)
-    summary[(kind, "best_ours")] += min(best[im] for im in impls if im != "lib") * calls
+    summary[(kind, "best_ours")] += min(best[im] for im in use if not im.startswith("lib")) * calls
+    summary.setdefault((kind, "best_lib"), 0.0)
+    summary[(kind, "best_lib")] += min([best[im] for im in use if im.startswith("lib")] or [0.0]) * calls
     del A, B, C
 for (kind, im), ms in sorted(summary.items()):
     print(f"step total {kind:5s} {im:9s}: {ms:7.3f} ms")

@@ -6,6 +6,7 @@ set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 mkdir -p $OUT
 export FF_SEARCH_PROGRESS=1
+export FF_JOINT_MAX_GRAPHS=${FF_JOINT_MAX_GRAPHS:-256}
 run() {
   local name=$1 limit=$2; shift 2
   timeout -k 10 $limit python -u scripts/export_search.py "$@" > $OUT/$name.log 2>&1

@@ -58,6 +58,7 @@ def _worker(rank, port, out_dir):
                 x = x * (1 + rank)  # partial sums: rank r holds (1 + r) g
         y = t.run(comm, x, like=g)
         res[f"kind{i}"] = np.array([t.kind == kind])
+        res[f"plans{i}"] = np.array([bool(t.__dict__.get("_plans"))])
         dp = D.parts_on(rank)
         if dp:
             ref = _part(D, dp[0], g) * (sum(1 + q for q in range(W)) if sp else 1)
@@ -66,11 +67,17 @@ def _worker(rank, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_transfers_over_gloo(tmp_path):
+@pytest.mark.parametrize("boxes", [False, True])
+def test_transfers_over_gloo(tmp_path, monkeypatch, boxes):
+    """boxes: the exchange / generic packs, unpacks and local moves run as box-copy plans
+    (parallel/boxcopy.py; on the GPU one transfer.hip launch each), emulated here on CPU tensors."""
+    monkeypatch.setenv("FF_BOXCOPY_EMULATE", "1" if boxes else "0")
     mp.start_processes(_worker, args=(_port(), str(tmp_path)), nprocs=W, join=True, start_method="spawn")
     for r in range(W):
         d = dict(np.load(tmp_path / f"r{r}.npz"))
         for i in range(len(CASES)):
             assert bool(d[f"kind{i}"][0]), (r, i, "kind")
+            if CASES[i][3] == "exchange":  # every rank packs and unpacks through box plans
+                assert bool(d[f"plans{i}"][0]) == boxes, (r, i, "box plans")
             if f"ok{i}" in d:
                 assert bool(d[f"ok{i}"][0]), (r, i, "value")
