@@ -1131,6 +1131,19 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
     const float* dl_l = lse_l + QT;
     const bool more = t + 1 < nqt;
     if (more) fetch(t + 1);  // in flight during this tile's MFMAs
+    // chain, key block > 0: the previous launch's dQ running sum for this wave's dQ tile, requested
+    // now so its HBM round trip runs under the tile's MFMAs (read at its use below, the load sat on
+    // the workgroup's critical path once per query tile)
+    float4 prev[4];
+    if constexpr (NW >= 2 * (D / 32)) {
+      const int tile = wave % (2 * (D / 32));
+      const int q = qbase + 32 * (tile / (D / 32)) + (lane & 31);
+      if (chain && kblk > 0 && wave < 2 * (D / 32) && (!MASK || q < a.Sq)) {
+        const float* prow = dq_part + (int64_t)q * D + 32 * (tile % (D / 32)) + 4 * h;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) prev[g] = *reinterpret_cast<const float4*>(prow + 8 * g);
+      }
+    }
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       // S[q][key] and dP[q][key] for 32 queries x this wave's 32 keys
@@ -1240,7 +1253,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
           // a causal block's query tiles all had key block kblk - 1 contributing too
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const float4 pv = *reinterpret_cast<const float4*>(prow + 8 * g);
+            float4 pv;
+            if constexpr (NW >= 2 * (D / 32)) pv = prev[g];  // prefetched at the top of the tile
+            else pv = *reinterpret_cast<const float4*>(prow + 8 * g);
             acc[4 * g] += pv.x; acc[4 * g + 1] += pv.y; acc[4 * g + 2] += pv.z; acc[4 * g + 3] += pv.w;
           }
         }
