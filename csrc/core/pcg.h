@@ -81,7 +81,12 @@ struct Node {
 struct MachineModel {
   int num_nodes = 1;
   int gpus_per_node = 8;
-  double link_gbps = 64.0;         // one xGMI link, one direction, GB/s
+  // one xGMI link, one direction, GB/s: MI355X's Infinity Fabric link is 153.6 GB/s counting both
+  // directions (7 links per GPU, 1075 GB/s aggregate peer bandwidth, the vendor data sheet figure
+  // this task quotes as "7 links x ~153 GB/s"), so 76.8 per direction; r1-r4 used MI300X's
+  // 128 / 2 = 64. A spec figure, not a measurement: no multi-GPU box was available to this work
+  // (coll_eff below is the assumed achieved fraction of it).
+  double link_gbps = 76.8;
   double links_per_gpu = 7;        // fully connected 8-GPU node
   double coll_eff = 0.75;          // achieved fraction of the (r-1) x link ring-bus bandwidth
   double inter_node_gbps = 50.0;   // per-GPU NIC bandwidth

@@ -87,6 +87,24 @@ def _saturate(device):
         pass
 
 
+def _hot_inputs(layer) -> list:
+    """Per input: is it still cache-resident when this op runs in a training step? An input the
+    directly preceding op (in the executor's topological order) produced was written microseconds
+    before; any other input (a residual stream, a model input, an activation produced several ops
+    earlier) comes from HBM. r4 timed every forward input cold, which made MHA +31 % and Linear
+    +15 % slow against the step; all-warm had made LayerNorm (whose residual input is cold) fast."""
+    m = getattr(layer, "model", None)
+    layers = getattr(m, "layers", None) or []
+    pos = {id(L): i for i, L in enumerate(layers)}
+    me = pos.get(id(layer))
+    out = []
+    for t in layer.inputs:
+        p = getattr(t, "owner_layer", None)
+        ok = me is not None and p is not None and p.op_type != OperatorType.OP_INPUT and pos.get(id(p)) == me - 1
+        out.append(bool(ok))
+    return out
+
+
 def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: int = 8) -> Tuple[float, float]:
     """Time the op's own forward/backward on this GPU with the shard shapes of `cfg`, the way a
     training step runs it (reference simulator.cu measure_operator_cost; model.cu:38-75):
@@ -100,15 +118,21 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
     need_dx0 = bool(layer.inputs) and layer.inputs[0].owner_layer is not None and \
         layer.inputs[0].owner_layer.op_type != OperatorType.OP_INPUT
     key = (layer.op_type, layer.impl.params_key(), tuple(l.local_shape(0) for l in lo.inputs),
-           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0)
+           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0, tuple(_hot_inputs(layer)))
     if key in _measured:
         return _measured[key]
     ct = torch.bfloat16 if compute_dtype == DataType.DT_BF16 else torch.float32
 
+    hot = _hot_inputs(layer)
+    shared: dict = {}
+
     def make_inputs():
         xs = []
-        for t, l in zip(layer.inputs, lo.inputs):
+        for i, (t, l) in enumerate(zip(layer.inputs, lo.inputs)):
             shp = l.local_shape(0)
+            if hot[i] and i in shared:  # produced just before this op in a step: one cache-warm copy
+                xs.append(shared[i])
+                continue
             if t.data_type in (DataType.DT_INT32, DataType.DT_INT64):
                 hi = 2
                 if layer.op_type == OperatorType.OP_EMBEDDING:
@@ -116,6 +140,8 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
                 xs.append(torch.randint(0, max(1, hi), shp, device=device, dtype=torch.int32))
             else:
                 xs.append(_step_layout(torch.randn(shp, device=device, dtype=ct)))
+            if hot[i]:
+                shared[i] = xs[-1]
         # identical tensors in the graph stay identical (fused self-attention)
         seen = {}
         for i, t in enumerate(layer.inputs):
@@ -160,6 +186,10 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
         n = max(2, min(reps, int(math.ceil(768e6 / max(in_bytes, 1)))))  # copies past the 256 MB MALL
         xs_all = [make_inputs() for _ in range(n)]
         ctxs = [make_ctx() for _ in range(n)]
+        # weights are cold in a step too (last touched by the previous step's update): one copy per
+        # repetition unless that would pass ~1 GiB (Embedding read a warm 62 MB table 22 % fast, r4)
+        wbytes = sum(w.numel() * w.element_size() for w in ws)
+        ws_all = [ws] + [[w.clone() for w in ws] for _ in range(n - 1)] if wbytes * n <= (1 << 30) else [ws] * n
         torch.cuda.synchronize()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # device time (queue saturated) and host time (the op's own dispatch): an eager step runs
@@ -170,8 +200,8 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
         _saturate(device)
         st.record()
         h0 = time.perf_counter()
-        for c, xs in zip(ctxs, xs_all):
-            impl.forward(c, xs, ws)
+        for c, xs, wk in zip(ctxs, xs_all, ws_all):
+            impl.forward(c, xs, wk)
         hf = (time.perf_counter() - h0) * 1e3 / n
         en.record()
         en.synchronize()
@@ -186,7 +216,7 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
         en.record()
         en.synchronize()
         tb = max(st.elapsed_time(en) / n, hb)
-        del ctxs, xs_all
+        del ctxs, xs_all, ws_all
     except Exception:
         tf, tb = analytic_cost(layer, cfg, compute_dtype)
     _measured[key] = (tf, tb)
