@@ -694,7 +694,7 @@ class GradBucketer:
                     self.on_ready(b, h)
 
     def _launch(self, b):
-        if (len(b["group"]) <= 1 and not self.comm.force) or not self.comm.distributed:
+        if (len(b["group"]) <= 1 and not getattr(self.comm, "force", False)) or not self.comm.distributed:
             return None
         view = b["flat"][b["lo"]:b["hi"]]
         g = self.comm.group(b["group"])
