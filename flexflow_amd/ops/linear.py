@@ -75,10 +75,13 @@ class Linear(OpImpl):
             b = None
         Kl = x.shape[-1]
         x2 = x.reshape(-1, Kl)
-        # when the consumer's dgrad GEMM applies this op's act' (Executor._plan_dact_fusion), the
-        # forward stores act'(z) instead of z: the fused epilogue then multiplies by it
+        # FF_DACT_STORE_GRAD=1: when the consumer's dgrad applies this op's act' (Executor.
+        # _plan_dact_fusion), the forward stores act'(z) instead of z and the backward only
+        # multiplies by it. Off by default: the forward pass then writes y AND act'(z) (384 instead
+        # of 256 MB per BERT-Large FFN1 call, bias_act_fwd 1.23 -> 1.61 ms per step) while the
+        # backward pass moves the same bytes either way (its act' VALU hides under HBM time).
         sg = bool(ctx.training and ctx.extra.get("dact_fused") and self.act != K.ACT_NONE
-                  and os.environ.get("FF_DACT_STORE_GRAD", "1") == "1")
+                  and os.environ.get("FF_DACT_STORE_GRAD", "0") == "1")
         y, z = K.linear_fwd(x2, w, b, self.act, save_z=ctx.training, store_grad=sg)
         if ctx.training:
             ctx.saved["x"] = x2

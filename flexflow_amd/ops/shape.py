@@ -8,10 +8,12 @@ every dim except the one they act on).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from .. import kernels as K
+from ..parallel import boxcopy
 from ..type import DataType, OperatorType
 from .base import OpImpl, register
 
@@ -180,7 +182,49 @@ class Concat(OpImpl):
         return [torch.cat(xs, self.attrs["axis"])]
 
     def backward(self, ctx, douts):
-        return list(torch.split(douts[0], ctx.saved.pop("sizes"), self.attrs["axis"]))
+        sizes = ctx.saved.pop("sizes")
+        dy = douts[0]
+        if len(sizes) > 1 and boxcopy.available(dy) and os.environ.get("FF_BOX_SPLIT", "1") == "1":
+            return _split_dense(self, dy, sizes, self.attrs["axis"])
+        return list(torch.split(dy, sizes, self.attrs["axis"]))
+
+
+def _split_dense(op, dy, sizes, ax):
+    """torch.split of a concat's gradient into DENSE parts (each in dy's memory format, side by
+    side in one buffer) by one box-copy launch (csrc/kernels/transfer.hip). The views torch.split
+    returns are strided along the split dim (a channel slice of an NHWC gradient), and every
+    consumer made its own ATen copy of one: Inception-v3 paid ~23 copy launches per backward
+    (reference concat_kernels.cu backward: one copy per input as well)."""
+    cl = dy.dim() == 4 and not dy.is_contiguous() and dy.is_contiguous(memory_format=torch.channels_last)
+    if not (cl or dy.is_contiguous()):
+        return list(torch.split(dy, sizes, ax))
+    flat = torch.empty(dy.numel(), dtype=dy.dtype, device=dy.device)
+    outs, boxes, off, lo = [], [], 0, 0
+    for n in sizes:
+        shp = list(dy.shape)
+        shp[ax] = n
+        if cl:  # NHWC strides of an [N, C, H, W] tensor
+            N_, C_, H_, W_ = shp
+            st = (H_ * W_ * C_, 1, W_ * C_, C_)
+        else:
+            st, acc = [], 1
+            for e in reversed(shp):
+                st.append(acc)
+                acc *= e
+            st = tuple(reversed(st))
+        outs.append(flat.as_strided(shp, st, off))
+        rel = [(0, e) for e in dy.shape]
+        rel[ax] = (lo, lo + n)
+        so, ss, ext = boxcopy.region_box(dy, rel)
+        boxes.append((so, ss, off, st, ext))
+        off += math.prod(shp)
+        lo += n
+    plans = op.__dict__.setdefault("_split_plans", {})
+    key = boxcopy.plan_key("split", dy, flat) + (tuple(sizes), ax)
+    if key not in plans:
+        plans[key] = boxcopy.BoxPlan(boxes, dy, flat)
+    plans[key].run(dy, flat)
+    return outs
 
 
 @register(OperatorType.OP_SPLIT)

@@ -81,3 +81,21 @@ def test_transfers_over_gloo(tmp_path, monkeypatch, boxes):
                 assert bool(d[f"plans{i}"][0]) == boxes, (r, i, "box plans")
             if f"ok{i}" in d:
                 assert bool(d[f"ok{i}"][0]), (r, i, "value")
+
+
+@pytest.mark.parametrize("cl", [False, True])
+def test_concat_backward_dense_split(monkeypatch, cl):
+    """Concat's backward splits its gradient into dense parts in dy's memory format with one box
+    plan (ops/shape.py _split_dense; one transfer.hip launch on the GPU), equal to torch.split."""
+    monkeypatch.setenv("FF_BOXCOPY_EMULATE", "1")
+    from flexflow_amd.ops.shape import _split_dense
+
+    class _Op:
+        pass
+    dy = torch.randn(2, 10, 3, 4)
+    if cl:
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    outs = _split_dense(_Op(), dy, [3, 5, 2], 1)
+    for a, b in zip(outs, torch.split(dy, [3, 5, 2], 1)):
+        assert torch.equal(a, b)
+        assert a.is_contiguous(memory_format=torch.channels_last) if cl else a.is_contiguous()
