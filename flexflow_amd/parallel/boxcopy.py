@@ -77,7 +77,10 @@ class BoxPlan:
         for so, ss, do, ds, ext in boxes:
             if any(e <= 0 for e in ext):
                 continue
-            dims = _coalesce(ext, ss, ds)
+            # iterate dims in the source's memory order (outermost stride first), so a box of a
+            # channel-last tensor walks its channels innermost: contiguous runs, 16-B vectors
+            order = sorted(range(len(ext)), key=lambda k: (-ss[k], -ds[k]))
+            dims = _coalesce([ext[k] for k in order], [ss[k] for k in order], [ds[k] for k in order])
             if len(dims) > _DIMS:
                 raise ValueError("box_copy: more than 6 non-contiguous dimensions")
             hi_s = so + sum((e - 1) * a for e, a, _ in dims)
