@@ -25,14 +25,18 @@ struct GemmArgs {
   int splitk = 1;
   int kchunk = 0;
   int64_t a_bytes = 0, b_bytes = 0;  // operand storage sizes (range checks of the DMA path)
-  int impl = 2;  // 6: persistent 8-wave ping-pong (gemm_pp.hip, falls back to 4), 5: persistent 4-wave, 4-deep BK=32 ring (gemm_w4q.hip, falls back to 4), 4: persistent 4-wave (gemm_w4p.hip, falls back to 3), 3: 4-wave 256x256x64 (gemm_w4.hip), 2: 256-row ping-pong kernel (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
+  // 6: persistent 8-wave ping-pong (gemm_pp.hip; falls back to 2 for what it refuses), 2: 256-row
+  // kernel with the fused epilogues (gemm256.hip), 1: 256x128 kernel (gemm_big.hip), 0: 128x128
+  // (this file). Round 5 removed the 4-wave kernels 3 / 4 / 5 (gemm_w4{,p,q}.hip): the ping-pong
+  // kernel matched or beat them at every zoo call site they won (profiles/gemm_zoo_tune_r5.txt).
+  int impl = 2;
   // Backward-activation epilogue (gemm256 only, see gemm_dact_bf16): C = (alpha*A.B) * act'(zin),
   // zin the producer's bf16 pre-activation in C's layout; colpart (optional) receives per-128-row
   // fp32 column sums of that product, [2 * ceil(M / 256)][N], for the producer's bias gradient.
   const void* zin = nullptr;
   float* colpart = nullptr;
   bool dact = false;
-  int ablate = 0;  // measurement builds only (impl 40 / 41 in the probes): see gemm_w4p.hip
+  int ablate = 0;  // measurement builds only (impl 61: gemm_pp without its loop DMA)
   bool skip_reduce = false;  // split-K: write the slabs only (the caller runs slab_sum, e.g. on a side stream)
 };
 
@@ -41,13 +45,6 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk);
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl = 2);
 bool gemm_big_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 bool gemm256_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
-// 4-wave 256x256x64 kernel, 128x128 outputs per wave, two-slot LDS-DMA ring (gemm_w4.hip); K % 128 == 0
-bool gemm_w4_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
-// the same main loop as a persistent launch (one workgroup per CU walks the tiles; the next tile's
-// first K-tiles load during this tile's epilogue), gemm_w4p.hip; batch 1, no beta / split-K / Z
-bool gemm_w4p_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
-// the same walk and epilogue with a 4-slot BK = 32 ring (K-tiles requested 3 steps ahead), gemm_w4q.hip
-bool gemm_w4q_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 // persistent 8-wave ping-pong 256x256x64 kernel, two waves per SIMD alternating MFMA and memory
 // phases (gemm_pp.hip); batch 1, no beta / split-K / activation, K % 64 == 0
 bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream);

@@ -351,10 +351,8 @@ int64_t gemm_workspace_bytes(int M, int N, int K, int batch, int splitk) {
 int gemm_pick_splitk(int M, int N, int K, int batch, int impl) {
   // tile count of the kernel that will run
   int64_t tiles;
-  if (impl == 4 || impl == 5 || impl == 6 || impl >= 40) return 1;  // persistent kernels and their ablations  // persistent: every CU busy whatever the tile count
-  if (impl == 3 && K % 128 == 0) {
-    tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
-  } else if (impl == 2 && K % 32 == 0) {
+  if (impl == 6 || impl >= 60) return 1;  // persistent ping-pong kernel: every CU busy whatever the tile count
+  if (impl == 2 && K % 32 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + gemm256_bn(M, N, batch, 1) - 1) / gemm256_bn(M, N, batch, 1)) * batch;
   } else if (impl >= 1 && K % 64 == 0) {
     tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128) * batch;
@@ -380,22 +378,7 @@ static bool try_large(const GemmArgs& p, bool a_al, bool b_al, hipStream_t strea
     q.impl = 6;
     return gemm_pp_bf16(q, p.a_bytes, p.b_bytes, stream);
   }
-  if (p.impl >= 50) {  // ablations of gemm_w4q (timing only): 51 no stores, 53 + no loop DMA, 57 + no barrier
-    GemmArgs q = p;
-    q.ablate = p.impl - 50;
-    q.impl = 5;
-    return gemm_w4q_bf16(q, p.a_bytes, p.b_bytes, stream);
-  }
-  if (p.impl >= 40) {  // ablations of the persistent kernel (timing only: outputs are NOT written)
-    GemmArgs q = p;
-    q.ablate = p.impl - 39;
-    q.impl = 4;
-    return gemm_w4p_bf16(q, p.a_bytes, p.b_bytes, stream);
-  }
   if (p.impl == 6 && gemm_pp_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
-  if (p.impl == 5 && gemm_w4q_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
-  if (p.impl >= 4 && gemm_w4p_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
-  if (p.impl >= 3 && gemm_w4_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl >= 2 && gemm256_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   if (p.impl >= 1 && gemm_big_bf16(p, p.a_bytes, p.b_bytes, stream)) return true;
   return false;

@@ -128,8 +128,8 @@ __device__ __forceinline__ void pin_acc(f32x4 (&acc)[8][NF]) {
 
 // Epilogue of a 256-row tile whose waves each own 128 rows x WN columns (acc[i][j]: rows
 // wr*128 + 16 i + (lane & 15), columns wc*WN + 16 j + 4 (lane >> 4) + r; the MFMA operands are
-// swapped so that a lane holds 4 consecutive columns). Shared by gemm256.hip (8 waves, WN = BN/4)
-// and gemm_w4.hip (4 waves, WN = 128). The LDS operand ring must be free when it is called.
+// swapped so that a lane holds 4 consecutive columns), gemm256.hip (8 waves, WN = BN/4). The LDS
+// operand ring must be free when it is called.
 template <int WN, int OUT_MODE, bool DACT = true, bool SCATTER = true>
 __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x4 (&acc)[8][WN / 16], char* smem, int wave, int wr,
                                            int wc, int lane, int m0, int n0, int b, int z, int tile_m) {

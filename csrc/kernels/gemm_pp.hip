@@ -6,7 +6,7 @@
 // hipBLASLt. Here each SIMD holds two waves that own different halves of the tile's rows and
 // alternate roles every ~1000 cycles:
 //   * a COMPUTE phase: 64 back-to-back v_mfma_f32_16x16x32_bf16 on fragments already in registers
-//     (128 x 64 outputs per wave, 128 AGPR accumulators);
+//     (128 x 64 outputs per wave, 128 accumulator VGPRs);
 //   * a MEMORY phase: this group's share of the LDS-DMA for the next K-tiles, the 24 fragment
 //     reads for its next compute phase and, at a tile boundary, the previous tile's epilogue.
 // Group 0 (waves 0-3: tile rows 0-127) runs one phase ahead of group 1 (waves 4-7: rows
@@ -27,18 +27,18 @@
 //     refills it right behind its own reads). Eight pieces per wave per memory phase.
 // Every piece has ~2 phases (~1 us) to land; each issuing wave retires its pieces with a counted
 // vmcnt before the barrier that precedes their first read (never vmcnt(0) in steady state).
-// The MFMAs are inline asm on "+a" accumulators, the first K-step of a tile uses a zero C operand
+// The MFMAs are inline asm on VGPR accumulators, the first K-step of a tile uses a zero C operand
 // (no accumulator clearing), and all LDS reads are inline asm (hipcc otherwise waits for the
 // LDS-DMA in flight before each read).
 //
 // Epilogue: alpha, bias (fp32 / bf16), bf16 or fp32 output, through a wave-private LDS image into
 // whole-row range-checked buffer stores (see epilogue()). Requires batch 1, beta 0, no activation, K % 64 == 0, 16-B aligned operand
-// rows, operands and output < 2 GiB. Image formats / swizzles as gemm_w4_core.h.
-#include "gemm_w4_core.h"
+// rows, operands and output < 2 GiB. Image formats / swizzles: gemm_pp_core.h, gemm256_tile.h.
+#include "gemm_pp_core.h"
 
 namespace ffk {
 namespace pp {
-using namespace w4;
+using namespace ppcore;
 
 constexpr int NTHR = 512;
 constexpr int NFB = 4;     // 16-column B fragments per wave (64 columns)

@@ -78,7 +78,7 @@ import os as _os
 
 _TUNE = _os.environ.get("FF_GEMM_TUNE", "1") != "0"
 # our kernels: 256-row ping-pong (csrc/kernels/gemm256.hip), 256x128 LDS-DMA (gemm_big.hip), 128x128
-IMPLS = {"pp": 6, "w4q": 5, "w4p": 4, "w4": 3, "k256": 2, "big": 1, "128": 0}
+IMPLS = {"pp": 6, "k256": 2, "big": 1, "128": 0}
 IMPL_DEFAULT = _os.environ.get("FF_GEMM_IMPL", "k256")
 _tuned: dict = {}
 TUNE_LOG: list = []
@@ -156,7 +156,14 @@ def tune_cache_save(path: str) -> int:
 def _tune_cache_lookup(kind, key):
     if not _TUNE_CACHE:
         return None
-    return _cached[kind].get(_ckey(key))
+    c = _cached[kind].get(_ckey(key))
+    # a cache written by an older build may name a kernel that no longer exists (round 5 removed
+    # the 4-wave GEMMs w4 / w4p / w4q): re-tune that site instead of failing at dispatch
+    if kind == "gemm" and isinstance(c, str) and not (
+            c in IMPLS or c in ("lib", "lib_act", "lib_bias_act", "fused", "unfused")
+            or c.startswith(("pp_sk", "lib_sk"))):
+        return None
+    return c
 
 
 if _TUNE_CACHE:
@@ -480,12 +487,9 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                 scratch = torch.zeros_like(C)
                 cands = {k: (lambda i=i: ours(i, scratch)) for k, i in IMPLS.items()}
                 if C.dtype == torch.float32 and batch == 1 and K >= 8192 and splitk is None:
-                    # weight gradients: the split-K factor of the 4-wave and the ping-pong kernels is
-                    # tuned like the library's (fp32 slabs folded by slab_sum)
-                    for S in (2, 4, 8, 16):
-                        if K % (S * 128) == 0:
-                            cands[f"w4_sk{S}"] = (lambda S=S: ours(IMPLS["w4"], scratch, S))
-                    # the ping-pong kernel takes uneven K slices: S that fill the CUs (48 tiles x 5)
+                    # weight gradients: the ping-pong kernel's split-K factor is tuned like the
+                    # library's (fp32 slabs folded by slab_sum); uneven K slices, so any S that fills
+                    # the CUs (48 tiles x 5)
                     for S in (2, 3, 4, 5, 6, 8, 16):
                         if K % 64 == 0 and K // 64 >= S:
                             cands[f"pp_sk{S}"] = (lambda S=S: ours(IMPLS["pp"], scratch, S))
@@ -522,8 +526,6 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
             _tuned[key] = choice
         if isinstance(choice, tuple):
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
-        elif isinstance(choice, str) and choice.startswith("w4_sk"):
-            ours(IMPLS["w4"], sk=int(choice[5:]))
         elif isinstance(choice, str) and choice.startswith("pp_sk"):
             ours(IMPLS["pp"], sk=int(choice[5:]))
         elif isinstance(choice, str) and choice.startswith("lib_sk"):

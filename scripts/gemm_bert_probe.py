@@ -35,7 +35,7 @@ SHAPES = [
     ("wgrad", 1024, 4096, T, False, False, 24, True),
     ("wgrad", 30528, 1024, T, False, False, 1, True),
 ]
-IMP = {"pp": 6, "pp_nodma": 61, "w4q": 5, "w4q_nostore": 51, "w4q_nodma": 53, "w4q_nobar": 57, "w4q_samek": 59, "w4q_sc1": 71, "w4q_nt": 72, "w4q_ntsc1": 73, "w4q_sc0": 74, "w4q_glds": 82, "w4p": 4, "w4p_nostore": 40, "w4": 3, "k256": 2, "big": 1, "128": 0}
+IMP = {"pp": 6, "pp_nodma": 61, "k256": 2, "big": 1, "128": 0}
 dev = "cuda"
 X = Kn.ext()
 
@@ -47,7 +47,7 @@ def runner(impl, A, B, C, M, N, K, a_k, b_k):
         return lambda: Kn._lib_gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, N, 1.0, 0.0, None, 1, 0, 0, 0)
     if impl.startswith("lib_sk"):
         return lambda: Kn._lib_gemm_splitk(A, B, C, M, N, K, a_k, b_k, lda, ldb, 0.0, int(impl[6:]))
-    if "_sk" in impl:  # e.g. pp_sk4, w4_sk8: that kernel with a fixed split-K factor
+    if "_sk" in impl:  # e.g. pp_sk4: that kernel with a fixed split-K factor
         i = IMP[impl.split("_sk")[0]]
         sk = int(impl.split("_sk")[1])
     else:

@@ -21,7 +21,7 @@ C = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if out == "bf16" else tor
 lda = K if a_k else M
 ldb = K if b_k else N
 X = Kn.ext()
-IMP = {"pp": 6, "w4q": 5, "w4p": 4, "w4": 3, "k256": 2, "big": 1, "128": 0}.get(impl, 2)
+IMP = {"pp": 6, "k256": 2, "big": 1, "128": 0}.get(impl, 2)
 splitk = X.gemm_pick_splitk(M, N, K, 1, IMP)
 ws = torch.empty(M * N * splitk, device=dev) if splitk > 1 else None
 for _ in range(reps):

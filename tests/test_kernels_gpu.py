@@ -28,7 +28,7 @@ def _gemm(C_, A, B, C, M, N, K, a_k, b_k, bias=None, Z=None, alpha=1.0, beta=0.0
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 136, 72), (1024, 1024, 1024), (300, 1002, 1030),
                                    (130, 258, 4099), (4096, 1024, 256), (2056, 2000, 192)])
-@pytest.mark.parametrize("impl", [6, 5, 4, 3, 2, 1, 0])
+@pytest.mark.parametrize("impl", [6, 2, 1, 0])
 def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
     torch.manual_seed(0)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -44,10 +44,10 @@ def test_gemm_layouts(ffC, a_k, b_k, M, N, K, impl):
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(8192, 1024, 4096, 1), (8192, 3072, 1024, 2), (1024, 4096, 8192, 4),
                                           (1000, 600, 1056, 1), (2048, 2048, 2048, 3), (3072, 1024, 16384, 5)])
-@pytest.mark.parametrize("impl", [6, 5, 4, 3, 2])
+@pytest.mark.parametrize("impl", [6, 2])
 def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
-    """256-row kernels (3: 4-wave 256x256x64, 128x128 per wave; 2: 8-wave ping-pong): BERT-Large shapes,
-    split-K slabs, edge tiles."""
+    """256-row kernels (6: persistent 8-wave ping-pong, uneven split-K slices; 2: gemm256.hip):
+    BERT-Large shapes, split-K slabs, edge tiles."""
     torch.manual_seed(11)
     Am = torch.randn(M, K, device=DEV).bfloat16()
     Bn = torch.randn(N, K, device=DEV).bfloat16()
@@ -63,19 +63,18 @@ def test_gemm256_shapes(ffC, a_k, b_k, M, N, K, splitk, impl):
     assert _rel(C32, ref + 1.0) < 1e-3
 
 
-@pytest.mark.parametrize("impl", [4, 5, 6])
+@pytest.mark.parametrize("impl", [6])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 1024), (8200, 2056, 512), (16384, 1024, 256), (3000, 1000, 1152),
                                    (2048, 768, 128)])
 @pytest.mark.parametrize("out", ["bf16", "f32"])
 @pytest.mark.parametrize("bias", [None, "f32", "bf16"])
 def test_gemm_persistent(ffC, a_k, b_k, M, N, K, out, bias, impl):
-    """Persistent 4-wave GEMMs (impl 4, gemm_w4p.hip: two-slot BK = 64 ring; impl 5, gemm_w4q.hip:
-    four-slot BK = 32 ring, K = 128 being a tile of only the final K-group): several tiles per
-    workgroup, the next tile's DMA in flight during the epilogue, edge tiles (rows / columns dropped
-    by the buffer-store range check), bias in the epilogue, fp32 / bf16 output; five launches bitwise
-    equal (no race between the epilogue's staging image, the ring refill and the next tile's first
-    reads)."""
+    """Persistent ping-pong GEMM (impl 6, gemm_pp.hip: two wave groups alternating MFMA and memory
+    phases over a two-slot BK = 64 ring): several tiles per workgroup, the next tile's DMA in flight
+    during the epilogue, edge tiles (rows / columns dropped by the buffer-store range check), bias in
+    the epilogue, fp32 / bf16 output; five launches bitwise equal (no race between the epilogue's
+    staging image, the ring refill and the next tile's first reads)."""
     torch.manual_seed(5)
     Am = torch.randn(M, K, device=DEV).bfloat16()
     Bn = torch.randn(N, K, device=DEV).bfloat16()
@@ -98,7 +97,7 @@ def test_gemm_persistent(ffC, a_k, b_k, M, N, K, out, bias, impl):
         assert torch.equal(C, first)
 
 
-@pytest.mark.parametrize("impl", [3, 4, 5, 6])
+@pytest.mark.parametrize("impl", [6, 2])
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("M,N,K,splitk", [(512, 512, 512, 1), (512, 512, 512, 2), (1024, 768, 1024, 1)])
 def test_gemm_repeat_bitwise(ffC, impl, a_k, b_k, M, N, K, splitk):

@@ -10,7 +10,7 @@ def test_tune_cache_round_trip(tmp_path, monkeypatch):
     path = str(tmp_path / "tune.json")
     gkey = (16384, 1024, 4096, True, False, 4096, 1024, 1024, 1, torch.bfloat16, False, False, 10, False, None)
     ckey = ("fwd", (64, 64, 56, 56, 64, 56, 56, 3, 3, 1, 1, 1, 1, 1))
-    monkeypatch.setattr(K, "_tuned", {gkey: "w4_sk4", ("dact", 1, 2): "unfused", (1, 2, 3): ("lt", 7, 0)})
+    monkeypatch.setattr(K, "_tuned", {gkey: "pp_sk4", ("dact", 1, 2): "unfused", (1, 2, 3): ("lt", 7, 0)})
     monkeypatch.setattr(K, "_timed", {gkey, ("dact", 1, 2), (1, 2, 3), (9, 9)})
     monkeypatch.setattr(K, "_conv_tuned", {ckey: "ours"})
     monkeypatch.setattr(K, "_cached", {"gemm": {}, "conv": {}})
@@ -21,7 +21,7 @@ def test_tune_cache_round_trip(tmp_path, monkeypatch):
     monkeypatch.setattr(K, "_conv_tuned", {})
     monkeypatch.setattr(K, "_TUNE_CACHE", path)
     assert K.tune_cache_load(path) == 3
-    assert K._tune_cache_lookup("gemm", gkey) == "w4_sk4"
+    assert K._tune_cache_lookup("gemm", gkey) == "pp_sk4"
     assert K._tune_cache_lookup("gemm", ("dact", 1, 2)) == "unfused"
     assert K._tune_cache_lookup("conv", ckey) == "ours"
     assert K._tune_cache_lookup("gemm", (1, 2, 3)) is None
