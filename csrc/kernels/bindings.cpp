@@ -107,25 +107,55 @@ bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias,
   return true;
 }
 
-void box_copy(Tensor src, Tensor dst, Tensor desc, int64_t nbox, int64_t max_n, int64_t vec_bytes, bool add) {
-  check_dev(src, "src"); check_dev(dst, "dst"); check_dev(desc, "desc");
+void box_copy(std::vector<Tensor> srcs, Tensor dst, Tensor desc, int64_t nbox, int64_t max_n, int64_t vec_bytes,
+              bool add, bool idx32) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ffk::kBoxSrcs, "box_copy: 1..16 sources");
+  check_dev(dst, "dst"); check_dev(desc, "desc");
   TORCH_CHECK(desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.numel() >= nbox * ffk::box_words(),
               "box_copy: descriptors");
   TORCH_CHECK(nbox >= 0 && nbox <= 65535, "box_copy: at most 65535 boxes per launch");
-  TORCH_CHECK(src.scalar_type() == dst.scalar_type(), "box_copy: one dtype");
+  std::vector<const void*> ptrs;
+  for (auto& t : srcs) {
+    check_dev(t, "src");
+    TORCH_CHECK(t.scalar_type() == dst.scalar_type(), "box_copy: one dtype");
+    TORCH_CHECK(add || (reinterpret_cast<uintptr_t>(t.data_ptr()) % vec_bytes) == 0,
+                "box_copy: source not aligned to the vector width");
+    ptrs.push_back(t.data_ptr());
+  }
   int dt = 0;
   if (add) {
-    TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16, "box_copy add: fp32 / bf16");
-    dt = src.scalar_type() == at::kFloat ? ffk::DT_F32 : ffk::DT_BF16;
+    TORCH_CHECK(dst.scalar_type() == at::kFloat || dst.scalar_type() == at::kBFloat16, "box_copy add: fp32 / bf16");
+    dt = dst.scalar_type() == at::kFloat ? ffk::DT_F32 : ffk::DT_BF16;
   } else {
     TORCH_CHECK(vec_bytes == 1 || vec_bytes == 2 || vec_bytes == 4 || vec_bytes == 8 || vec_bytes == 16,
                 "box_copy: vector width");
-    TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) % vec_bytes) == 0 &&
-                    (reinterpret_cast<uintptr_t>(dst.data_ptr()) % vec_bytes) == 0,
-                "box_copy: pointers not aligned to the vector width");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(dst.data_ptr()) % vec_bytes) == 0,
+                "box_copy: destination not aligned to the vector width");
   }
-  ffk::box_copy(src.data_ptr(), dst.data_ptr(), desc.data_ptr<int64_t>(), (int)nbox, max_n, (int)vec_bytes,
-                add ? 1 : 0, dt, cur_stream());
+  ffk::box_copy(ptrs.data(), (int)ptrs.size(), dst.data_ptr(), desc.data_ptr<int64_t>(), (int)nbox, max_n,
+                (int)vec_bytes, add ? 1 : 0, dt, idx32 ? 1 : 0, cur_stream());
+}
+
+// x [.., xd, inner] and idx / out [.., dsz, inner], contiguous, other dims equal (checked by caller)
+void gather_fwd(Tensor x, Tensor idx, Tensor out, int64_t dsz, int64_t inner, int64_t xd) {
+  check_dev(x, "x"); check_dev(idx, "idx"); check_dev(out, "out");
+  TORCH_CHECK(x.is_contiguous() && idx.is_contiguous() && out.is_contiguous() && out.numel() == idx.numel() &&
+              out.scalar_type() == x.scalar_type(), "gather_fwd: contiguous x / idx / out");
+  TORCH_CHECK(idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong, "gather_fwd: int32 / int64 indices");
+  TORCH_CHECK(dsz > 0 && inner > 0 && xd > 0 && idx.numel() % (dsz * inner) == 0 &&
+              x.numel() == idx.numel() / dsz * xd, "gather_fwd: geometry");
+  ffk::gather_fwd(dtcode(x), idx.scalar_type() == at::kLong, x.data_ptr(), idx.data_ptr(), out.data_ptr(),
+                  idx.numel(), dsz, inner, xd, cur_stream());
+}
+void gather_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t dsz, int64_t inner, int64_t xd) {
+  check_dev(dy, "dy"); check_dev(idx, "idx"); check_dev(dx, "dx");
+  TORCH_CHECK(dy.is_contiguous() && idx.is_contiguous() && dx.is_contiguous() && dy.numel() == idx.numel() &&
+              dx.scalar_type() == at::kFloat, "gather_bwd: contiguous dy / idx, fp32 dx");
+  TORCH_CHECK(idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong, "gather_bwd: int32 / int64 indices");
+  TORCH_CHECK(dsz > 0 && inner > 0 && xd > 0 && idx.numel() % (dsz * inner) == 0 &&
+              dx.numel() == idx.numel() / dsz * xd, "gather_bwd: geometry");
+  ffk::gather_bwd(dtcode(dy), idx.scalar_type() == at::kLong, dy.data_ptr(), idx.data_ptr(), dx.data_ptr<float>(),
+                  idx.numel(), dsz, inner, xd, cur_stream());
 }
 
 int64_t gemm_pick_splitk(int64_t M, int64_t N, int64_t K, int64_t batch, int64_t impl) {
@@ -730,6 +760,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("act"), py::arg("splitk"), py::arg("ws"), py::arg("impl") = 2, py::arg("skip_reduce") = false);
   m.def("gemm_dact", &gemm_dact);
   m.def("box_copy", &box_copy);
+  m.def("gather_fwd", &gather_fwd);
+  m.def("gather_bwd", &gather_bwd);
   m.def("box_words", []() { return ffk::box_words(); });
   m.def("box_dims", []() { return ffk::box_dims(); });
   m.def("lstm_fwd_cell", &lstm_fwd_cell);

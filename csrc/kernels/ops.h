@@ -48,10 +48,15 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
 // transfer.hip: one launch over a list of boxes (pack / unpack / local re-layout of activation
 // shards); desc: device int64 [nbox][box_words()] (see transfer.hip), units of vec_bytes (copy)
 // or elements of dt (add: dst += src)
+void gather_fwd(int dt, int idx64, const void* x, const void* idx, void* out, int64_t n, int64_t dsz, int64_t inner,
+                int64_t xd, hipStream_t st);
+void gather_bwd(int dt, int idx64, const void* dy, const void* idx, float* dx, int64_t n, int64_t dsz, int64_t inner,
+                int64_t xd, hipStream_t st);
+constexpr int kBoxSrcs = 16;  // source tensors per launch
 int box_words();
 int box_dims();
-void box_copy(const void* src, void* dst, const int64_t* desc, int nbox, int64_t max_n, int vec_bytes, int add,
-              int dt, hipStream_t st);
+void box_copy(const void* const* srcs, int nsrc, void* dst, const int64_t* desc, int nbox, int64_t max_n,
+              int vec_bytes, int add, int dt, int idx32, hipStream_t st);
 
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
 // on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.

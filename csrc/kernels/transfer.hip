@@ -6,7 +6,8 @@
 // copies) and of concat_kernels.cu's per-input copies.
 //
 // A box is a rectangular region of up to kBoxDims dimensions with an element offset and strides on
-// each side (the flat side has contiguous strides). The host coalesces dimensions contiguous on
+// each side (the flat side has contiguous strides; a source stride may be negative: Reverse), read
+// from one of up to kBoxSrcs source tensors (Concat's inputs in one launch). The host coalesces dimensions contiguous on
 // both sides and picks the widest vector (16 / 8 / 4 / 2 / 1 bytes) that divides every inner run,
 // stride and offset, so a typical box is 1-3 dims of 16-B vectors. Descriptors live in a small
 // device array the host builds once per transfer plan (no per-call H2D copy: graph-capturable).
@@ -18,53 +19,60 @@ namespace ffk {
 
 namespace {
 
-// one box: [src_off, dst_off, numel, ext[kBoxDims], sstr[kBoxDims], dstr[kBoxDims]] (int64, in
-// units of the launch's vector), dims innermost last, leading unused dims with extent 1
+// one box: [src index, src_off, dst_off, numel, ext[kBoxDims], sstr[kBoxDims], dstr[kBoxDims]]
+// (int64, in units of the launch's vector), dims innermost last, leading unused dims with extent 1;
+// the source is one of up to kBoxSrcs tensors (a concat's inputs), passed by value per launch
 constexpr int kBoxDims = 6;
-constexpr int kBoxWords = 3 + 3 * kBoxDims;
+constexpr int kBoxWords = 4 + 3 * kBoxDims;
 
-template <typename V>
-__global__ void __launch_bounds__(256) box_copy_kernel(const V* __restrict__ src, V* __restrict__ dst,
-                                                       const int64_t* __restrict__ desc) {
-  const int64_t* d = desc + (int64_t)blockIdx.y * kBoxWords;
-  const int64_t n = d[2];
-  const int64_t* ext = d + 3;
+struct BoxSrcs {
+  const void* p[kBoxSrcs];
+};
+
+// IT: int32_t when every offset a launch reaches and every box size fit (the host checks): the
+// per-element index math is then 32-bit divisions (~10 VALU each instead of ~60 at 64 bits: the
+// 64-bit form made a channel-last concat of 2-B elements compute-bound)
+template <typename IT>
+__device__ __forceinline__ void box_index(const int64_t* d, IT e, IT& so, IT& dof) {
+  const int64_t* ext = d + 4;
   const int64_t* ss = ext + kBoxDims;
   const int64_t* ds = ss + kBoxDims;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
-    int64_t rem = e, so = d[0], dof = d[1];
+  IT rem = e;
+  so = (IT)d[1];
+  dof = (IT)d[2];
 #pragma unroll
-    for (int k = kBoxDims - 1; k >= 0; --k) {
-      const int64_t x = ext[k];
-      if (x == 1) continue;
-      const int64_t q = rem / x, c = rem - q * x;
-      so += c * ss[k];
-      dof += c * ds[k];
-      rem = q;
-    }
+  for (int k = kBoxDims - 1; k >= 0; --k) {
+    const IT x = (IT)ext[k];
+    if (x == 1) continue;
+    const IT q = rem / x, c = rem - q * x;
+    so += c * (IT)ss[k];
+    dof += c * (IT)ds[k];
+    rem = q;
+  }
+}
+
+template <typename V, typename IT>
+__global__ void __launch_bounds__(256) box_copy_kernel(BoxSrcs srcs, V* __restrict__ dst,
+                                                       const int64_t* __restrict__ desc) {
+  const int64_t* d = desc + (int64_t)blockIdx.y * kBoxWords;
+  const V* __restrict__ src = reinterpret_cast<const V*>(srcs.p[d[0]]);
+  const IT n = (IT)d[3];
+  for (IT e = (IT)blockIdx.x * 256 + (IT)threadIdx.x; e < n; e += (IT)gridDim.x * 256) {
+    IT so, dof;
+    box_index<IT>(d, e, so, dof);
     dst[dof] = src[so];
   }
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) box_add_kernel(const T* __restrict__ src, T* __restrict__ dst,
+__global__ void __launch_bounds__(256) box_add_kernel(BoxSrcs srcs, T* __restrict__ dst,
                                                       const int64_t* __restrict__ desc) {
   const int64_t* d = desc + (int64_t)blockIdx.y * kBoxWords;
-  const int64_t n = d[2];
-  const int64_t* ext = d + 3;
-  const int64_t* ss = ext + kBoxDims;
-  const int64_t* ds = ss + kBoxDims;
+  const T* __restrict__ src = reinterpret_cast<const T*>(srcs.p[d[0]]);
+  const int64_t n = d[3];
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
-    int64_t rem = e, so = d[0], dof = d[1];
-#pragma unroll
-    for (int k = kBoxDims - 1; k >= 0; --k) {
-      const int64_t x = ext[k];
-      if (x == 1) continue;
-      const int64_t q = rem / x, c = rem - q * x;
-      so += c * ss[k];
-      dof += c * ds[k];
-      rem = q;
-    }
+    int64_t so, dof;
+    box_index<int64_t>(d, e, so, dof);
     dst[dof] = Cvt<T>::from_f(Cvt<T>::to_f(dst[dof]) + Cvt<T>::to_f(src[so]));
   }
 }
@@ -76,36 +84,94 @@ int box_dims() { return kBoxDims; }
 
 // vec_bytes: 16 / 8 / 4 / 2 / 1 (copy) — the unit of every offset, extent and stride in desc;
 // add: dt (DT_F32 / DT_BF16), desc in elements. max_n: the largest box (units) — sizes the grid.
-void box_copy(const void* src, void* dst, const int64_t* desc, int nbox, int64_t max_n, int vec_bytes, int add,
-              int dt, hipStream_t st) {
-  if (nbox <= 0 || max_n <= 0) return;
+void box_copy(const void* const* srcs, int nsrc, void* dst, const int64_t* desc, int nbox, int64_t max_n,
+              int vec_bytes, int add, int dt, int idx32, hipStream_t st) {
+  if (nbox <= 0 || max_n <= 0 || nsrc <= 0 || nsrc > kBoxSrcs) return;
+  BoxSrcs s{};
+  for (int i = 0; i < nsrc; ++i) s.p[i] = srcs[i];
   const int64_t blocks = std::min<int64_t>((max_n + 255) / 256, std::max<int64_t>(1, 8192 / nbox));
   dim3 grid((unsigned)std::max<int64_t>(blocks, 1), (unsigned)nbox);
   if (add) {
-    if (dt == DT_F32)
-      hipLaunchKernelGGL(box_add_kernel<float>, grid, dim3(256), 0, st, (const float*)src, (float*)dst, desc);
-    else
-      hipLaunchKernelGGL(box_add_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)src, (bf16_t*)dst, desc);
+    if (dt == DT_F32) hipLaunchKernelGGL(box_add_kernel<float>, grid, dim3(256), 0, st, s, (float*)dst, desc);
+    else hipLaunchKernelGGL(box_add_kernel<bf16_t>, grid, dim3(256), 0, st, s, (bf16_t*)dst, desc);
     return;
   }
-  switch (vec_bytes) {
-    case 16:
-      hipLaunchKernelGGL(box_copy_kernel<uint4>, grid, dim3(256), 0, st, (const uint4*)src, (uint4*)dst, desc);
-      break;
-    case 8:
-      hipLaunchKernelGGL(box_copy_kernel<uint2>, grid, dim3(256), 0, st, (const uint2*)src, (uint2*)dst, desc);
-      break;
-    case 4:
-      hipLaunchKernelGGL(box_copy_kernel<uint32_t>, grid, dim3(256), 0, st, (const uint32_t*)src, (uint32_t*)dst,
-                         desc);
-      break;
-    case 2:
-      hipLaunchKernelGGL(box_copy_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)src, (uint16_t*)dst,
-                         desc);
-      break;
-    default:
-      hipLaunchKernelGGL(box_copy_kernel<uint8_t>, grid, dim3(256), 0, st, (const uint8_t*)src, (uint8_t*)dst, desc);
+  auto go = [&](auto vtag, auto itag) {
+    using V = decltype(vtag);
+    using IT = decltype(itag);
+    hipLaunchKernelGGL((box_copy_kernel<V, IT>), grid, dim3(256), 0, st, s, (V*)dst, desc);
+  };
+  auto by_width = [&](auto itag) {
+    switch (vec_bytes) {
+      case 16: go(uint4{}, itag); break;
+      case 8: go(uint2{}, itag); break;
+      case 4: go(uint32_t{}, itag); break;
+      case 2: go(uint16_t{}, itag); break;
+      default: go(uint8_t{}, itag);
+    }
+  };
+  if (idx32) by_width(int32_t{});
+  else by_width(int64_t{});
+}
+
+// ------------------------------------------------------------------------------- gather
+// torch.gather along one dim of contiguous tensors whose other dims match (reference
+// src/ops/gather.cc / kernels): out[o][j][i] = x[o][idx[o][j][i]][i]; the backward adds dy into an
+// fp32 dx at the same positions (float atomics: indices may repeat, as in the reference's
+// atomicAdd-based backward). Indices are clamped to the dim (an out-of-range index is a user
+// error torch would raise on; here it must not become an out-of-bounds access).
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) gather_fwd_kernel(const T* __restrict__ x, const I* __restrict__ idx,
+                                                         T* __restrict__ out, int64_t n, int64_t dsz, int64_t inner,
+                                                         int64_t xd) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int64_t o = e / (dsz * inner), i = e % inner;
+    int64_t k = (int64_t)idx[e];
+    k = k < 0 ? 0 : (k >= xd ? xd - 1 : k);
+    out[e] = x[(o * xd + k) * inner + i];
   }
+}
+
+template <typename T, typename I>
+__global__ void __launch_bounds__(256) gather_bwd_kernel(const T* __restrict__ dy, const I* __restrict__ idx,
+                                                         float* __restrict__ dx, int64_t n, int64_t dsz, int64_t inner,
+                                                         int64_t xd) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int64_t o = e / (dsz * inner), i = e % inner;
+    int64_t k = (int64_t)idx[e];
+    k = k < 0 ? 0 : (k >= xd ? xd - 1 : k);
+    atomicAdd(dx + (o * xd + k) * inner + i, Cvt<T>::to_f(dy[e]));
+  }
+}
+
+void gather_fwd(int dt, int idx64, const void* x, const void* idx, void* out, int64_t n, int64_t dsz, int64_t inner,
+                int64_t xd, hipStream_t st) {
+  if (n <= 0) return;
+  const dim3 grid(ew_grid(n, 256));
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    if (idx64) hipLaunchKernelGGL((gather_fwd_kernel<T, int64_t>), grid, dim3(256), 0, st, (const T*)x,
+                                  (const int64_t*)idx, (T*)out, n, dsz, inner, xd);
+    else hipLaunchKernelGGL((gather_fwd_kernel<T, int32_t>), grid, dim3(256), 0, st, (const T*)x, (const int32_t*)idx,
+                            (T*)out, n, dsz, inner, xd);
+  };
+  if (dt == DT_BF16) go(bf16_t{});
+  else go(float{});
+}
+
+void gather_bwd(int dt, int idx64, const void* dy, const void* idx, float* dx, int64_t n, int64_t dsz, int64_t inner,
+                int64_t xd, hipStream_t st) {
+  if (n <= 0) return;
+  const dim3 grid(ew_grid(n, 256));
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    if (idx64) hipLaunchKernelGGL((gather_bwd_kernel<T, int64_t>), grid, dim3(256), 0, st, (const T*)dy,
+                                  (const int64_t*)idx, dx, n, dsz, inner, xd);
+    else hipLaunchKernelGGL((gather_bwd_kernel<T, int32_t>), grid, dim3(256), 0, st, (const T*)dy,
+                            (const int32_t*)idx, dx, n, dsz, inner, xd);
+  };
+  if (dt == DT_BF16) go(bf16_t{});
+  else go(float{});
 }
 
 }  // namespace ffk

@@ -179,12 +179,19 @@ class Concat(OpImpl):
 
     def forward(self, ctx, xs, ws):
         ctx.saved["sizes"] = [x.shape[self.attrs["axis"]] for x in xs]
+        # the forward stays on torch.cat (one ATen launch) unless FF_BOX_CONCAT=1: the box-kernel
+        # concat measured 12.5 -> 12.9 ms per Inception-v3 b64 step (profiles/concat_box_ab_r5.txt)
+        if len(xs) > 1 and _box_ok(xs[0]) and os.environ.get("FF_BOX_CONCAT", "0") == "1" \
+                and all(x.dtype == xs[0].dtype for x in xs):
+            out = boxcopy.concat(self.__dict__.setdefault("_box_plans", {}), list(xs), self.attrs["axis"])
+            if out is not None:
+                return [out]
         return [torch.cat(xs, self.attrs["axis"])]
 
     def backward(self, ctx, douts):
         sizes = ctx.saved.pop("sizes")
         dy = douts[0]
-        if len(sizes) > 1 and boxcopy.available(dy) and os.environ.get("FF_BOX_SPLIT", "1") == "1":
+        if len(sizes) > 1 and _box_ok(dy) and os.environ.get("FF_BOX_SPLIT", "1") == "1":
             return _split_dense(self, dy, sizes, self.attrs["axis"])
         return list(torch.split(dy, sizes, self.attrs["axis"]))
 
@@ -195,36 +202,12 @@ def _split_dense(op, dy, sizes, ax):
     returns are strided along the split dim (a channel slice of an NHWC gradient), and every
     consumer made its own ATen copy of one: Inception-v3 paid ~23 copy launches per backward
     (reference concat_kernels.cu backward: one copy per input as well)."""
-    cl = dy.dim() == 4 and not dy.is_contiguous() and dy.is_contiguous(memory_format=torch.channels_last)
-    if not (cl or dy.is_contiguous()):
-        return list(torch.split(dy, sizes, ax))
-    flat = torch.empty(dy.numel(), dtype=dy.dtype, device=dy.device)
-    outs, boxes, off, lo = [], [], 0, 0
-    for n in sizes:
-        shp = list(dy.shape)
-        shp[ax] = n
-        if cl:  # NHWC strides of an [N, C, H, W] tensor
-            N_, C_, H_, W_ = shp
-            st = (H_ * W_ * C_, 1, W_ * C_, C_)
-        else:
-            st, acc = [], 1
-            for e in reversed(shp):
-                st.append(acc)
-                acc *= e
-            st = tuple(reversed(st))
-        outs.append(flat.as_strided(shp, st, off))
-        rel = [(0, e) for e in dy.shape]
-        rel[ax] = (lo, lo + n)
-        so, ss, ext = boxcopy.region_box(dy, rel)
-        boxes.append((so, ss, off, st, ext))
-        off += math.prod(shp)
-        lo += n
-    plans = op.__dict__.setdefault("_split_plans", {})
-    key = boxcopy.plan_key("split", dy, flat) + (tuple(sizes), ax)
-    if key not in plans:
-        plans[key] = boxcopy.BoxPlan(boxes, dy, flat)
-    plans[key].run(dy, flat)
-    return outs
+    outs = boxcopy.split_dense(op.__dict__.setdefault("_box_plans", {}), dy, sizes, ax)
+    return outs if outs is not None else list(torch.split(dy, sizes, ax))
+
+
+def _box_ok(t) -> bool:
+    return boxcopy.available(t) and os.environ.get("FF_BOX_SHAPE", "1") == "1"
 
 
 @register(OperatorType.OP_SPLIT)
@@ -261,6 +244,11 @@ class Split(OpImpl):
         return [tuple(range(n)) for _ in self.layer.outputs]
 
     def forward(self, ctx, xs, ws):
+        if len(self.attrs["sizes"]) > 1 and _box_ok(xs[0]):
+            outs = boxcopy.split_dense(self.__dict__.setdefault("_box_plans", {}), xs[0], self.attrs["sizes"],
+                                       self.attrs["axis"])
+            if outs is not None:
+                return outs
         return [K.dense(t) for t in torch.split(xs[0], self.attrs["sizes"], self.attrs["axis"])]
 
     def backward(self, ctx, douts):
@@ -272,6 +260,10 @@ class Split(OpImpl):
                 shp[self.attrs["axis"]] = s
                 d = torch.zeros(shp, dtype=like.dtype, device=like.device)
             parts.append(d)
+        if len(parts) > 1 and _box_ok(parts[0]) and all(p.dtype == parts[0].dtype for p in parts):
+            out = boxcopy.concat(self.__dict__.setdefault("_box_plans", {}), parts, self.attrs["axis"])
+            if out is not None:
+                return [out]
         return [torch.cat(parts, self.attrs["axis"])]
 
 
@@ -287,11 +279,17 @@ class Reverse(OpImpl):
     def supports_axis(self, axis):
         return axis != self.attrs["axis"] % len(self.layer.outputs[0].dims)
 
+    def _flip(self, t):
+        ax = self.attrs["axis"] % t.dim()
+        if _box_ok(t):  # one box-copy launch walking the source backwards along the axis
+            return boxcopy.reverse(self.__dict__.setdefault("_box_plans", {}), t, ax)
+        return torch.flip(t, [ax])
+
     def forward(self, ctx, xs, ws):
-        return [torch.flip(xs[0], [self.attrs["axis"]])]
+        return [self._flip(xs[0])]
 
     def backward(self, ctx, douts):
-        return [torch.flip(douts[0], [self.attrs["axis"]])]
+        return [self._flip(douts[0])]
 
 
 @register(OperatorType.OP_GATHER)
@@ -316,16 +314,37 @@ class Gather(OpImpl):
         n = len(self.layer.outputs[0].dims)
         return [(0,) + (None,) * (len(self.layer.inputs[0].dims) - 1), (0,) + (None,) * (n - 1)]
 
+    def _geom(self, shape, dtype, on_gpu, idx):
+        """(dsz, inner, xd) for the HIP kernels (transfer.hip), or None: a bf16 / fp32 x on the GPU,
+        int32 / int64 indices, every dim but `dim` equal between x and idx."""
+        n = len(shape)
+        d = self.attrs["dim"] % n
+        if not (on_gpu and dtype in (torch.bfloat16, torch.float32) and idx.dtype in (torch.int32, torch.int64)
+                and idx.dim() == n and all(shape[k] == idx.shape[k] for k in range(n) if k != d)):
+            return None
+        g = (idx.shape[d], math.prod(shape[d + 1:]), shape[d])
+        return g if min(g) > 0 else None
+
     def forward(self, ctx, xs, ws):
         x, idx = xs
         ctx.saved.update(shape=x.shape, idx=idx)
+        g = self._geom(tuple(x.shape), x.dtype, x.is_cuda, idx)
+        if g is not None:
+            out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
+            K.ext().gather_fwd(x.contiguous(), idx.contiguous(), out, *g)
+            return [out]
         return [torch.gather(x, self.attrs["dim"], idx.long())]
 
     def backward(self, ctx, douts):
         shp, idx = ctx.saved.pop("shape"), ctx.saved.pop("idx")
-        dx = torch.zeros(shp, dtype=torch.float32, device=douts[0].device)
-        dx.scatter_add_(self.attrs["dim"], idx.long(), douts[0].float())
-        return [dx.to(douts[0].dtype), None]
+        dy = douts[0]
+        dx = torch.zeros(shp, dtype=torch.float32, device=dy.device)
+        g = self._geom(tuple(shp), dy.dtype, dy.is_cuda, idx)
+        if g is not None:  # fp32 atomics into dx (repeated indices), then one cast
+            K.ext().gather_bwd(dy.contiguous(), idx.contiguous(), dx, *g)
+        else:
+            dx.scatter_add_(self.attrs["dim"], idx.long(), dy.float())
+        return [dx.to(dy.dtype), None]
 
     def needs_input_grad(self, i):
         return i == 0

@@ -88,3 +88,51 @@ def test_out_of_range_box_is_refused_on_the_host():
     flat = torch.zeros(16, device=DEV)
     with pytest.raises(ValueError):
         boxcopy.BoxPlan([(0, (8, 1), 0, (8, 1), (3, 8))], x, flat)  # 24 elements into 16
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+def test_concat_split_reverse_match_torch(dtype, cl):
+    """Concat (one launch over up to 16 inputs, more in groups), dense Split and Reverse on the
+    box kernel against torch.cat / torch.split / torch.flip."""
+    torch.manual_seed(2)
+    fmt = torch.channels_last if cl else torch.contiguous_format
+    xs = [torch.randn(4, c, 5, 6, device=DEV).to(dtype).contiguous(memory_format=fmt) for c in (8, 16, 24, 8)]
+    cache = {}
+    out = boxcopy.concat(cache, xs, 1)
+    assert torch.equal(out, torch.cat(xs, 1))
+    assert out.is_contiguous(memory_format=fmt)
+    many = [torch.randn(3, 8, device=DEV).to(dtype) for _ in range(37)]
+    assert torch.equal(boxcopy.concat(cache, many, 1), torch.cat(many, 1))
+    # rows of 5 elements do not vectorize: the caller keeps torch.cat
+    assert boxcopy.concat(cache, [torch.randn(3, 5, device=DEV).to(dtype)] * 2, 1) is None
+    parts = boxcopy.split_dense(cache, out, [8, 16, 24, 8], 1)
+    for p, r in zip(parts, xs):
+        assert torch.equal(p, r)
+    for ax in range(4):
+        assert torch.equal(boxcopy.reverse(cache, out, ax), torch.flip(out, [ax]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("itype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("dim", [0, 1, 2])
+def test_gather_kernels_match_torch(ffC, dtype, itype, dim):
+    """transfer.hip gather forward and its scatter-add backward against torch.gather / scatter_add_
+    (fp32 reference), repeated indices included."""
+    torch.manual_seed(3)
+    shp = [6, 7, 9]
+    x = torch.randn(shp, device=DEV).to(dtype)
+    ishp = list(shp)
+    ishp[dim] = 5
+    idx = torch.randint(0, shp[dim], ishp, device=DEV, dtype=itype)
+    inner = 1
+    for e in shp[dim + 1:]:
+        inner *= e
+    out = torch.empty(ishp, device=DEV, dtype=dtype)
+    ffC.gather_fwd(x, idx, out, ishp[dim], inner, shp[dim])
+    assert torch.equal(out, torch.gather(x, dim, idx.long()))
+    dy = torch.randn(ishp, device=DEV).to(dtype)
+    dx = torch.zeros(shp, device=DEV)
+    ffC.gather_bwd(dy, idx, dx, ishp[dim], inner, shp[dim])
+    ref = torch.zeros(shp, device=DEV).scatter_add_(dim, idx.long(), dy.float())
+    assert torch.allclose(dx, ref, atol=1e-5, rtol=1e-5)
