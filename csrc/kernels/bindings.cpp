@@ -731,7 +731,8 @@ void conv2d_fwd(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor ws, 
                   cur_stream(), ptr(wpack_bwd));
 }
 void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Tensor> dw, Tensor ws,
-                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc, bool accum_dx, optional<Tensor> wpack) {
+                std::vector<int64_t> g, bool x_nhwc, bool dy_nhwc, bool accum_dx, optional<Tensor> wpack,
+                optional<Tensor> dmask, optional<Tensor> dpart) {
   check_dev(x, "x");
   const auto gi = conv_geom(g);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv2d: bf16 tensors");
@@ -746,8 +747,21 @@ void conv2d_bwd(Tensor x, Tensor w, Tensor dy, optional<Tensor> dx, optional<Ten
   TORCH_CHECK(ws.numel() * ws.element_size() >= 2 * conv_ws(g), "conv2d_bwd: workspace too small");
   TORCH_CHECK(!wpack.has_value() || (wpack->scalar_type() == at::kBFloat16 && wpack->numel() >= conv_wpack(g)),
               "conv2d_bwd: wpack");
+  if (dmask.has_value()) {  // the producer's channel-last output, x's geometry; the partial slab
+    TORCH_CHECK(x_nhwc && dx.has_value() && !accum_dx && (g[1] / g[13]) % 8 == 0, "conv2d_bwd dmask: channel-last dx");
+    TORCH_CHECK(dmask->scalar_type() == at::kBFloat16 && dmask->numel() == x.numel(), "conv2d_bwd dmask: x's size");
+    check_layout(*dmask, true, g[1] / g[13], "conv2d_bwd dmask");
+    TORCH_CHECK(!dpart.has_value() || (dpart->scalar_type() == at::kFloat && dpart->is_contiguous() &&
+                                        dpart->numel() >= ffk::conv_dact_rows(gi.data()) * g[1]),
+                "conv2d_bwd dpart: rows x C fp32");
+  }
   ffk::conv2d_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), ptr(dx), ptr<float>(dw), ws.data_ptr(), gi.data(),
-                  dx.has_value(), x_nhwc, dy_nhwc, accum_dx && dx.has_value(), cur_stream(), ptr(wpack));
+                  dx.has_value(), x_nhwc, dy_nhwc, accum_dx && dx.has_value(), cur_stream(), ptr(wpack),
+                  dmask.has_value() ? dmask->data_ptr() : nullptr, dmask.has_value() ? ptr<float>(dpart) : nullptr);
+}
+int64_t conv_dact_rows(std::vector<int64_t> g) {
+  const auto gi = conv_geom(g);
+  return ffk::conv_dact_rows(gi.data());
 }
 
 }  // namespace
@@ -850,5 +864,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_ws", &conv_ws);
   m.def("conv_wpack", &conv_wpack);
   m.def("conv2d_fwd", &conv2d_fwd);
-  m.def("conv2d_bwd", &conv2d_bwd);
+  m.def("conv2d_bwd", &conv2d_bwd, py::arg("x"), py::arg("w"), py::arg("dy"), py::arg("dx"), py::arg("dw"),
+        py::arg("ws"), py::arg("g"), py::arg("x_nhwc"), py::arg("dy_nhwc"), py::arg("accum_dx"), py::arg("wpack"),
+        py::arg("dmask") = py::none(), py::arg("dpart") = py::none());
+  m.def("conv_dact_rows", &conv_dact_rows);
 }

@@ -130,6 +130,13 @@ struct IGemmArgs {
   int out_nhwc;      // channel-last output (M % 8 == 0)
   int accum;         // add into the existing output (a gradient summed over several consumers)
   int nph;           // backward-data by stride phase (sh * sw sub-GEMMs, grid z = G * nph); 0 / 1: off
+  // backward-data of a convolution whose input came from a bias + ReLU convolution (its only
+  // consumer): the epilogue writes that producer's pre-activation gradient dx * (y > 0) (dmask = its
+  // channel-last output y) and adds the per-channel sums of it into row (phase * gridDim.x +
+  // blockIdx.x) of dpart ([rows][G * M] fp32, zeroed by the host), folded into the producer's bias
+  // gradient afterwards (Executor._plan_dact_fusion; the producer skips its own mask + sum pass)
+  const bf16_t* dmask = nullptr;
+  float* dpart = nullptr;
 };
 
 // Column -> output pixel of the implicit GEMMs: the identity, or (stride-phase backward-data) the
@@ -157,6 +164,22 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   if (a.out_nhwc) {
+    const int64_t ldo = (int64_t)a.G * a.M;
+    constexpr int ITERS = BN * (BM / 8) / 256;
+    static_assert(ITERS * 256 == BN * (BM / 8), "whole store passes");
+    // the producer's outputs for every chunk this thread stores, all requested up front (one
+    // dependent global load per pass exposed its latency 8 times per tile)
+    uint4 ym[ITERS];
+    if (a.dmask) {
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int k = tid + 256 * it, px = k / (BM / 8), c = k % (BM / 8);
+        const int64_t p = p0 + px;
+        const int m = m0 + c * 8;
+        ym[it] = (p < P && m < a.M) ? *reinterpret_cast<const uint4*>(a.dmask + pix(p) * ldo + (int64_t)g * a.M + m)
+                                    : make_uint4(0, 0, 0, 0);
+      }
+    }
     // stage the tile as [pixel][channel] in LDS (the K loop's buffers are free after its last
     // barrier), then store whole 16-B channel chunks: a pixel's BM channels are one contiguous run
     // of the channel-last output, consecutive lanes on consecutive chunks. The lane's bias values
@@ -197,14 +220,31 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)
       }
     }
     __syncthreads();
-    const int64_t ldo = (int64_t)a.G * a.M;
-    for (int k = tid; k < BN * (BM / 8); k += 256) {
+    // dact: this thread's 8 channels (chunk c = tid % (BM / 8): 256 is a multiple of BM / 8, so c
+    // is fixed across the loop) summed over the pixels it stores
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int k = tid + 256 * it;
       const int px = k / (BM / 8), c = k % (BM / 8);
       const int64_t p = p0 + px;
       const int m = m0 + c * 8;
       if (p < P && m < a.M) {
-        uint4* dst = reinterpret_cast<uint4*>(a.out + pix(p) * ldo + (int64_t)g * a.M + m);
+        const int64_t eoff = pix(p) * ldo + (int64_t)g * a.M + m;
+        uint4* dst = reinterpret_cast<uint4*>(a.out + eoff);
         uint4 v = *reinterpret_cast<const uint4*>(smem + px * RS + c * 16);
+        if (a.dmask) {  // the producer's ReLU: keep the gradient where its output was positive
+          const uint4 yv = ym[it];
+          const uint32_t* yw = reinterpret_cast<const uint32_t*>(&yv);
+          uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool lo_on = bf2f((bf16_t)(yw[q] & 0xffff)) > 0.f, hi_on = bf2f((bf16_t)(yw[q] >> 16)) > 0.f;
+            vw[q] = (lo_on ? (vw[q] & 0xffffu) : 0u) | (hi_on ? (vw[q] & 0xffff0000u) : 0u);
+            csum[2 * q] += bf2f((bf16_t)(vw[q] & 0xffff));
+            csum[2 * q + 1] += bf2f((bf16_t)(vw[q] >> 16));
+          }
+        }
         if (a.accum) {  // fp32 sum of the staged value and the existing gradient, one rounding
           const uint4 o = *dst;
           const uint32_t* ow = reinterpret_cast<const uint32_t*>(&o);
@@ -217,6 +257,25 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x16 (&acc)
           }
         }
         *dst = v;
+      }
+    }
+    if (a.dpart) {
+      // fold the 256 / (BM / 8) threads that share a chunk through LDS, then one thread per
+      // channel adds the workgroup's partial into its slab row
+      constexpr int CPT = BM / 8, TPC = 256 / CPT;
+      __syncthreads();  // every thread is done reading the staged tile
+      float* red = reinterpret_cast<float*>(smem);  // [TPC][BM]
+      const int c = tid % CPT, t = tid / CPT;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[t * BM + c * 8 + e] = csum[e];
+      __syncthreads();
+      if (tid < BM) {
+        float sum = 0.f;
+        for (int q = 0; q < TPC; ++q) sum += red[q * BM + tid];
+        const int m = m0 + tid;
+        constexpr bool kPhase = std::is_same<PixMap, PhasePix>::value;
+        const int row = (kPhase ? (int)(blockIdx.z % a.nph) * (int)gridDim.x : 0) + (int)blockIdx.x;
+        if (m < a.M) a.dpart[(int64_t)row * ldo + (int64_t)g * a.M + m] = sum;
       }
     }
     return;
@@ -1097,8 +1156,17 @@ void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* w
   launch_igemm<false>(a, (int64_t)N * OH * OW, Kg, G, st);
 }
 
+// rows of the dact partial slab conv2d_bwd writes (an upper bound over its tilings)
+int64_t conv_dact_rows(const int* geom) {
+  const int N = geom[0], H = geom[2], W = geom[3], sh = geom[9], sw = geom[10];
+  const int nph = conv_dgrad_phases() ? sh * sw : 1;
+  if (nph > 1) return (int64_t)nph * (((int64_t)N * ((H + sh - 1) / sh) * ((W + sw - 1) / sw) + 63) / 64);
+  return ((int64_t)N * H * W + 63) / 64;
+}
+
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
-                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st, const void* wpack) {
+                int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st, const void* wpack,
+                const void* dmask, float* dpart) {
   const int N = geom[0], C = geom[1], H = geom[2], W = geom[3], K = geom[4], OH = geom[5], OW = geom[6];
   const int KH = geom[7], KW = geom[8], sh = geom[9], sw = geom[10], ph = geom[11], pw = geom[12], G = geom[13];
   const int Cg = C / G, Kg = K / G, Cp = round8(Cg), Kgp = round8(Kg);
@@ -1120,6 +1188,11 @@ void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* d
                          (const bf16_t*)w, wp, G, Kg, Cg, KH, KW, Kp, 1, nullptr, 0);
     IGemmArgs a{wpack ? (const bf16_t*)wpack : wp, ysrc, (bf16_t*)dx, nullptr, N, G, Cg, Kp, OH, OW, Kgp, H, W, KH, KW, sh, sw, ph, pw, 0, x_nhwc,
                 accum_dx, conv_dgrad_phases() ? sh * sw : 1};
+    if (dmask && x_nhwc && !accum_dx && Cg % 8 == 0) {
+      a.dmask = (const bf16_t*)dmask;
+      a.dpart = dpart;
+      if (dpart) hipMemsetAsync(dpart, 0, conv_dact_rows(geom) * (int64_t)C * sizeof(float), st);
+    }
     launch_igemm<true>(a, (int64_t)N * H * W, Cg, G, st);
   }
   if (dw) {

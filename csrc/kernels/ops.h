@@ -175,8 +175,11 @@ int64_t conv_ws_elems(int N, int C, int H, int W, int K, int OH, int OW, int KH,
 int64_t conv_wpack_elems(int C, int K, int KH, int KW, int G);
 void conv2d_fwd(const void* x, const void* w, const void* bias, void* y, void* ws, const int* geom, int relu,
                 int x_nhwc, int y_nhwc, hipStream_t st, void* wpack_bwd = nullptr);
+// accum_dx: dx +=; dmask / dpart: fused producer ReLU mask + bias-gradient partials (conv.hip
+// IGemmArgs), dpart of conv_dact_rows(geom) x C floats
 void conv2d_bwd(const void* x, const void* w, const void* dy, void* dx, float* dw, void* ws, const int* geom,
                 int need_dx, int x_nhwc, int dy_nhwc, int accum_dx, hipStream_t st,
-                const void* wpack = nullptr);  // accum_dx: dx +=
+                const void* wpack = nullptr, const void* dmask = nullptr, float* dpart = nullptr);
+int64_t conv_dact_rows(const int* geom);
 
 }  // namespace ffk

@@ -1481,10 +1481,18 @@ def _nhwc_flag(t, c):
     return cl_ok(t, c) and is_nhwc(t)
 
 
-def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False, wpack=None):
+def _conv_ours_bwd(x, w, dy, g, dx_out, dw_out, accum_dx=False, wpack=None, dact=None):
+    """dact = (y_p, db_p): the dgrad epilogue applies the producer's ReLU (y_p > 0) and adds the
+    per-channel sums of the result into db_p (fp32, may be None) — see conv.hip IGemmArgs.dmask."""
     ws = torch.empty(ext().conv_ws(g), device=x.device, dtype=torch.bfloat16)
+    dmask = dpart = None
+    if dact is not None:
+        dmask = dact[0]
+        dpart = torch.empty(ext().conv_dact_rows(g) * g[1], device=x.device, dtype=torch.float32)
     ext().conv2d_bwd(x, w, dy, dx_out, dw_out, ws, g, _nhwc_flag(x, g[1] // g[13]), _nhwc_flag(dy, g[4] // g[13]),
-                     accum_dx, wpack)
+                     accum_dx, wpack, dmask, dpart)
+    if dact is not None and dact[1] is not None:
+        ext().col_reduce_add3(dpart, dact[1].view(-1), None, None, ext().conv_dact_rows(g), g[1])
 
 
 def _pointwise_gemm_ok(g, *ts):
@@ -1584,14 +1592,25 @@ def conv2d_fwd(x, w, b, stride, pad, groups, relu, bwd_pack=None):
     return _conv_lib_fwd(x, w, b, g, relu)
 
 
-def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None, wpack=None):
+def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None, wpack=None, dact=None):
     """Backward of conv2d_fwd for geometry g (conv_geometry): returns dx (or None) and adds the
     weight gradient into dw (fp32, shaped like w, may be None). dx_acc: an existing gradient of x
     that dx is added into (and returned): our dgrad kernel accumulates in its epilogue when dx_acc
     has x's memory layout, otherwise a separate add. wpack: the backward-data weight operand packed
-    by this step's forward (conv2d_fwd bwd_pack), used by our dgrad kernel instead of a pack pass."""
+    by this step's forward (conv2d_fwd bwd_pack), used by our dgrad kernel instead of a pack pass.
+    dact = (y_p, db_p): x came from a bias + ReLU convolution whose only consumer this is; the
+    returned dx is that producer's pre-activation gradient dx * (y_p > 0), and db_p (fp32, may be
+    None) gets its per-channel sums — in our dgrad kernel's epilogue when that kernel runs on
+    channel-last tensors, else by the separate mask + sum pass (Executor._plan_dact_fusion)."""
     if not need_dx:
         dx_acc = None
+    if dact is not None:
+        assert need_dx and dx_acc is None, "dact fusion needs a fresh dx"
+        fused = _conv2d_bwd_dact(x, w, dy, g, dw, wpack, dact)
+        if fused is not None:
+            return fused
+        dx = conv2d_bwd(x, w, dy, g, dw, need_dx, None, wpack)
+        return conv_bias_relu_bwd(dx, dact[0], dact[1])
     if native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16:
         x = cl_dense(x, cl_ok(x, g[1] // g[13]))
         dy = cl_dense(dy, cl_ok(dy, g[4] // g[13]))
@@ -1644,6 +1663,33 @@ def conv2d_bwd(x, w, dy, g, dw, need_dx, dx_acc=None, wpack=None):
     if dx_acc is not None:
         dx_acc.add_(dxo)
         return dx_acc
+    return dxo
+
+
+def _conv2d_bwd_dact(x, w, dy, g, dw, wpack, dact):
+    """The fused form of conv2d_bwd(dact=...) when our dgrad kernel serves this geometry on
+    channel-last x / y_p (the per-site pick chose "ours"); None otherwise."""
+    yp, dbp = dact
+    if not (native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
+        return None
+    cg = g[1] // g[13]
+    if cg % 8 or not (is_nhwc(x) and is_nhwc(yp)) or yp.shape != x.shape or yp.dtype != torch.bfloat16:
+        return None
+    if dbp is not None and (dbp.dtype != torch.float32 or dbp.numel() != g[1]):
+        return None
+    pick = _CONV_IMPL if _CONV_IMPL in ("ours", "lib") else _conv_tuned.get(("bwd", tuple(g) + (True, dw is not None, True)))
+    if pick != "ours":
+        return None  # not timed yet (the unfused step times it), or the GEMM / library form won
+    dy = cl_dense(dy, cl_ok(dy, g[4] // g[13]))
+    w = w.contiguous()
+    dxo = torch.empty_like(x)
+    if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.shape == w.shape:
+        _conv_ours_bwd(x, w, dy, g, dxo, dw, False, wpack, dact)
+    else:
+        dwo = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if dw is not None else None
+        _conv_ours_bwd(x, w, dy, g, dxo, dwo, False, wpack, dact)
+        if dw is not None:
+            dw.add_(dwo.view_as(dw))
     return dxo
 
 

@@ -165,17 +165,29 @@ class Conv2D(_Spatial):
                                                                         "wpack"))
         act = self.attrs.get("activation", ActiMode.AC_MODE_NONE)
         dy = douts[0].to(y.dtype)
-        if act not in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU):
-            dy = (dy.float() * K.act_grad_ref(z.float(), act.value)).to(y.dtype)
         db = ctx.wgrads[1] if (has_b and len(ctx.wgrads) > 1) else None
-        dz = K.conv_bias_relu_bwd(dy, y if act == ActiMode.AC_MODE_RELU else None, db)
+        if ctx.extra.get("dact_fused"):
+            # the consuming convolution's dgrad already applied this op's ReLU and summed its bias
+            # gradient (Executor._plan_dact_fusion): dy is the pre-activation gradient
+            dz = dy
+        else:
+            if act not in (ActiMode.AC_MODE_NONE, ActiMode.AC_MODE_RELU):
+                dy = (dy.float() * K.act_grad_ref(z.float(), act.value)).to(y.dtype)
+            dz = K.conv_bias_relu_bwd(dy, y if act == ActiMode.AC_MODE_RELU else None, db)
         kh, kw, sh, sw, ph, pw = self._kp()
         g = K.conv_geometry(xc, w, (sh, sw), pad, self.attrs.get("groups", 1))
         dw = ctx.wgrads[0] if ctx.wgrads else None
         acc = (ctx.extra.get("dx_accum") or {}).get(0)
         if acc is not None and tuple(xc.shape) != tuple(x_shape):
             acc = None  # attribute-parallel crop: dx is scattered into a fresh block below
-        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True), dx_acc=acc, wpack=wpack)
+        dact = None
+        src = ctx.extra.get("dact_src")  # (producer's ctx,): this op's dgrad applies its ReLU
+        if src is not None:
+            pctx = src[0]
+            pdb = pctx.wgrads[1] if (pctx.saved.get("has_b") and len(pctx.wgrads) > 1) else None
+            assert acc is None and tuple(xc.shape) == tuple(x_shape), "conv dact fusion needs a fresh, uncropped dx"
+            dact = (pctx.saved["y"], pdb)
+        dx = K.conv2d_bwd(xc, w, dz, g, dw, ctx.extra.get("need_dx0", True), dx_acc=acc, wpack=wpack, dact=dact)
         if dx is None:  # the input needs no gradient (the data, or a frozen producer)
             return [None]
         if tuple(dx.shape) != tuple(x_shape):  # attribute-parallel: scatter crop back into halo'd block

@@ -28,7 +28,7 @@ from ..ops import OpCtx, torch_dtype
 from ..parallel.comm import Communicator, GradBucketer, Transfer
 from ..parallel.layout import Layout, rel_slices
 from ..pcg.strategy import OpConfig, op_layouts
-from ..type import DataType, LossType, MetricsType, OperatorType
+from ..type import ActiMode, DataType, LossType, MetricsType, OperatorType
 from ..ops.elementwise import BINARY as _BINARY
 
 BINARY_OPS = frozenset(_BINARY.keys())
@@ -877,12 +877,31 @@ class Executor:
         prod = {o.guid: L for L in self.layers for o in L.outputs}
         out_guid = self.output_tensor.guid if self.output_tensor is not None else None
         n = 0
+        # Conv -> Conv fusion is opt-in (FF_CONV_DACT_FUSION=1): bench-neutral to slightly slower on
+        # Inception-v3 / ResNet-50 (profiles/conv_dact_ab_r5.txt) — most consumer dgrads there run
+        # as 1x1 GEMMs or MIOpen, which keep the separate mask pass, and the fused sites pay a slab
+        # clear and a fold launch
+        conv_ok = os.environ.get("FF_CONV_DACT_FUSION", "0") == "1"
         for L in self.layers:
-            if L.op_type != OperatorType.OP_LINEAR or L.name not in self.ctx or not self.layer_bwd.get(L.name):
+            if L.name not in self.ctx or not self.layer_bwd.get(L.name):
                 continue
-            t = L.inputs[0]
-            P = prod.get(t.guid)
-            if P is None or P.op_type != OperatorType.OP_LINEAR or P.name not in self.ctx or P.impl.act == K.ACT_NONE:
+            t = L.inputs[0] if L.inputs else None
+            P = prod.get(t.guid) if t is not None else None
+            if P is None or P.name not in self.ctx:
+                continue
+            if L.op_type == OperatorType.OP_LINEAR:
+                if P.op_type != OperatorType.OP_LINEAR or P.impl.act == K.ACT_NONE:
+                    continue
+            elif L.op_type == OperatorType.OP_CONV2D and conv_ok:
+                # Conv -> Conv: the consumer's dgrad epilogue applies the producer's ReLU and sums its
+                # bias gradient (conv.hip IGemmArgs.dmask); no spatial split on either side (a halo'd
+                # block's dx is cropped and scattered, not the producer's output layout)
+                if P.op_type != OperatorType.OP_CONV2D or \
+                        P.attrs.get("activation", ActiMode.AC_MODE_NONE) != ActiMode.AC_MODE_RELU:
+                    continue
+                if any(d > 1 for d in list(self.ctx[L.name].degrees)[2:4] + list(self.ctx[P.name].degrees)[2:4]):
+                    continue
+            else:
                 continue
             if consumers.get(t.guid, 0) != 1 or t.guid == out_guid or not self.layer_bwd.get(P.name):
                 continue
@@ -893,7 +912,7 @@ class Executor:
             pctx = self.ctx[P.name]
             if pctx.wgrads and len(pctx.wgrads) > 1 and pctx.wgrads[1].dtype != torch.float32:
                 continue
-            self.ctx[L.name].extra["dact_src"] = (pctx, P.impl.act)
+            self.ctx[L.name].extra["dact_src"] = (pctx, getattr(P.impl, "act", K.ACT_RELU))
             pctx.extra["dact_fused"] = True
             n += 1
         return n

@@ -312,3 +312,44 @@ def test_world1_rccl_step_graph_captures_collectives():
     assert not e["captured"] and e["all_reduce_calls"] >= 8 * e["buckets"], e
     np.testing.assert_allclose(g["w0"], e["w0"], rtol=2e-2, atol=2e-4)
     assert abs(g["wsum"] - e["wsum"]) <= 1e-3 * abs(e["wsum"])
+
+
+def _conv_chain_train(monkeypatch, fuse):
+    import numpy as np
+    from flexflow_amd.core import ActiMode, DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+    monkeypatch.setenv("FF_CONV_DACT_FUSION", "1" if fuse else "0")
+    cfg = FFConfig(["--dtype", "bf16", "--no-hip-graphs"])
+    B = 8
+    cfg.batch_size = B
+    ff = FFModel(cfg)
+    x = ff.create_tensor([B, 16, 20, 20], DataType.DT_FLOAT, name="x")
+    t = ff.conv2d(x, 32, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = ff.conv2d(t, 48, 3, 3, 2, 2, 1, 1, ActiMode.AC_MODE_RELU, name="c2")   # stride-phase dgrad
+    t = ff.conv2d(t, 64, 1, 7, 1, 1, 0, 3, ActiMode.AC_MODE_RELU, name="c3")
+    t = ff.conv2d(t, 32, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_NONE, name="c4")
+    t = ff.flat(t, name="f")
+    t = ff.dense(t, 10, name="d")
+    ff.softmax(t, name="sm")
+    ff.optimizer = SGDOptimizer(ff, 0.01)
+    ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+    rng = np.random.default_rng(0)
+    x.set_tensor(ff, rng.standard_normal((B, 16, 20, 20)).astype(np.float32))
+    ff.label_tensor.set_tensor(ff, rng.integers(0, 10, (B, 1)).astype(np.int32))
+    fused = sum(1 for c in ff.executor.ctx.values() if c.extra.get("dact_fused"))
+    for _ in range(4):  # the first backward tunes each site (unfused), later ones take the fused dgrad
+        ff.train_step()
+    torch.cuda.synchronize()
+    w = {L.name: [np.asarray(p.get_weights(ff), dtype=np.float32) for p in L.weights] for L in ff.layers if L.weights}
+    return fused, w
+
+
+def test_conv_dact_fusion_matches_unfused(monkeypatch):
+    """Conv -> Conv (Executor._plan_dact_fusion): the consumer's dgrad epilogue applies the
+    producer's ReLU and sums its bias gradient (conv.hip IGemmArgs.dmask / dpart) — four SGD steps
+    land where the separate mask + channel-sum pass does."""
+    nf, wf = _conv_chain_train(monkeypatch, True)
+    nu, wu = _conv_chain_train(monkeypatch, False)
+    assert nf == 3 and nu == 0, (nf, nu)
+    for name in wu:
+        for a, b in zip(wf[name], wu[name]):
+            np.testing.assert_allclose(a, b, rtol=2e-2, atol=2e-3, err_msg=name)
