@@ -99,14 +99,20 @@ __device__ __forceinline__ int opaque_lane() {
 // ~150 VGPRs into scratch, the spill traffic forced vmcnt(0) into every memory phase, and it was
 // numerically wrong in the last row pass; gemm_dact's impl-2 kernel and the library GEMM + pass
 // pair cover that op.)
-template <bool F32OUT>
-constexpr int epi_ops() { return (F32OUT ? 32 : 16) + 2; }
+// ACT (bf16 output only): activation in the epilogue, the pre-activation (z + bias) stored to Z in
+// the same pass (16 more stores; issued out of range when Z is null so the count stays fixed)
+template <bool F32OUT, bool ACT = false>
+constexpr int epi_ops() { return (F32OUT ? 32 : 16) + 2 + (ACT ? 16 : 0); }
 
-template <bool A_K, bool B_K, bool F32OUT, bool SPLIT>
+// ACTK: 0, or the activation (ACT_RELU / ACT_GELU) as a compile-time constant: one code path per
+// instantiation (a run-time switch over every activation cost ~10 more VGPR spills)
+template <bool A_K, bool B_K, bool F32OUT, bool SPLIT, int ACTK = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
-  constexpr int EPI = epi_ops<F32OUT>();
+  constexpr bool ACT = ACTK != 0;
+  constexpr int EPI = epi_ops<F32OUT, ACT>();
+  static_assert(!ACT || (!F32OUT && !SPLIT), "activation epilogue: bf16 output, no split-K");
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -320,6 +326,10 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   const int bsz = p.bias ? (p.bias_bf16 ? 2 : 4) : 0;
   __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias : p.A), (short)0, p.N * bsz, 0x00020000);
   const float alpha = p.alpha;
+  // ACT: the pre-activation store (same layout as C); a null Z gets an empty range (stores dropped)
+  __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(ACT && p.Z ? p.Z : p.C), (short)0,
+                                                                ACT && p.Z ? (int)min(c_bytes, (int64_t)0x7fffffff) : 0,
+                                                                0x00020000);
   // Epilogue through a wave-private fp32 staging image (16 rows x 64 columns, 4 KiB, outside the
   // ring): the accumulator layout puts 4 consecutive columns of one row in a lane, so direct 8-B
   // stores leave a wave as 16 scattered 32-B row pieces per instruction, store-issue bound at
@@ -392,6 +402,14 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           __builtin_amdgcn_raw_buffer_store_b128(o0, rc, off, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b128(o1, rc, in ? off + 16 : off, 0, 0);
         } else {
+          if constexpr (ACT) {
+            u32x4 zo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) zo[e] = (uint32_t)f2bf(x[2 * e]) | ((uint32_t)f2bf(x[2 * e + 1]) << 16);
+            __builtin_amdgcn_raw_buffer_store_b128(zo, rz, off, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = act_fwd(ACTK, x[e]);
+          }
           u32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (uint32_t)f2bf(x[2 * e]) | ((uint32_t)f2bf(x[2 * e + 1]) << 16);
@@ -476,12 +494,12 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   }
 }
 
-template <bool F32OUT, bool SPLIT>
+template <bool F32OUT, bool SPLIT, int ACTK = 0>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
-  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
 }  // namespace pp
@@ -490,7 +508,12 @@ static int g_pp_cus = 0;
 
 bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
   using namespace pp;
-  if (p.dact || p.Z || p.act != ACT_NONE) return false;
+  // activation epilogue (bias + act, optional pre-activation store): bf16 output, no split-K
+  const bool act = p.Z || p.act != ACT_NONE;
+  if (p.dact) return false;
+  if (act && (p.out_f32 || (p.act != ACT_NONE && p.act != ACT_RELU && p.act != ACT_GELU) || (p.splitk > 1 && p.ws) ||
+              ((uintptr_t)p.Z & 15)))
+    return false;
   const bool split = p.splitk > 1 && p.ws;
   if (split && (!p.out_f32 || p.bias || p.alpha != 1.f || p.K / BK < p.splitk ||
                 (int64_t)p.splitk * p.M * p.N * 4 > 0x7fffff00LL))
@@ -514,6 +537,9 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   dim3 grid(std::min(tiles, g_pp_cus));
   if (split) launch<true, true>(p, grid, stream, a_bytes, b_bytes);  // split-K: fp32 slabs only
   else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
+  else if (act && p.act == ACT_GELU) launch<false, false, ACT_GELU>(p, grid, stream, a_bytes, b_bytes);
+  else if (act && p.act == ACT_RELU) launch<false, false, ACT_RELU>(p, grid, stream, a_bytes, b_bytes);
+  else if (act) launch<false, false, ACT_NONE>(p, grid, stream, a_bytes, b_bytes);  // Z store, no activation
   else launch<false, false>(p, grid, stream, a_bytes, b_bytes);
   return true;
 }

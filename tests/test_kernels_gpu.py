@@ -1000,3 +1000,27 @@ def test_attention_f32_path(causal, fused):
     o = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v).reshape(48, 64)
     ref = (o @ W["o_weight"].reshape(64, 64).t() + W["o_bias"]).view(2, 24, 64)
     assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("act", [14, 11])  # GELU, RELU
+@pytest.mark.parametrize("M,N,K", [(16384, 4096, 1024), (1000, 1032, 256), (520, 264, 128)])
+def test_gemm_pp_activation_epilogue(ffC, M, N, K, act):
+    """Ping-pong GEMM (impl 6) with bias, activation and the pre-activation store in its epilogue
+    (the FFN1 forward of BERT: y = act(x W^T + b), z = x W^T + b) against fp32 torch; repeat bitwise."""
+    from flexflow_amd.kernels import act_ref
+    torch.manual_seed(8)
+    A = torch.randn(M, K, device=DEV).bfloat16()
+    B = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    zref = A.float() @ B.float().t() + bias.float()
+    yref = act_ref(zref.bfloat16().float(), act)
+    first = None
+    for _ in range(3):
+        C = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        Z = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        ffC.gemm(A, B, C, bias, Z, M, N, K, K, K, N, 0, 0, 0, 1, True, True, 1.0, 0.0, act, 1, None, 6)
+        if first is None:
+            first = (C.clone(), Z.clone())
+            assert _rel(Z, zref) < 1e-2 and _rel(C, yref) < 1e-2
+        else:
+            assert torch.equal(C, first[0]) and torch.equal(Z, first[1])
