@@ -18,6 +18,7 @@ struct AttnArgs {
   uint16_t* dv = nullptr; int64_t dv_sb = 0, dv_sh = 0, dv_ss = 0;
   float* dq_acc = nullptr;  // [ceil(Sk/128)][B*H][Sq][D] partials
   float* delta = nullptr;   // [B*H][Sq]
+  float* lse2 = nullptr;    // [B*H][Sq] lse * log2(e) (attn_bwd_pre_kernel)
   int B = 0, H = 0, Sq = 0, Sk = 0, D = 64;
   float scale = 1.f;
   int causal = 0;

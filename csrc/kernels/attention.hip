@@ -987,7 +987,10 @@ __global__ void attn_bwd_pre_kernel(AttnArgs a) {
   }
 #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (row < total && part == 0) a.delta[row] = s;
+  if (row < total && part == 0) {
+    a.delta[row] = s;
+    a.lse2[row] = a.lse[row] * LOG2E;  // the DMA backward reads lse in log2 units
+  }
 }
 
 // dS^T image [key][64 queries] (128-B rows): byte offset of (key row, query q), q % 4 == 0. The
@@ -1032,7 +1035,12 @@ __device__ __forceinline__ unsigned pack_bf2(float x, float y) {
 //    small batch x heads use one launch with per-key-block slabs + attn_dq_finish_kernel.
 //  * 1-D grid through xcd_remap: the key blocks of one (batch, head) share an XCD (and its L2 copy
 //    of Q / dO).
-template <int D, int NW, bool MASK, bool CHAIN>
+//  * KREG: the K^T fragments of the wave's dQ tile (constant over the query loop) are read from
+//    the K image once, before the loop, instead of twice per dQ MFMA — half the dQ stage's LDS reads.
+//  * DMA: the next Q / dO tile and its lse2 / delta rows go global -> LDS by buffer_load ... lds
+//    (no staging registers, no ds_write of the tile); vmcnt also counts stores, so the dQ tile's
+//    global stores are issued after the end-of-tile barrier, behind the wait for the DMA.
+template <int D, int NW, bool MASK, bool CHAIN, bool KREG = false, bool DMA = false>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, int nkb, int pass) {
   constexpr int NT = 64 * NW;
   constexpr int QT = 64;       // queries per loop step
@@ -1066,6 +1074,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
   const float* LSE = a.lse + (int64_t)bh * a.Sq;
   const float* DL = a.delta + (int64_t)bh * a.Sq;
   const float sl2 = a.scale * LOG2E;
+  static_assert(!DMA || NW >= 2 * (D / 32), "DMA defers one dQ tile per wave past the barrier");
+  // DMA: buffer resources over this (batch, head)'s Q / dO rows and lse2 / delta entries
+  const int qbytes = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sq - 1) * a.q_ss + D) * 2);
+  const int dbytes = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sq - 1) * a.do_ss + D) * 2);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, qbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc((void*)dO, (short)0, dbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.lse2 + (int64_t)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdl = __builtin_amdgcn_make_buffer_rsrc((void*)DL, (short)0, a.Sq * 4, 0x00020000);
   // chain: slab 0 carries the running dQ sum; otherwise one fp32 slab per key block
   const bool chain = CHAIN || nkb == 1;
   float* dq_part = a.dq_acc + (int64_t)(chain ? 0 : kblk) * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
@@ -1091,6 +1108,22 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
+  // KREG (one dQ tile per wave: NW >= NTILE): A-operand K^T fragments of this wave's (dt, key part)
+  constexpr int NTILE_ = 2 * (D / 32);
+  constexpr int KSPLIT_ = NW > NTILE_ ? NW / NTILE_ : 1;
+  constexpr int KS_PER_ = KB / 16 / KSPLIT_;
+  static_assert(!KREG || NW >= NTILE_, "KREG needs one dQ tile per wave");
+  bf16x8 kq[KREG ? KS_PER_ : 1];
+  if constexpr (KREG) {
+    const int G_ = lane >> 4, qi_ = (lane & 15) >> 2, pi_ = lane & 3;
+    const int dt = (wave % NTILE_) % (D / 32), part = KSPLIT_ > 1 ? wave / NTILE_ : 0;
+    const int cd = 32 * dt + 16 * (G_ & 1) + 4 * pi_;
+#pragma unroll
+    for (int i = 0; i < KS_PER_; ++i) {
+      const int kr = 16 * (part * KS_PER_ + i) + 8 * h + qi_;
+      kq[i] = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
+    }
+  }
 
   const int qt_begin = (MASK && a.causal) ? kb0 / QT : 0;
   const int nqt = (a.Sq + QT - 1) / QT;
@@ -1117,10 +1150,30 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
       reinterpret_cast<float*>(tb + 2 * QB)[QT + tid] = dl_r;
     }
   };
-  if (qt_begin < nqt) fetch(qt_begin);
-  __syncthreads();  // every wave has its V fragments: the tile buffers can be overwritten
-  if (qt_begin < nqt) stash(qt_begin);
-  __syncthreads();
+  // DMA: tile t's Q / dO image (the TileStage layout) and lse2 / delta rows into buffer t & 1;
+  // rows past Sq read as zero (range check), which makes their P x dO and dS x Q terms zero
+  auto dma_rows = [&](int t) {
+    char* tb = smem + (t & 1) * TILE;
+    dma_tile<D, NW>(rq, tb, a.q_ss, t * QT, wave, lane);
+    dma_tile<D, NW>(rdo, tb + QB, a.do_ss, t * QT, wave, lane);
+    if (wave == NW - 1) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_ptr_t)(tb + 2 * QB), 4, (t * QT + lane) * 4, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdl, (lds_ptr_t)(tb + 2 * QB + QT * 4), 4, (t * QT + lane) * 4, 0, 0, 0);
+    }
+  };
+  if constexpr (DMA) {
+    __syncthreads();  // every wave has its V fragments: the tile buffers can be overwritten
+    if (qt_begin < nqt) {
+      dma_rows(qt_begin);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  } else {
+    if (qt_begin < nqt) fetch(qt_begin);
+    __syncthreads();  // every wave has its V fragments: the tile buffers can be overwritten
+    if (qt_begin < nqt) stash(qt_begin);
+    __syncthreads();
+  }
 
   for (int t = qt_begin; t < nqt; ++t) {
     const int qbase = t * QT;
@@ -1130,7 +1183,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
     const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
     const float* dl_l = lse_l + QT;
     const bool more = t + 1 < nqt;
-    if (more) fetch(t + 1);  // in flight during this tile's MFMAs
+    if (more) {  // in flight during this tile's MFMAs
+      if constexpr (DMA) dma_rows(t + 1);  // buffer (t+1)&1: its readers finished before tile t-1's mid barrier
+      else fetch(t + 1);
+    }
     // chain, key block > 0: the previous launch's dQ running sum for this wave's dQ tile, requested
     // now so its HBM round trip runs under the tile's MFMAs (read at its use below, the load sat on
     // the workgroup's critical path once per query tile)
@@ -1207,44 +1263,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
       }
     }
     lds_barrier();
-    // dQ^T tile (d x query) = K^T . dS^T over this block's keys: wave -> (qt, dt) tiles (and, with
-    // KSPLIT > 1, a 1/KSPLIT slice of the keys); lane = query, rows = d (r&3) + 8(r>>2) + 4h
-    for (int tile = wave % NTILE; tile < NTILE; tile += (NW < NTILE ? NW : NTILE)) {
+    // the dQ tile's running-sum / final store (deferred past the end-of-tile barrier under DMA)
+    auto put_dq = [&](f32x16& acc, int tile, int part) {
       const int qt = tile / (D / 32), dt = tile % (D / 32);
-      const int part = KSPLIT > 1 ? wave / NTILE : 0;
-      constexpr int KS_PER = KB / 16 / KSPLIT;
-      f32x16 acc = f32x16{};
-#pragma unroll
-      for (int ks = part * KS_PER; ks < (part + 1) * KS_PER; ++ks) {
-        const int kr = 16 * ks + 8 * h + qi;
-        const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
-        const bf16x8 af = cat8(tr_read(ds_l, dst_off(kr, cq)), tr_read(ds_l, dst_off(kr + 4, cq)));
-        const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
-        const bf16x8 bk = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bk, af, acc, 0, 0, 0);
-      }
-      if constexpr (KSPLIT > 1) {
-        // parts 1.. park their partial in LDS (lane-major: conflict-free 16-B rows), part 0 adds
-        float* slot = dqx_l + ((part - 1) * NTILE + tile) * 1024;
-        if (part > 0) {
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4)
-            *reinterpret_cast<float4*>(slot + (r4 * 64 + lane) * 4) =
-                make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
-        }
-        lds_barrier();
-        if (part == 0) {
-#pragma unroll
-          for (int p2 = 1; p2 < KSPLIT; ++p2) {
-            const float* o = dqx_l + ((p2 - 1) * NTILE + tile) * 1024;
-#pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-              const float4 v = *reinterpret_cast<const float4*>(o + (r4 * 64 + lane) * 4);
-              acc[4 * r4] += v.x; acc[4 * r4 + 1] += v.y; acc[4 * r4 + 2] += v.z; acc[4 * r4 + 3] += v.w;
-            }
-          }
-        }
-      }
       const int q = qbase + 32 * qt + (lane & 31);
       if (part == 0 && (!MASK || q < a.Sq)) {
         float* prow = dq_part + (int64_t)q * D + 32 * dt + 4 * h;
@@ -1274,9 +1295,78 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
             *reinterpret_cast<float4*>(prow + 8 * g) = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
         }
       }
+    };
+    auto add_parts = [&](f32x16& acc, int tile) {
+#pragma unroll
+      for (int p2 = 1; p2 < KSPLIT; ++p2) {
+        const float* o = dqx_l + ((p2 - 1) * NTILE + tile) * 1024;
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const float4 v = *reinterpret_cast<const float4*>(o + (r4 * 64 + lane) * 4);
+          acc[4 * r4] += v.x; acc[4 * r4 + 1] += v.y; acc[4 * r4 + 2] += v.z; acc[4 * r4 + 3] += v.w;
+        }
+      }
+    };
+    f32x16 dq_keep;
+    int dq_tile = -1, dq_kpart = 0;
+    // dQ^T tile (d x query) = K^T . dS^T over this block's keys: wave -> (qt, dt) tiles (and, with
+    // KSPLIT > 1, a 1/KSPLIT slice of the keys); lane = query, rows = d (r&3) + 8(r>>2) + 4h
+    for (int tile = wave % NTILE; tile < NTILE; tile += (NW < NTILE ? NW : NTILE)) {
+      const int qt = tile / (D / 32), dt = tile % (D / 32);
+      const int part = KSPLIT > 1 ? wave / NTILE : 0;
+      constexpr int KS_PER = KB / 16 / KSPLIT;
+      f32x16 acc = f32x16{};
+      // fully unrolled the 16-step form (4 waves: one wave per tile) spilled 14 VGPRs
+#pragma unroll(KS_PER > 8 ? 4 : KS_PER)
+      for (int ks = part * KS_PER; ks < (part + 1) * KS_PER; ++ks) {
+        const int kr = 16 * ks + 8 * h + qi;
+        const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
+        const bf16x8 af = cat8(tr_read(ds_l, dst_off(kr, cq)), tr_read(ds_l, dst_off(kr + 4, cq)));
+        bf16x8 bk;
+        if constexpr (KREG) {
+          bk = kq[ks - part * KS_PER];
+        } else {
+          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
+          bk = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bk, af, acc, 0, 0, 0);
+      }
+      if constexpr (KSPLIT > 1) {
+        // parts 1.. park their partial in LDS (lane-major: conflict-free 16-B rows), part 0 adds
+        // (under DMA after the end-of-tile barrier, which then orders the exchange: one barrier less)
+        float* slot = dqx_l + ((part - 1) * NTILE + tile) * 1024;
+        if (part > 0) {
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<float4*>(slot + (r4 * 64 + lane) * 4) =
+                make_float4(acc[4 * r4], acc[4 * r4 + 1], acc[4 * r4 + 2], acc[4 * r4 + 3]);
+        }
+        if constexpr (!DMA) {
+          lds_barrier();
+          if (part == 0) add_parts(acc, tile);
+        }
+      }
+      if constexpr (DMA) {
+        dq_keep = acc;
+        dq_tile = tile;
+        dq_kpart = part;
+      } else {
+        put_dq(acc, tile, part);
+      }
     }
-    if (more) stash(t + 1);  // other buffer: its last readers finished before this tile's first sync
-    lds_barrier();           // tile t+1 visible; dS^T reads of tile t done before it is rewritten
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed (and older dQ stores done)
+      lds_barrier();
+      if (dq_tile >= 0) {
+        if constexpr (KSPLIT > 1) {
+          if (dq_kpart == 0) add_parts(dq_keep, dq_tile);
+        }
+        put_dq(dq_keep, dq_tile, dq_kpart);
+      }
+    } else {
+      if (more) stash(t + 1);  // other buffer: its last readers finished before this tile's first sync
+      lds_barrier();           // tile t+1 visible; dS^T reads of tile t done before it is rewritten
+    }
   }
   // slabs, causal: query tiles before qt_begin get nothing from this key block; zero its rows
   if (MASK && a.causal && !chain) {
@@ -1304,6 +1394,268 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
     bf16_t* dKb = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh;
     bf16_t* dVb = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh;
     constexpr int CPR = D / 8;  // 16-B chunks per row
+#pragma unroll
+    for (int i = 0; i < KB * CPR / NT; ++i) {
+      const int id = tid + i * NT, r = id / CPR, c = id % CPR;
+      const int off = r * (D * 2) + ((c ^ (r & 7)) << 4);
+      if (!MASK || kb0 + r < a.Sk) {
+        *reinterpret_cast<uint4*>(dKb + (int64_t)(kb0 + r) * a.dk_ss + 8 * c) = *reinterpret_cast<const uint4*>(k_l + off);
+        *reinterpret_cast<uint4*>(dVb + (int64_t)(kb0 + r) * a.dv_ss + 8 * c) = *reinterpret_cast<const uint4*>(dv_l + off);
+      }
+    }
+  }
+}
+
+// Backward, one barrier per query tile (variant 9; D = 64, 8 waves x 32 keys, LDS-DMA tiles):
+// attn_bwd_kernel software-pipelined over the query tiles. Iteration t computes S / dP / dV / dK
+// of tile t (its dS^T into one of two LDS images) and the dQ of tile t-1 from the other image, so
+// the one end-of-iteration barrier orders the tile buffers, both dS^T images and the DMA of tile
+// t+1 at once (attn_bwd_kernel: three barriers per tile, two with DMA), and a wave's dQ MFMAs do
+// not depend on its S / dP work of the same iteration. dQ^T runs on 16x16x32 MFMAs: 16 (d x query)
+// tiles of 16 x 16, two per wave sharing the K^T operand, each over all KB keys, so no wave hands
+// a partial sum to another (no exchange buffer: the second dS^T image takes its LDS).
+template <bool MASK, bool CHAIN, bool SB = false>
+__global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb, int pass) {
+  constexpr int D = 64, NW = 8, NT = 64 * NW, QT = 64, KB = 32 * NW, QB = QT * D * 2;
+  constexpr int TILE = 2 * QB + 2 * QT * 4;  // Q tile, dO tile, lse2, delta
+  constexpr int DS = KB * QT * 2;            // one dS^T image [KB][QT]
+  static_assert(2 * TILE >= KB * D * 2, "tile buffers stage the V block and the dV image");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + 2 * DS];
+  char* k_l = smem + 2 * TILE;
+  char* ds0 = k_l + KB * D * 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int groups = CHAIN ? 1 : nkb;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = lid / groups, b = bh / a.H, hh = bh % a.H;
+  const int kblk = CHAIN ? pass : lid % groups;
+  const int kb0 = kblk * KB;
+  const int key = kb0 + wave * 32 + (lane & 31);
+  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
+  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
+  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
+  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh;
+  const float* DL = a.delta + (int64_t)bh * a.Sq;
+  const float sl2 = a.scale * LOG2E;
+  const int qbytes = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sq - 1) * a.q_ss + D) * 2);
+  const int dbytes = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sq - 1) * a.do_ss + D) * 2);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, qbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdo = __builtin_amdgcn_make_buffer_rsrc((void*)dO, (short)0, dbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.lse2 + (int64_t)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdl = __builtin_amdgcn_make_buffer_rsrc((void*)DL, (short)0, a.Sq * 4, 0x00020000);
+  const bool chain = CHAIN || nkb == 1;
+  float* dq_part = a.dq_acc + (int64_t)(chain ? 0 : kblk) * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
+  bf16_t* dQb = a.dq + (int64_t)b * a.dq_sb + (int64_t)hh * a.dq_sh;
+
+  bf16x8 kf[D / 16], vf[D / 16];
+  {
+    TileStage<D, KB, NT> sk, sv;
+    sk.load(K, a.k_ss, kb0, MASK ? a.Sk : 1 << 30, tid);
+    sv.load(V, a.v_ss, kb0, MASK ? a.Sk : 1 << 30, tid);
+    sk.store(k_l, tid);
+    sv.store(smem, tid);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const int row = wave * 32 + (lane & 31);
+    kf[s] = *reinterpret_cast<const bf16x8*>(k_l + aoff<D>(row, 16 * s + 8 * h));
+    vf[s] = *reinterpret_cast<const bf16x8*>(smem + aoff<D>(row, 16 * s + 8 * h));
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
+
+  const int qt_begin = (MASK && a.causal) ? kb0 / QT : 0;
+  const int nqt = (a.Sq + QT - 1) / QT;
+  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3, l16 = lane & 15;
+  auto dma_rows = [&](int t) {
+    char* tb = smem + (t & 1) * TILE;
+    dma_tile<D, NW>(rq, tb, a.q_ss, t * QT, wave, lane);
+    dma_tile<D, NW>(rdo, tb + QB, a.do_ss, t * QT, wave, lane);
+    if (wave == NW - 1) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_ptr_t)(tb + 2 * QB), 4, (t * QT + lane) * 4, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdl, (lds_ptr_t)(tb + 2 * QB + QT * 4), 4, (t * QT + lane) * 4, 0, 0, 0);
+    }
+  };
+  __syncthreads();  // every wave has its V fragments: the tile buffers can be overwritten
+  if (qt_begin < nqt) {
+    dma_rows(qt_begin);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  // dQ^T mapping: rows d0 .. d0+15, query columns q0 + {0..15, 16..31} of the tile
+  const int dq_d0 = 16 * (wave & 3), dq_q0 = 32 * (wave >> 2);
+  f32x4 dqa[2];
+  float4 prevq[2];
+  // one iteration: S / dP / dV / dK of tile t (s_tile), dQ of tile t-1 (dq_tile); the first and
+  // last iterations are peeled so that the steady-state body is one basic block in which the
+  // scheduler can interleave the two independent halves
+  auto prefetch = [&](int t) {  // the previous launch's running sum of tile t-1's dQ
+    const int pq = (t - 1) * QT;
+    if (chain && kblk > 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = pq + dq_q0 + 16 * j + l16;
+        if (!MASK || q < a.Sq) prevq[j] = *reinterpret_cast<const float4*>(dq_part + (int64_t)q * D + dq_d0 + 4 * G);
+      }
+        }
+  };
+  // hook(stage): stage 2 qt after the S / dP MFMAs, 2 qt + 1 after the dV / dK MFMAs of half qt
+  auto s_tile = [&](int t, auto hook) {
+      const int qbase = t * QT;
+      const char* tb = smem + (t & 1) * TILE;
+      const char* q_l = tb;
+      const char* do_l = tb + QB;
+      const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
+      const float* dl_l = lse_l + QT;
+      char* ds_l = ds0 + (t & 1) * DS;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x16 sacc = f32x16{}, pacc = f32x16{};
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          const int row = 32 * qt + (lane & 31);
+          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
+          const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
+        }
+        hook(2 * qt);
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
+          const float lv[4] = {L4.x, L4.y, L4.z, L4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = fast_exp2(sacc[4 * g4 + j] * sl2 - lv[j]);
+        }
+        if (MASK) {
+          const bool need = (kb0 + wave * 32 + 31 >= a.Sk) || (a.causal && kb0 + wave * 32 + 31 > qbase + 32 * qt);
+          if (need) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (key >= a.Sk || (a.causal && key > q)) sacc[r] = 0.f;
+            }
+          }
+        }
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 D4 = *reinterpret_cast<const float4*>(dl_l + 32 * qt + 8 * g4 + 4 * h);
+          const float dv4[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pacc[4 * g4 + j] = sacc[4 * g4 + j] * (pacc[4 * g4 + j] - dv4[j]);
+        }
+        const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
+        const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
+            const bf16x8 ao = cat8(tr_read(do_l, aoff<D>(r0, col)), tr_read(do_l, aoff<D>(r0 + 8, col)));
+            const bf16x8 aq = cat8(tr_read(q_l, aoff<D>(r0, col)), tr_read(q_l, aoff<D>(r0 + 8, col)));
+            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, s2 ? pb1 : pb0, dv[dt], 0, 0, 0);
+            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, s2 ? sb1 : sb0, dk[dt], 0, 0, 0);
+          }
+        }
+        hook(2 * qt + 1);
+        const int krow = wave * 32 + (lane & 31);
+        const bf16x4 parts[4] = {sb0.lo, sb0.hi, sb1.lo, sb1.hi};
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(ds_l + dst_off(krow, 32 * qt + 8 * g + 4 * h)) = parts[g];
+      }
+      };
+  // dQ^T (16 d x 16 queries, two tiles) = K^T . dS^T of tile t-1 over key slices [32 k0, 32 k1)
+  auto dq_chunk = [&](int t, int k0, int k1) {
+      const char* dsl = ds0 + ((t - 1) & 1) * DS;
+      if (k0 == 0) dqa[0] = dqa[1] = f32x4{};
+#pragma unroll
+      for (int ks = k0; ks < k1; ++ks) {
+        const int kr = 32 * ks + 8 * G + qi;
+        const bf16x8 ka = cat8(tr_read(k_l, aoff<D>(kr, dq_d0 + 4 * pi)), tr_read(k_l, aoff<D>(kr + 4, dq_d0 + 4 * pi)));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int cq = dq_q0 + 16 * j + 4 * pi;
+          const bf16x8 sbq = cat8(tr_read(dsl, dst_off(kr, cq)), tr_read(dsl, dst_off(kr + 4, cq)));
+          dqa[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, sbq, dqa[j], 0, 0, 0);
+        }
+      }
+      };
+  auto dq_tile = [&](int t) { dq_chunk(t, 0, KB / 32); };
+  auto dq_store = [&](int t) {  // after the barrier: vmcnt counts stores, the next wait is a tile away
+    const int pq = (t - 1) * QT;
+      int last = nkb - 1;
+      if (MASK && a.causal) last = min(last, (pq + QT - 1) / KB);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = pq + dq_q0 + 16 * j + l16;
+        if (!MASK || q < a.Sq) {
+          f32x4 acc = dqa[j];
+          if (chain && kblk > 0) {
+            acc[0] += prevq[j].x; acc[1] += prevq[j].y; acc[2] += prevq[j].z; acc[3] += prevq[j].w;
+          }
+          if (chain && kblk == last) {
+            *reinterpret_cast<uint2*>(dQb + (int64_t)q * a.dq_ss + dq_d0 + 4 * G) =
+                make_uint2(pack_bf2(acc[0] * a.scale, acc[1] * a.scale), pack_bf2(acc[2] * a.scale, acc[3] * a.scale));
+          } else {
+            *reinterpret_cast<float4*>(dq_part + (int64_t)q * D + dq_d0 + 4 * G) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          }
+        }
+      }
+      };
+  auto finish = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed; older dQ stores done
+    lds_barrier();
+  };
+  if (qt_begin < nqt) {
+    if (qt_begin + 1 < nqt) dma_rows(qt_begin + 1);
+    s_tile(qt_begin, [](int) {});
+    finish();
+    for (int t = qt_begin + 1; t < nqt; ++t) {
+      if (t + 1 < nqt) dma_rows(t + 1);  // buffer (t+1)&1: read during iteration t-1, before its barrier
+      prefetch(t);
+      // tile t-1's dQ in four key-slice chunks between the S / dP and dV / dK stages of tile t
+      s_tile(t, [&](int st) {
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+        dq_chunk(t, 2 * st, 2 * st + 2);
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+      });
+      finish();
+      dq_store(t);
+    }
+    prefetch(nqt);
+    dq_tile(nqt);
+    finish();
+    dq_store(nqt);
+  }
+  if (MASK && a.causal && !chain) {
+    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
+  }
+  if (qt_begin >= nqt) __syncthreads();
+  {
+    char* dv_l = smem;
+    const int row = wave * 32 + (lane & 31);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 4 * dt + g;
+        const int off = row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h;
+        *reinterpret_cast<uint2*>(k_l + off) = make_uint2(pack_bf2(dk[dt][4 * g] * a.scale, dk[dt][4 * g + 1] * a.scale),
+                                                          pack_bf2(dk[dt][4 * g + 2] * a.scale, dk[dt][4 * g + 3] * a.scale));
+        *reinterpret_cast<uint2*>(dv_l + off) = make_uint2(pack_bf2(dv[dt][4 * g], dv[dt][4 * g + 1]),
+                                                           pack_bf2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
+      }
+    }
+    lds_barrier();
+    bf16_t* dKb = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh;
+    bf16_t* dVb = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh;
+    constexpr int CPR = D / 8;
 #pragma unroll
     for (int i = 0; i < KB * CPR / NT; ++i) {
       const int id = tid + i * NT, r = id / CPR, c = id % CPR;
@@ -1578,13 +1930,19 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
 // one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64); 2 (default) =
 // attn_bwd_kernel with 8 waves x 32 keys at D = 64 (4 at D = 128), chained launches when B*H
 // workgroups fill the chip (>= 256) or there is one key block, else slabs; 3 = variant 2 always
-// chained; 4 = variant 2 always with slabs. Settable for A/B runs in one process
+// chained; 4 = variant 2 always with slabs; 5 = 4 waves x 32 keys chained (two independent
+// workgroups per CU instead of one 8-wave workgroup); 6 = variant 2 with KREG (D = 64); 7 = variant
+// 2 with DMA; 8 = variant 2 with KREG and DMA; 9 = attn_bwd1b_kernel (one barrier per query tile);
+// 10 (default) = attn_bwd1b_kernel with its dQ chunks fenced between the S / dP and dV / dK stages
+// when chained (B*H >= 256), else variant 7; without 16-B aligned Q / dO rows the DMA variants
+// fall back to variant 2 (B32 H16 S512 D64: 2 / 7 / 9 / 10 = 162 / 158 / 155 / 154 us,
+// profiles/attn_bwd_r5.txt). Settable for A/B runs in one process
 // (attn_set_bwd_variant); default from FF_ATTN_BWD.
 static int g_bwd_variant = -1;
 int attn_bwd_variant() {
   if (g_bwd_variant < 0) {
     const char* e = getenv("FF_ATTN_BWD");
-    g_bwd_variant = e ? atoi(e) : 2;
+    g_bwd_variant = e ? atoi(e) : 10;
   }
   return g_bwd_variant;
 }
@@ -1593,13 +1951,13 @@ void attn_set_bwd_variant(int v) { g_bwd_variant = v; }
 // keys per backward workgroup
 static int bwd_keys(int D) {
   const int v = attn_bwd_variant();
-  if (v == 0) return 128;
+  if (v == 0 || v == 5) return 128;
   return D == 64 ? 256 : 128;
 }
 
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
-  return (int64_t)nkb * B * H * Sq * D + (int64_t)B * H * Sq;
+  return (int64_t)nkb * B * H * Sq * D + 2 * (int64_t)B * H * Sq;  // slabs, delta, lse2
 }
 
 // Forward structure: 4 = persistent 64 rows per wave (attn_fwd2p_kernel; D = 64, non-causal,
@@ -1684,18 +2042,18 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   }
 }
 
-template <int D, int NW>
+template <int D, int NW, bool KREG = false, bool DMA = false>
 static void launch_bwd_main(AttnArgs a, int nkb, bool chain, hipStream_t st) {
   const bool mask = a.causal || a.Sk % (32 * NW) != 0 || a.Sq % 64 != 0;
   const int bh = a.B * a.H;
   if (chain) {
     for (int p = 0; p < nkb; ++p) {
-      if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, true>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
-      else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, true>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+      if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, true, KREG, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+      else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, true, KREG, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
     }
   } else {
-    if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, false>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
-    else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, false>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+    if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, false, KREG, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+    else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, false, KREG, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
   }
 }
 
@@ -1707,12 +2065,33 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
   const dim3 gfin(ew_grid(per / 4, 256));
   // (every attn_bwd_kernel launch with a single key block writes the final dQ itself)
-  const bool chain = v == 3 || (v == 2 && a.B * a.H >= 256);
+  const bool chain = v == 3 || v == 5 || ((v == 2 || v >= 6) && a.B * a.H >= 256);
   const bool finish = v == 1 || (!chain && nkb > 1);
+  // the DMA variants need 16-B aligned Q / dO rows and buffer offsets below 2 GiB
+  const bool dma_ok = ((uintptr_t)a.q & 15) == 0 && ((uintptr_t)a.dout & 15) == 0 && a.q_ss % 8 == 0 &&
+                      a.do_ss % 8 == 0 && (int64_t)(a.Sq + 64) * a.q_ss * 2 < 0x7fffffffLL &&
+                      (int64_t)(a.Sq + 64) * a.do_ss * 2 < 0x7fffffffLL;
   if (a.D == 64) {
     hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
     if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<64, 2>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
-    else if (v == 0) launch_bwd_main<64, 4>(a, nkb, false, st);
+    else if (v == 0 || v == 5) launch_bwd_main<64, 4>(a, nkb, v == 5, st);
+    else if (v == 6) launch_bwd_main<64, 8, true>(a, nkb, chain, st);
+    else if (v == 8 && dma_ok) launch_bwd_main<64, 8, true, true>(a, nkb, chain, st);
+    else if ((v == 9 || (v == 10 && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
+      const bool m = a.causal || a.Sk % 256 != 0 || a.Sq % 64 != 0;
+      const int bh = a.B * a.H;
+      if (chain) {
+        for (int p = 0; p < nkb; ++p) {
+          if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
+          else if (v == 10) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
+          else hipLaunchKernelGGL((attn_bwd1b_kernel<false, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
+        }
+      } else {
+        if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, false>), dim3(bh * nkb), dim3(512), 0, st, a, nkb, 0);
+        else hipLaunchKernelGGL((attn_bwd1b_kernel<false, false>), dim3(bh * nkb), dim3(512), 0, st, a, nkb, 0);
+      }
+    }
+    else if ((v == 7 || v == 10) && dma_ok) launch_bwd_main<64, 8, false, true>(a, nkb, chain, st);
     else launch_bwd_main<64, 8>(a, nkb, chain, st);
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
   } else if (a.D == 128) {

@@ -536,7 +536,8 @@ void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
   a.lse = lse.data_ptr<float>();
   const int64_t ws_floats = ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D);
   a.dq_acc = ws.data_ptr<float>();
-  a.delta = a.dq_acc + ws_floats - (int64_t)B * H * Sq;  // layout: [nkb partial dQ slabs][delta]
+  a.delta = a.dq_acc + ws_floats - 2 * (int64_t)B * H * Sq;  // layout: [nkb partial dQ slabs][delta][lse2]
+  a.lse2 = a.delta + (int64_t)B * H * Sq;
   a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.D = D; a.scale = scale; a.causal = causal;
   ffk::attn_bwd(a, cur_stream());
 }

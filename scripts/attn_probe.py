@@ -71,19 +71,20 @@ X.attn_set_rescale_thr(default_thr)
 lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
 # backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
 default_variant = X.attn_bwd_variant()
-res = {0: [], 1: [], 2: []}
+BV = tuple(int(x) for x in (sys.argv[6].split(',') if len(sys.argv) > 6 else '0,1,2,5,6,7,8'.split(',')))
+res = {v: [] for v in BV}
 outs = {}
 for rnd in range(3):
-    for var in (0, 1, 2):
+    for var in BV:
         X.attn_set_bwd_variant(var)
         res[var].append(timed(lambda: Kn.flash_attn_bwd(q, sq, k, sq, v, sq, o, so, do, so, lse, dq, sq, dk, sq,
                                                         dv, sq, B, H, S, S, D, scale, False)))
         outs[var] = dqkv.clone()
 fl_b = 2.5 * fl_f
-for var in (0, 1, 2):
+for var in BV:
     ms = min(res[var])
     print(f"attn bwd variant {var}: {ms:.3f} ms {fl_b / ms / 1e9:.1f} TFLOPS  (rounds {[round(t, 3) for t in res[var]]})")
-for var in (1, 2):
-    d = (outs[0].float() - outs[var].float()).abs().max().item()
-    print(f"max |variant0 - variant{var}| over dq/dk/dv: {d:.4g}")
+for var in BV[1:]:
+    d = (outs[BV[0]].float() - outs[var].float()).abs().max().item()
+    print(f"max |variant{BV[0]} - variant{var}| over dq/dk/dv: {d:.4g}")
 X.attn_set_bwd_variant(default_variant)

@@ -205,13 +205,16 @@ def _attn_ref(q, k, v, scale, causal):
     return torch.einsum("bhqk,bhkd->bhqd", p, v), torch.logsumexp(s, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("S,D,causal", [(512, 64, False), (200, 64, False), (256, 128, False), (384, 64, True),
                                         (640, 64, True), (300, 128, True), (1024, 64, True), (512, 128, False)])
 def test_flash_attention(ffC, S, D, causal, variant):
     """Every backward structure (0: 4 waves x 32 keys + slabs; 1: one wave per SIMD, 64 keys per
     wave at D = 64; 2: default; 3: chained per-key-block launches carrying the fp32 dQ sum; 4:
-    8 waves + slabs) against an fp32 PyTorch reference, incl. ragged and causal key blocks."""
+    8 waves + slabs; 5: 4 waves chained; 6: K^T dQ fragments in registers; 7: LDS-DMA Q / dO tiles;
+    8: 6 + 7; 9: one barrier per query tile, dQ on 16x16x32; 10: 9 with fenced dQ chunks, the
+    default) against an fp32 PyTorch reference,
+    incl. ragged and causal key blocks."""
     torch.manual_seed(3)
     prev_variant = ffC.attn_bwd_variant()
     ffC.attn_set_bwd_variant(variant)
@@ -292,7 +295,7 @@ def test_flash_attention_bwd_default_chain(ffC):
     attention shape with the fused [B,S,3,H,D] projection layout, against fp32 autograd."""
     torch.manual_seed(6)
     B, S, H, D = 16, 512, 16, 64
-    assert ffC.attn_bwd_variant() == 2
+    assert ffC.attn_bwd_variant() == 10
     qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
     o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B * H * S, device=DEV)
