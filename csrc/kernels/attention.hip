@@ -1414,7 +1414,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
 // not depend on its S / dP work of the same iteration. dQ^T runs on 16x16x32 MFMAs: 16 (d x query)
 // tiles of 16 x 16, two per wave sharing the K^T operand, each over all KB keys, so no wave hands
 // a partial sum to another (no exchange buffer: the second dS^T image takes its LDS).
-template <bool MASK, bool CHAIN, bool SB = false>
+template <bool MASK, bool CHAIN, bool SB = false, bool PRIO = false>
 __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb, int pass) {
   constexpr int D = 64, NW = 8, NT = 64 * NW, QT = 64, KB = 32 * NW, QB = QT * D * 2;
   constexpr int TILE = 2 * QB + 2 * QT * 4;  // Q tile, dO tile, lse2, delta
@@ -1612,6 +1612,11 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed; older dQ stores done
     lds_barrier();
   };
+  // PRIO: the younger half of the workgroup (waves 4-7) at priority 1 for the whole loop, so it
+  // does not lose VALU arbitration to the older half at every segment start (guide T5, static form)
+  if constexpr (PRIO) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   if (qt_begin < nqt) {
     if (qt_begin + 1 < nqt) dma_rows(qt_begin + 1);
     s_tile(qt_begin, [](int) {});
@@ -2077,13 +2082,14 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
     else if (v == 0 || v == 5) launch_bwd_main<64, 4>(a, nkb, v == 5, st);
     else if (v == 6) launch_bwd_main<64, 8, true>(a, nkb, chain, st);
     else if (v == 8 && dma_ok) launch_bwd_main<64, 8, true, true>(a, nkb, chain, st);
-    else if ((v == 9 || (v == 10 && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
+    else if ((v == 9 || ((v == 10 || v == 11) && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
       const bool m = a.causal || a.Sk % 256 != 0 || a.Sq % 64 != 0;
       const int bh = a.B * a.H;
       if (chain) {
         for (int p = 0; p < nkb; ++p) {
           if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
           else if (v == 10) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
+          else if (v == 11) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
           else hipLaunchKernelGGL((attn_bwd1b_kernel<false, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
         }
       } else {
