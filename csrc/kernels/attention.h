@@ -19,6 +19,11 @@ struct AttnArgs {
   float* dq_acc = nullptr;  // [ceil(Sk/128)][B*H][Sq][D] partials
   float* delta = nullptr;   // [B*H][Sq]
   float* lse2 = nullptr;    // [B*H][Sq] lse * log2(e) (attn_bwd_pre_kernel)
+  // fused bias gradient of the [B,S,3,H,D] QKV projection: dbias [3][H][D] += column sums of dq /
+  // dk / dv (attn_bwd1b_kernel partials in dbp, folded by attn_bias_fold_kernel); attn_bwd returns
+  // whether it did, else the caller sums the bias gradient itself
+  float* dbp = nullptr;
+  float* dbias = nullptr;
   int B = 0, H = 0, Sq = 0, Sk = 0, D = 64;
   float scale = 1.f;
   int causal = 0;
@@ -26,8 +31,9 @@ struct AttnArgs {
 };
 
 void attn_fwd(AttnArgs a, hipStream_t st);
-void attn_bwd(AttnArgs a, hipStream_t st);
+bool attn_bwd(AttnArgs a, hipStream_t st);
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D);
+int64_t attn_bwd_slab_floats(int B, int H, int Sq, int Sk, int D);  // offset of delta in the workspace
 int attn_bwd_variant();
 void attn_set_bwd_variant(int v);
 int attn_fwd_variant();

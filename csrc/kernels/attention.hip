@@ -1587,6 +1587,11 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
       }
       };
   auto dq_tile = [&](int t) { dq_chunk(t, 0, KB / 32); };
+  // dbp (fused QKV-bias gradient, non-causal chain): column sums of the final dQ (last pass) and of
+  // this block's dK / dV, as partials [B*H][2][D] (dQ, per query half of the waves) and
+  // [nkb][B*H][D] (dK, dV) that attn_bias_fold adds into the bias gradient
+  const bool bsum = a.dbp != nullptr;
+  float dqs[4] = {0.f, 0.f, 0.f, 0.f};
   auto dq_store = [&](int t) {  // after the barrier: vmcnt counts stores, the next wait is a tile away
     const int pq = (t - 1) * QT;
       int last = nkb - 1;
@@ -1600,8 +1605,12 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
             acc[0] += prevq[j].x; acc[1] += prevq[j].y; acc[2] += prevq[j].z; acc[3] += prevq[j].w;
           }
           if (chain && kblk == last) {
-            *reinterpret_cast<uint2*>(dQb + (int64_t)q * a.dq_ss + dq_d0 + 4 * G) =
-                make_uint2(pack_bf2(acc[0] * a.scale, acc[1] * a.scale), pack_bf2(acc[2] * a.scale, acc[3] * a.scale));
+            const unsigned w0 = pack_bf2(acc[0] * a.scale, acc[1] * a.scale), w1 = pack_bf2(acc[2] * a.scale, acc[3] * a.scale);
+            *reinterpret_cast<uint2*>(dQb + (int64_t)q * a.dq_ss + dq_d0 + 4 * G) = make_uint2(w0, w1);
+            if (bsum) {  // the bias gradient sums the stored (bf16) dQ, as the unfused column sum would
+              dqs[0] += __uint_as_float(w0 << 16); dqs[1] += __uint_as_float(w0 & 0xffff0000u);
+              dqs[2] += __uint_as_float(w1 << 16); dqs[3] += __uint_as_float(w1 & 0xffff0000u);
+            }
           } else {
             *reinterpret_cast<float4*>(dq_part + (int64_t)q * D + dq_d0 + 4 * G) = make_float4(acc[0], acc[1], acc[2], acc[3]);
           }
@@ -1641,6 +1650,15 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
   if (MASK && a.causal && !chain) {
     for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
   }
+  if (bsum && kblk == nkb - 1) {  // dQ column sums: over the 16 query lanes of each d quad
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dqs[i] += __shfl_xor(dqs[i], off, 64);
+    if (l16 == 0)
+      *reinterpret_cast<float4*>(a.dbp + ((int64_t)bh * 2 + (wave >> 2)) * D + dq_d0 + 4 * G) =
+          make_float4(dqs[0], dqs[1], dqs[2], dqs[3]);
+  }
   if (qt_begin >= nqt) __syncthreads();
   {
     char* dv_l = smem;
@@ -1661,15 +1679,81 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
     bf16_t* dKb = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh;
     bf16_t* dVb = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh;
     constexpr int CPR = D / 8;
+    static_assert(NT % CPR == 0, "a thread's chunk column is fixed");
+    float sk[8] = {}, sv[8] = {};
 #pragma unroll
     for (int i = 0; i < KB * CPR / NT; ++i) {
       const int id = tid + i * NT, r = id / CPR, c = id % CPR;
       const int off = r * (D * 2) + ((c ^ (r & 7)) << 4);
       if (!MASK || kb0 + r < a.Sk) {
-        *reinterpret_cast<uint4*>(dKb + (int64_t)(kb0 + r) * a.dk_ss + 8 * c) = *reinterpret_cast<const uint4*>(k_l + off);
-        *reinterpret_cast<uint4*>(dVb + (int64_t)(kb0 + r) * a.dv_ss + 8 * c) = *reinterpret_cast<const uint4*>(dv_l + off);
+        const uint4 kv4 = *reinterpret_cast<const uint4*>(k_l + off);
+        const uint4 vv4 = *reinterpret_cast<const uint4*>(dv_l + off);
+        *reinterpret_cast<uint4*>(dKb + (int64_t)(kb0 + r) * a.dk_ss + 8 * c) = kv4;
+        *reinterpret_cast<uint4*>(dVb + (int64_t)(kb0 + r) * a.dv_ss + 8 * c) = vv4;
+        if (bsum) {
+          const unsigned kw[4] = {kv4.x, kv4.y, kv4.z, kv4.w}, vw[4] = {vv4.x, vv4.y, vv4.z, vv4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sk[2 * e] += __uint_as_float(kw[e] << 16); sk[2 * e + 1] += __uint_as_float(kw[e] & 0xffff0000u);
+            sv[2 * e] += __uint_as_float(vw[e] << 16); sv[2 * e + 1] += __uint_as_float(vw[e] & 0xffff0000u);
+          }
+        }
       }
     }
+    if (bsum) {  // dK / dV column sums: lanes l, l^8, l^16, l^32 share the chunk, then the 8 waves via LDS
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sk[e] += __shfl_xor(sk[e], off, 64);
+          sv[e] += __shfl_xor(sv[e], off, 64);
+        }
+      float* red = reinterpret_cast<float*>(ds0);  // the dS^T images are dead here
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[(wave * CPR + lane) * 8 + e] = sk[e];
+          red[NW * CPR * 8 + (wave * CPR + lane) * 8 + e] = sv[e];
+        }
+      }
+      __syncthreads();
+      if (tid < 2 * D) {
+        const int which = tid / D, d = tid % D;  // d = 8 * chunk + e
+        float acc = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) acc += red[which * NW * CPR * 8 + (w * CPR + d / 8) * 8 + d % 8];
+        float* part = a.dbp + (int64_t)a.B * a.H * 2 * D + (int64_t)which * nkb * a.B * a.H * D;
+        part[((int64_t)kblk * a.B * a.H + bh) * D + d] = acc;
+      }
+    }
+  }
+}
+
+// db[which][h][d] += the partials of attn_bwd1b_kernel: dQ over (batch, query half), dK / dV over
+// (key block, batch) — the fused QKV projection's bias gradient in its [3][H][D] layout. One
+// workgroup per (which, head): 4 groups of D threads each sum a quarter of the partial rows
+// (coalesced D-float rows, independent loads), then fold through LDS (one thread per output
+// looping over all rows was latency-bound: 21 us per call).
+__global__ void __launch_bounds__(256) attn_bias_fold_kernel(const float* __restrict__ part, float* __restrict__ db,
+                                                             int B, int H, int D, int nkb) {
+  __shared__ float red[256];
+  const int which = blockIdx.x / H, h = blockIdx.x % H;
+  const int d = threadIdx.x % D, grp = threadIdx.x / D, ngrp = blockDim.x / D;
+  float s = 0.f;
+  if (grp < ngrp) {
+    if (which == 0) {  // rows (b, x): part[((b*H + h)*2 + x)*D + d]
+      for (int r = grp; r < 2 * B; r += ngrp) s += part[((int64_t)((r >> 1) * H + h) * 2 + (r & 1)) * D + d];
+    } else {  // rows (kb, b): p[((kb*B + b)*H + h)*D + d]
+      const float* p = part + (int64_t)B * H * 2 * D + (int64_t)(which - 1) * nkb * B * H * D;
+      for (int r = grp; r < nkb * B; r += ngrp) s += p[((int64_t)r * H + h) * D + d];
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < D) {
+    float t = 0.f;
+    for (int g = 0; g < ngrp; ++g) t += red[g * D + threadIdx.x];
+    db[((int64_t)which * H + h) * D + threadIdx.x] += t;
   }
 }
 
@@ -1960,9 +2044,15 @@ static int bwd_keys(int D) {
   return D == 64 ? 256 : 128;
 }
 
+int64_t attn_bwd_slab_floats(int B, int H, int Sq, int Sk, int D) {
+  const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
+  return (int64_t)nkb * B * H * Sq * D;
+}
+
 int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
-  return (int64_t)nkb * B * H * Sq * D + 2 * (int64_t)B * H * Sq;  // slabs, delta, lse2
+  // slabs, delta, lse2, bias-gradient partials (attn_bwd1b_kernel)
+  return (int64_t)nkb * B * H * Sq * D + 2 * (int64_t)B * H * Sq + (int64_t)B * H * D * (2 + 2 * nkb);
 }
 
 // Forward structure: 4 = persistent 64 rows per wave (attn_fwd2p_kernel; D = 64, non-causal,
@@ -2062,7 +2152,8 @@ static void launch_bwd_main(AttnArgs a, int nkb, bool chain, hipStream_t st) {
   }
 }
 
-void attn_bwd(AttnArgs a, hipStream_t st) {
+bool attn_bwd(AttnArgs a, hipStream_t st) {
+  bool bias_done = false;
   const int v = attn_bwd_variant();
   const int nkb = (a.Sk + bwd_keys(a.D) - 1) / bwd_keys(a.D);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
@@ -2085,6 +2176,10 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
     else if ((v == 9 || ((v == 10 || v == 11) && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
       const bool m = a.causal || a.Sk % 256 != 0 || a.Sq % 64 != 0;
       const int bh = a.B * a.H;
+      // fused bias-gradient sums: chained and non-causal (every query tile's last key block is
+      // the last launch)
+      if (!(chain && !a.causal)) a.dbp = nullptr;
+      bias_done = a.dbp != nullptr;
       if (chain) {
         for (int p = 0; p < nkb; ++p) {
           if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
@@ -2106,6 +2201,10 @@ void attn_bwd(AttnArgs a, hipStream_t st) {
     else launch_bwd_main<128, 4>(a, nkb, v != 0 && chain, st);
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
   }
+  if (bias_done)
+    hipLaunchKernelGGL(attn_bias_fold_kernel, dim3((unsigned)(3 * a.H)), dim3(256), 0, st, a.dbp, a.dbias, a.B, a.H,
+                       a.D, nkb);
+  return bias_done;
 }
 
 }  // namespace ffk

@@ -516,11 +516,11 @@ void attn_fwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
 int64_t attn_bwd_ws(int64_t B, int64_t H, int64_t Sq, int64_t Sk, int64_t D) {
   return ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D);
 }
-void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
+bool attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> ks, Tensor v,
               std::vector<int64_t> vs, Tensor o, std::vector<int64_t> os, Tensor dout, std::vector<int64_t> dos,
               Tensor lse, Tensor dq, std::vector<int64_t> dqs, Tensor dk, std::vector<int64_t> dks, Tensor dv,
               std::vector<int64_t> dvs, Tensor ws, int64_t B, int64_t H, int64_t Sq, int64_t Sk, int64_t D,
-              double scale, bool causal) {
+              double scale, bool causal, optional<Tensor> dbias) {
   TORCH_CHECK(D == 64 || D == 128, "flash attention supports head_dim 64/128");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D),
               "attn_bwd: workspace too small");
@@ -534,12 +534,18 @@ void attn_bwd(Tensor q, std::vector<int64_t> qs, Tensor k, std::vector<int64_t> 
   a.dk = (uint16_t*)dk.data_ptr(); a.dk_sb = dks[0]; a.dk_sh = dks[1]; a.dk_ss = dks[2];
   a.dv = (uint16_t*)dv.data_ptr(); a.dv_sb = dvs[0]; a.dv_sh = dvs[1]; a.dv_ss = dvs[2];
   a.lse = lse.data_ptr<float>();
-  const int64_t ws_floats = ffk::attn_bwd_workspace_floats(B, H, Sq, Sk, D);
   a.dq_acc = ws.data_ptr<float>();
-  a.delta = a.dq_acc + ws_floats - 2 * (int64_t)B * H * Sq;  // layout: [nkb partial dQ slabs][delta][lse2]
+  // layout: [nkb partial dQ slabs][delta][lse2][bias-gradient partials]
+  a.delta = a.dq_acc + ffk::attn_bwd_slab_floats(B, H, Sq, Sk, D);
   a.lse2 = a.delta + (int64_t)B * H * Sq;
+  if (dbias) {  // [3*H*D] fp32, accumulated into
+    TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() == 3 * H * D,
+                "attn_bwd: dbias must be a contiguous fp32 [3*H*D] tensor");
+    a.dbp = a.lse2 + (int64_t)B * H * Sq;
+    a.dbias = dbias->data_ptr<float>();
+  }
   a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.D = D; a.scale = scale; a.causal = causal;
-  ffk::attn_bwd(a, cur_stream());
+  return ffk::attn_bwd(a, cur_stream());
 }
 
 
@@ -846,7 +852,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("aggregate_fwd", &aggregate_fwd);
   m.def("aggregate_bwd", &aggregate_bwd);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("qs"), py::arg("k"), py::arg("ks"), py::arg("v"), py::arg("vs"),
+        py::arg("o"), py::arg("os"), py::arg("dout"), py::arg("dos"), py::arg("lse"), py::arg("dq"), py::arg("dqs"),
+        py::arg("dk"), py::arg("dks"), py::arg("dv"), py::arg("dvs"), py::arg("ws"), py::arg("B"), py::arg("H"),
+        py::arg("Sq"), py::arg("Sk"), py::arg("D"), py::arg("scale"), py::arg("causal"),
+        py::arg("dbias") = py::none());
   m.def("attn_bwd_ws", &attn_bwd_ws);
   m.def("attn_set_bwd_variant", [](int v) { ffk::attn_set_bwd_variant(v); });
   m.def("attn_fwd_variant", []() { return ffk::attn_fwd_variant(); });

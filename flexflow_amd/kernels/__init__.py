@@ -815,13 +815,16 @@ def flash_attn_fwd(q, qs, k, ks, v, vs, o, os_, B, H, Sq, Sk, D, scale, causal):
 
 
 def flash_attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, B, H, Sq, Sk, D, scale,
-                   causal):
+                   causal, dbias=None):
+    """dbias: optional contiguous fp32 [3*H*D] bias gradient of a fused [B,S,3,H,D] QKV projection
+    (dq/dk/dv inside one dqkv buffer). Returns True when the kernel added the column sums of dq / dk /
+    dv into it (attn_bwd1b_kernel, non-causal); False: the caller still owes that bias gradient."""
     X = ext()
     from ..runtime.device import DeviceContext
     # dQ partial slabs + delta: one arena buffer shared (stream-ordered) by every attention layer
     ws = DeviceContext.get(q.device).workspace("attn_bwd", X.attn_bwd_ws(B, H, Sq, Sk, D))
-    X.attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, ws, B, H, Sq, Sk, D, scale,
-               causal)
+    return bool(X.attn_bwd(q, qs, k, ks, v, vs, o, os_, do, dos, lse, dq, dqs, dk, dks, dv, dvs, ws, B, H, Sq, Sk, D,
+                           scale, causal, dbias))
 
 
 # ---------------------------------------------------------------------------- layer norm

@@ -208,6 +208,7 @@ class MultiHeadAttention(OpImpl):
         scale, causal = s["scale"], s["causal"]
         qs, ks, vs, os_ = s["qs"], s["ks"], s["vs"], s["os"]
         fused = s["fused"]
+        bias_done = False
         if fused:
             qkv = s["qkv"]
             qv, kv, vv = qkv.view(-1), qkv.view(-1)[Hl * kd:], qkv.view(-1)[2 * Hl * kd:]
@@ -228,8 +229,15 @@ class MultiHeadAttention(OpImpl):
             for g, st, pg, S_, d in ((dq, qs, pdq, Sq, kd), (dk, ks, pdk, Sk, kd), (dv, vs, pdv, Sk, vd)):
                 g.as_strided((B, Hl, S_, d), (st[0], st[1], st[2], 1)).copy_(pg[..., :d].permute(0, 2, 1, 3))
         elif "lse" in s:
-            K.flash_attn_bwd(qv, qs, kv, ks, vv, vs, o, os_, do, os_, s["lse"], dq, qs, dk, ks, dv, vs,
-                             B, Hl, Sq, Sk, kd, scale, causal)
+            # fused projection: the kernel can add the QKV bias gradient (column sums of dq / dk / dv)
+            # itself, sparing linear_bwd a pass over dqkv (bias_act_bwd + fold)
+            dbq = gw("qkv_bias") if (fused and os.environ.get("FF_ATTN_BIAS_FUSION", "1") == "1") else None
+            if dbq is not None and dbq.dtype == torch.float32 and dbq.is_contiguous():
+                bias_done = K.flash_attn_bwd(qv, qs, kv, ks, vv, vs, o, os_, do, os_, s["lse"], dq, qs, dk, ks, dv, vs,
+                                             B, Hl, Sq, Sk, kd, scale, causal, dbias=dbq.view(-1))
+            else:
+                K.flash_attn_bwd(qv, qs, kv, ks, vv, vs, o, os_, do, os_, s["lse"], dq, qs, dk, ks, dv, vs,
+                                 B, Hl, Sq, Sk, kd, scale, causal)
         elif "P" in s:
             K.attn_f32_bwd(qv, qs, kv, ks, vv, vs, do.contiguous().view(-1), os_, s["P"], dq.view(-1), dk.view(-1),
                            dv.view(-1), B, Hl, Sq, Sk, kd, vd, scale)
@@ -246,7 +254,7 @@ class MultiHeadAttention(OpImpl):
             dv.as_strided((B, Hl, Sk, vd), (vs[0], vs[1], vs[2], 1)).copy_(gv)
         if fused:
             dw = gw("qkv_weight")
-            db = gw("qkv_bias")
+            db = None if bias_done else gw("qkv_bias")
             acc = (ctx.extra.get("dx_accum") or {}).get(0)
             dx2 = K.linear_bwd(dqkv, s["x2"], s["wqkv"], None, K.ACT_NONE,
                                dw.view(3 * Hl * kd, -1) if dw is not None else None,

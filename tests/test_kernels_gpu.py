@@ -317,6 +317,37 @@ def test_flash_attention_bwd_default_chain(ffC):
         assert _rel(dqkv[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
 
 
+@pytest.mark.parametrize("S,causal,fused", [(512, False, True), (448, False, True), (512, True, False)])
+def test_flash_attention_fused_qkv_bias_grad(ffC, S, causal, fused):
+    """The chained non-causal backward adds the fused QKV projection's bias gradient (column sums of
+    dq / dk / dv, bf16 as stored) into dbias itself and says so; causal: it declines (False) and
+    leaves dbias untouched. Against fp32 column sums of the dqkv it wrote."""
+    torch.manual_seed(8)
+    B, H, D = 16, 16, 64  # B*H >= 256: the chained default path
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
+    o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=DEV)
+    sq = [S * 3 * H * D, D, 3 * H * D]
+    so = [S * H * D, D, H * D]
+    base = qkv.view(-1)
+    ffC.attn_fwd(base, sq, base[H * D:], sq, base[2 * H * D:], sq, o, so, lse, B, H, S, S, D, 0.125, causal)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(qkv)
+    g = dqkv.view(-1)
+    n = ffC.attn_bwd_ws(B, H, S, S, D)
+    wsg = torch.full((n + 65536,), 7.0, device=DEV)  # a guard band after the workspace
+    dbias = torch.full((3 * H * D,), 0.5, device=DEV)
+    done = ffC.attn_bwd(base, sq, base[H * D:], sq, base[2 * H * D:], sq, o, so, do, so, lse, g, sq, g[H * D:], sq,
+                        g[2 * H * D:], sq, wsg[:n], B, H, S, S, D, 0.125, causal, dbias)
+    assert done == fused
+    assert torch.equal(wsg[n:], torch.full_like(wsg[n:], 7.0)), "attn_bwd wrote past its workspace"
+    if fused:
+        ref = dqkv.float().sum(dim=(0, 1)).reshape(-1) + 0.5
+        assert torch.allclose(dbias, ref, rtol=1e-4, atol=1e-2), (dbias - ref).abs().max()
+    else:
+        assert torch.equal(dbias, torch.full_like(dbias, 0.5))
+
+
 def test_flash_attention_strided_qkv(ffC):
     """Q/K/V read straight out of a fused [B,S,3,H,D] projection, O written as [B,S,H,D]."""
     torch.manual_seed(4)
