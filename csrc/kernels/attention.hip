@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
 // (708 -> 725-740 TF/s at B32 H16 S512, 794 -> 840 at S4096), -1..7 % at S = 256; taking the row
 // sums on the matrix core (ones x P^T) as well did not help. Bitwise equal to the 4-wave kernel.
 // D = 64; the default for Sq >= 512 (variant 3).
-template <bool MASK>
+template <bool MASK, bool PRIO = false>
 __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
   constexpr int D = 64, KV = 64, QB = 2, ROWS = 4 * 32 * QB;
   constexpr int TB = KV * D * 2;
@@ -409,6 +409,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
     f32x16 sacc[QB][2];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < D / 16; ++s)
 #pragma unroll
@@ -418,6 +419,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
         for (int qb = 0; qb < QB; ++qb)
           sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
       }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     const int kbase = t * KV;
     bf16x8 pf[QB][2][2];
 #pragma unroll
@@ -466,6 +468,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) { pf[qb][kt][0] = pack8(sacc[qb][kt], 0); pf[qb][kt][1] = pack8(sacc[qb][kt], 8); }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -479,6 +482,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
           for (int qb = 0; qb < QB; ++qb)
             oacc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][kt][s2], oacc[qb][dt], 0, 0, 0);
         }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -1731,12 +1735,12 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
 
 // db[which][h][d] += the partials of attn_bwd1b_kernel: dQ over (batch, query half), dK / dV over
 // (key block, batch) — the fused QKV projection's bias gradient in its [3][H][D] layout. One
-// workgroup per (which, head): 4 groups of D threads each sum a quarter of the partial rows
+// workgroup per (which, head): 1024 / D groups of D threads each sum a few of the partial rows
 // (coalesced D-float rows, independent loads), then fold through LDS (one thread per output
-// looping over all rows was latency-bound: 21 us per call).
-__global__ void __launch_bounds__(256) attn_bias_fold_kernel(const float* __restrict__ part, float* __restrict__ db,
-                                                             int B, int H, int D, int nkb) {
-  __shared__ float red[256];
+// looping over all rows was latency-bound: 21 us per call; 4 groups per head still 9 us).
+__global__ void __launch_bounds__(1024) attn_bias_fold_kernel(const float* __restrict__ part, float* __restrict__ db,
+                                                              int B, int H, int D, int nkb) {
+  __shared__ float red[1024];
   const int which = blockIdx.x / H, h = blockIdx.x % H;
   const int d = threadIdx.x % D, grp = threadIdx.x / D, ngrp = blockDim.x / D;
   float s = 0.f;
@@ -2109,9 +2113,10 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   }
   // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
   // (half the workgroups), profiles/attn_fwd_variants_r4.txt
-  if (attn_fwd_variant() == 3 && dma_ok && a.D == 64 && a.Sq >= 512) {
+  if ((attn_fwd_variant() == 3 || attn_fwd_variant() == 5) && dma_ok && a.D == 64 && a.Sq >= 512) {
     const dim3 g3((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
     if (mask) hipLaunchKernelGGL((attn_fwd2_kernel<true>), g3, dim3(256), 0, st, a);
+    else if (attn_fwd_variant() == 5) hipLaunchKernelGGL((attn_fwd2_kernel<false, true>), g3, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd2_kernel<false>), g3, dim3(256), 0, st, a);
     return;
   }
@@ -2202,7 +2207,7 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
   }
   if (bias_done)
-    hipLaunchKernelGGL(attn_bias_fold_kernel, dim3((unsigned)(3 * a.H)), dim3(256), 0, st, a.dbp, a.dbias, a.B, a.H,
+    hipLaunchKernelGGL(attn_bias_fold_kernel, dim3((unsigned)(3 * a.H)), dim3(1024), 0, st, a.dbp, a.dbias, a.B, a.H,
                        a.D, nkb);
   return bias_done;
 }

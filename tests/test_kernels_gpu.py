@@ -228,10 +228,11 @@ def test_flash_attention(ffC, S, D, causal, variant):
     scale = 1.0 / math.sqrt(D)
     ffC.attn_fwd(q, st, k, st, v, st, o, st, lse, B, H, S, S, D, scale, causal)
     # the forward structures (0: 4 waves, register-staged K/V; 1: 4 waves, LDS-DMA; 2: 8-wave
-    # ping-pong; 3: 64 rows per wave; 4: persistent 64 rows per wave) run the same per-row
+    # ping-pong; 3: 64 rows per wave; 4: persistent 64 rows per wave; 5: 3 with the MFMA clusters at
+    # priority 1) run the same per-row
     # arithmetic: bitwise equal
     prev_fwd = ffC.attn_fwd_variant()
-    for fv in (0, 1, 2, 3, 4):
+    for fv in (0, 1, 2, 3, 4, 5):
         ffC.attn_set_fwd_variant(fv)
         o2, lse2 = torch.full_like(o, 3.0), torch.full_like(lse, 3.0)
         ffC.attn_fwd(q, st, k, st, v, st, o2, st, lse2, B, H, S, S, D, scale, causal)
