@@ -103,8 +103,8 @@ __global__ void ln_fwd_generic(const T* __restrict__ x, const T* __restrict__ re
   }
 }
 
-template <typename T, int NCH>
-__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int NCH, int NT = 256>
+__global__ void __launch_bounds__(NT) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const T* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                      const T* __restrict__ dres_in, float* __restrict__ pgam,
@@ -175,9 +175,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  // per-wave partial column sums -> folded over the block's 4 waves in LDS -> one plain-stored slab
-  // row per block (reduced by col_reduce_add2); dynamic LDS = 4 * cols floats, reused for beta
+  // per-wave partial column sums -> folded over the block's NT / 64 waves in LDS -> one
+  // plain-stored slab row per block (reduced by col_reduce_add3); dynamic LDS = NT / 64 * cols
+  // floats, reused for beta
   extern __shared__ float lds_red[];
+  constexpr int NWB = NT / 64;
   const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int pass = 0; pass < 3; ++pass) {
@@ -191,9 +193,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
         for (int j = 0; j < V; ++j) lds_red[w * cols + col + j] = pass == 2 ? pd[c][j] : (pass ? pb[c][j] : pg[c][j]);
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < cols; k += 256)
-      slab[(int64_t)blockIdx.x * cols + k] =
-          lds_red[k] + lds_red[cols + k] + lds_red[2 * cols + k] + lds_red[3 * cols + k];
+    for (int k = threadIdx.x; k < cols; k += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWB; ++q) t += lds_red[q * cols + k];
+      slab[(int64_t)blockIdx.x * cols + k] = t;
+    }
     __syncthreads();
   }
 }
@@ -233,6 +238,18 @@ __global__ void ln_bwd_generic(const T* __restrict__ dy, const T* __restrict__ x
 
 static bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// FF_LN_BWD_WIDE=1: the 1024-thread LayerNorm backward (256 partial rows). Opt-in: same-box A/B at
+// BERT-Large b32 43.95 vs 43.94 ms/step (profiles/ln_bwd_wide_ab_r5.txt) — the shorter fold is
+// paid back inside the kernel.
+static bool ln_bwd_wide_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_LN_BWD_WIDE");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int rows, int cols, float eps, hipStream_t st) {
   if (rows == 0) return;
@@ -260,7 +277,14 @@ void layernorm_fwd(int dt, const void* x, const void* res, void* sum_out, const 
 #undef LNF
 }
 
-int layernorm_bwd_waves(int rows) { return std::max(1, std::min((rows + 15) / 16, 1024)); }  // slab rows = blocks
+// slab rows = blocks: 1024-thread blocks (16 waves, ~4 rows each) when the LDS fold fits (cols <=
+// 1024): a quarter of the partial rows of the 256-thread form, so the fold reads 4x less and its
+// serial per-column chain is 4x shorter. layernorm_bwd_waves(rows) bounds both (workspace size).
+int layernorm_bwd_waves(int rows) { return std::max(1, std::min((rows + 15) / 16, 1024)); }
+static bool ln_bwd_wide(int cols) { return cols <= 1024 && ln_bwd_wide_on(); }
+static int ln_bwd_blocks(int rows, int cols) {
+  return ln_bwd_wide(cols) ? std::max(1, std::min((rows + 63) / 64, 256)) : layernorm_bwd_waves(rows);
+}
 
 void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    void* dx, const void* dres_in, float* dgamma, float* dbeta, float* dsum, float* ws, int rows,
@@ -272,7 +296,8 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
                    (!gamma || a16(gamma));
   const int nch = (cols + 64 * V - 1) / (64 * V);
   // ~4 rows per wave: enough waves in flight to cover HBM latency, slab partials stay small
-  const int blocks = std::max(1, std::min((rows + 15) / 16, 1024));
+  const bool wide = ln_bwd_wide(cols);
+  const int blocks = ln_bwd_blocks(rows, cols);
   const int nw = blocks;
   // slab layout: [dgamma | dbeta | dsum] partials, nw rows each (absent ones skipped)
   float* pg = dgamma ? ws : nullptr;
@@ -285,8 +310,11 @@ void layernorm_bwd(int dt, const void* dy, const void* x, const void* gamma, con
     else if (dsum) bias_act_bwd(dt, dx, nullptr, nullptr, dsum, ws + 2 * (int64_t)nw * cols, rows, cols, ACT_NONE, st, 2);
     return;
   }
-#define LNB(T, N) do { used_slab = true; hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 4 * cols * sizeof(float), st, (const T*)dy, (const T*)x, \
-                                     (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, pd, rows, cols, accumulate); } while (0)
+#define LNB(T, N) do { used_slab = true; \
+    if (wide) hipLaunchKernelGGL((ln_bwd_kernel<T, N, 1024>), dim3(blocks), dim3(1024), 16 * cols * sizeof(float), st, (const T*)dy, \
+                                 (const T*)x, (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, pd, rows, cols, accumulate); \
+    else hipLaunchKernelGGL((ln_bwd_kernel<T, N>), dim3(blocks), dim3(256), 4 * cols * sizeof(float), st, (const T*)dy, (const T*)x, \
+                            (const T*)gamma, mean, rstd, (T*)dx, (const T*)dres_in, pg, pb, pd, rows, cols, accumulate); } while (0)
   if (dt == DT_BF16) {
     using T = bf16_t;
     if (vec && nch <= 1) LNB(T, 1); else if (vec && nch <= 2) LNB(T, 2); else if (vec && nch <= 4) LNB(T, 4);
