@@ -330,12 +330,15 @@ void sgd_update(Tensor master, Tensor grad, optional<Tensor> mom, optional<Tenso
                   momentum, nesterov, wd, gscale, cur_stream(), (int)max_blocks);
 }
 void adam_update(Tensor master, Tensor grad, Tensor m, Tensor v, optional<Tensor> lowp, double alpha_t, double b1,
-                 double b2, double wd, double eps, double gscale, int64_t max_blocks) {
+                 double b2, double wd, double eps, double gscale, int64_t max_blocks, optional<Tensor> alpha_dev) {
+  if (alpha_dev) TORCH_CHECK(alpha_dev->scalar_type() == at::kFloat && alpha_dev->numel() == 1 && alpha_dev->is_cuda(),
+                             "adam_update: alpha_dev must be a one-element fp32 device tensor");
   TORCH_CHECK(master.numel() == grad.numel() && m.numel() == master.numel() && v.numel() == master.numel());
   if (lowp.has_value() && lowp->defined())
     TORCH_CHECK(lowp->scalar_type() == at::kBFloat16 && lowp->numel() == master.numel());
   ffk::adam_update(master.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                   ptr(lowp), master.numel(), alpha_t, b1, b2, wd, eps, gscale, cur_stream(), (int)max_blocks);
+                   ptr(lowp), master.numel(), alpha_t, b1, b2, wd, eps, gscale, cur_stream(), (int)max_blocks,
+                   alpha_dev ? alpha_dev->data_ptr<float>() : nullptr);
 }
 void embedding_fwd(Tensor idx, Tensor table, Tensor out, int64_t n_rows, int64_t bag, int64_t dim, bool avg) {
   TORCH_CHECK(idx.numel() == n_rows * bag && out.numel() == n_rows * dim && table.size(-1) == dim);
@@ -834,7 +837,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_sparse_rows", &sgd_sparse_rows);
   m.def("adam_update", &adam_update, py::arg("master"), py::arg("grad"), py::arg("m"), py::arg("v"), py::arg("lowp"),
         py::arg("alpha_t"), py::arg("b1"), py::arg("b2"), py::arg("wd"), py::arg("eps"), py::arg("gscale"),
-        py::arg("max_blocks") = 0);
+        py::arg("max_blocks") = 0, py::arg("alpha_dev") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("init_uniform", &init_uniform);

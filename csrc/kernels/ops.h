@@ -108,7 +108,7 @@ void sgd_sparse_rows(const int64_t* idx, int n, int64_t rows, int dim, int* mark
 void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, int64_t n, float lr, float momentum,
                 int nesterov, float wd, float gscale, hipStream_t st, int max_blocks = 0);
 void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,
-                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st, int max_blocks = 0);
+                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st, int max_blocks = 0, const float* alpha_dev = nullptr);
 
 // embedding.hip
 void embedding_fwd(int dt, int idx64, const void* idx, const void* table, void* out, int64_t n_out_rows, int bag,

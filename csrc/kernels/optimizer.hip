@@ -50,9 +50,12 @@ __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, f
   }
 }
 
+// alpha_dev: the step size read from device memory instead of the argument (a captured hipGraph
+// of the whole training step replays one launch whose alpha_t changes every step)
 __global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16_t* __restrict__ wl, int64_t n, float alpha_t, float b1,
-                            float b2, float wd, float eps, float gscale) {
+                            float b2, float wd, float eps, float gscale, const float* __restrict__ alpha_dev) {
+  if (alpha_dev) alpha_t = *alpha_dev;
   const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
@@ -138,10 +141,11 @@ void sgd_update(float* master, const float* grad, float* mom, void* param_lowp, 
                      (bf16_t*)param_lowp, n, lr, momentum, nesterov, wd, gscale);
 }
 void adam_update(float* master, const float* grad, float* m, float* v, void* param_lowp, int64_t n, float alpha_t,
-                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st, int max_blocks) {
+                 float beta1, float beta2, float wd, float eps, float gscale, hipStream_t st, int max_blocks,
+                 const float* alpha_dev) {
   if (n == 0) return;
   hipLaunchKernelGGL(adam_kernel, dim3(opt_grid(n, max_blocks)), dim3(256), 0, st, master, grad, m, v,
-                     (bf16_t*)param_lowp, n, alpha_t, beta1, beta2, wd, eps, gscale);
+                     (bf16_t*)param_lowp, n, alpha_t, beta1, beta2, wd, eps, gscale, alpha_dev);
 }
 
 }  // namespace ffk

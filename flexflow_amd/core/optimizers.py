@@ -70,6 +70,13 @@ class AdamOptimizer(Optimizer):
         self.beta1_t = 1.0
         self.beta2_t = 1.0
         self.alpha_t = alpha
+        # device copy of alpha_t, set up by a captured whole-step hipGraph (runtime/graph.py): the
+        # replayed Adam launches read the step size from it, next() refreshes it before each step
+        self.alpha_dev = None
+
+    def use_device_alpha(self, device):
+        if self.alpha_dev is None:
+            self.alpha_dev = torch.full((1,), float(self.alpha_t), device=device, dtype=torch.float32)
 
     def set_learning_rate(self, learning_rate):
         self.alpha = learning_rate
@@ -83,14 +90,16 @@ class AdamOptimizer(Optimizer):
         self.beta1_t *= self.beta1
         self.beta2_t *= self.beta2
         self.alpha_t = self.alpha * math.sqrt(1 - self.beta2_t) / (1 - self.beta1_t)
+        if self.alpha_dev is not None:
+            self.alpha_dev.fill_(self.alpha_t)
 
     def step(self, arena):
         m, v = self.state[id(arena)]
         K.adam_update(arena.master, arena.grad, m, v, arena.lowp, self.alpha_t, self.beta1, self.beta2,
-                      self.weight_decay, self.epsilon)
+                      self.weight_decay, self.epsilon, alpha_dev=self.alpha_dev)
 
     def step_range(self, arena, lo, hi, max_blocks=0):
         m, v = self.state[id(arena)]
         K.adam_update(arena.master[lo:hi], arena.grad[lo:hi], m[lo:hi], v[lo:hi],
                       arena.lowp[lo:hi] if arena.lowp is not None else None, self.alpha_t, self.beta1, self.beta2,
-                      self.weight_decay, self.epsilon, max_blocks=max_blocks)
+                      self.weight_decay, self.epsilon, max_blocks=max_blocks, alpha_dev=self.alpha_dev)

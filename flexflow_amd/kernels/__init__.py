@@ -1245,10 +1245,14 @@ def sgd_sparse_rows(idx, mark, master, grad, lowp, lr):
         lowp[rows] = master[rows].to(lowp.dtype)
 
 
-def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0, max_blocks=0):
+def adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale=1.0, max_blocks=0, alpha_dev=None):
+    """alpha_dev: optional one-element fp32 device tensor the kernel reads the step size from (a
+    captured training step replays the launch while alpha_t changes every step)."""
     if native(master):
-        ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale, max_blocks)
+        ext().adam_update(master, grad, m, v, lowp, alpha_t, b1, b2, wd, eps, gscale, max_blocks, alpha_dev)
         return
+    if alpha_dev is not None:
+        alpha_t = float(alpha_dev.item())
     g = grad * gscale + wd * master
     m.mul_(b1).add_((1 - b1) * g)
     v.mul_(b2).add_((1 - b2) * g * g)

@@ -90,6 +90,19 @@ class StepGraph:
         # are then joined inside the graph, see step()); every decision is agreed over all ranks
         return _collectives_capturable(ex, "0")
 
+    def _full_step(self, m, ex) -> bool:
+        """Capture the optimizer update too (its overlapped per-bucket launches on the side stream
+        included): one process, Adam (its launches read the per-step alpha_t from a device scalar
+        that next() refreshes before each replay). Other optimizers and multi-rank steps keep
+        update() eager after the replay. Opt-in (FF_GRAPH_UPDATE=1): same-box A/B AlexNet 1.665-1.671
+        vs 1.670-1.682 ms, ResNet-50 7.58-7.60 vs 7.60 ms (profiles/graph_update_ab_r5.txt) — the
+        eager update after the replay was not exposed enough for the overlap to pay."""
+        import torch.distributed as dist
+        from ..core.optimizers import AdamOptimizer
+        if ex.comm.distributed or getattr(ex.comm, "force", False) or (dist.is_available() and dist.is_initialized()):
+            return False  # any process group (a forced world-1 RCCL one included): update() stays eager
+        return type(m.optimizer) is AdamOptimizer and os.environ.get("FF_GRAPH_UPDATE", "0") == "1"
+
     def step(self):
         m = self.model
         ex = m.executor
@@ -128,22 +141,38 @@ class StepGraph:
                 else:
                     self.decision = False
             return
+        full = self._full_step(m, ex)
+        just_captured = False
         if self.graph is None:
             import torch.distributed as dist
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             err = None
+            step_idx = ex.step_idx
+            if full:
+                m.optimizer.use_device_alpha(ex.device)  # allocated outside the capture
             try:
                 with torch.cuda.graph(g):
                     ex.zero_gradients()
                     ex.forward()
-                    ex.backward()
-                    if ex.comm.distributed:
-                        # every bucket all-reduce is issued and joined back into the captured
-                        # stream, so update() after a replay finds final gradients and no handle
-                        ex.bucketer.flush()
+                    if full:
+                        # the whole step: the overlapped per-bucket update and the rest of update();
+                        # next() runs on the host before every replay (alpha_dev), not in the graph
+                        ex.backward(overlap_update=ov)
+                        ex._opt_next_done = m.optimizer
+                        ex.update(m.optimizer)
+                    else:
+                        ex.backward()
+                        if ex.comm.distributed:
+                            # every bucket all-reduce is issued and joined back into the captured
+                            # stream, so update() after a replay finds final gradients and no handle
+                            ex.bucketer.flush()
             except Exception as e:  # noqa: BLE001 - any capture error falls back to eager
                 err = e
+                ex.step_idx = step_idx
+                ex._opt_next_done = None
+                ex._overlap_active = False
+                ex._upd_done = set()
             # capture success is agreed over the world: a rank replaying its graph while a peer
             # runs eagerly would issue its collectives in a different order
             ok = _agree(ex, 0.0 if err is not None else 1.0, dist.ReduceOp.MIN) > 0.5
@@ -159,13 +188,20 @@ class StepGraph:
                 ex.update(m.optimizer)
                 return
             self.graph = g
+            just_captured = True
         timed = self.decision == "trial" and self.trial >= 1  # the first replay pays first-use costs
         if timed:
             torch.cuda.synchronize()
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record()
-        self.graph.replay()
-        ex.update(m.optimizer)
+        if full:
+            m.optimizer.next()  # alpha_t of this step into the device scalar the graph reads
+            self.graph.replay()
+            if not just_captured:  # the captured update() already counted the capturing step
+                ex.step_idx += 1
+        else:
+            self.graph.replay()
+            ex.update(m.optimizer)
         if self.decision == "trial":
             self.trial += 1
             if timed:
