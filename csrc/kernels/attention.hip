@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
 // (708 -> 725-740 TF/s at B32 H16 S512, 794 -> 840 at S4096), -1..7 % at S = 256; taking the row
 // sums on the matrix core (ones x P^T) as well did not help. Bitwise equal to the 4-wave kernel.
 // D = 64; the default for Sq >= 512 (variant 3).
-template <bool MASK, bool PRIO = false>
+template <bool MASK, bool PRIO = false, bool KPRE = false>
 __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
   constexpr int D = 64, KV = 64, QB = 2, ROWS = 4 * 32 * QB;
   constexpr int TB = KV * D * 2;
@@ -410,15 +410,33 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (KPRE) {
+      // KPRE: all 8 K fragments of the tile requested before the first S MFMA (the compiler's
+      // schedule keeps only two reads ahead and waits for each pair)
+      bf16x8 kfr[D / 16][2];
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s)
+      for (int s = 0; s < D / 16; ++s)
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+        for (int kt = 0; kt < 2; ++kt) kfr[s][kt] = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb)
-          sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
-      }
+      for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[s][kt], qf[qb][s], sacc[qb][kt], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
+        }
+    }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     const int kbase = t * KV;
     bf16x8 pf[QB][2][2];
@@ -2113,10 +2131,12 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   }
   // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
   // (half the workgroups), profiles/attn_fwd_variants_r4.txt
-  if ((attn_fwd_variant() == 3 || attn_fwd_variant() == 5) && dma_ok && a.D == 64 && a.Sq >= 512) {
+  if ((attn_fwd_variant() == 3 || attn_fwd_variant() == 5 || attn_fwd_variant() == 6) && dma_ok && a.D == 64 &&
+      a.Sq >= 512) {
     const dim3 g3((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
     if (mask) hipLaunchKernelGGL((attn_fwd2_kernel<true>), g3, dim3(256), 0, st, a);
     else if (attn_fwd_variant() == 5) hipLaunchKernelGGL((attn_fwd2_kernel<false, true>), g3, dim3(256), 0, st, a);
+    else if (attn_fwd_variant() == 6) hipLaunchKernelGGL((attn_fwd2_kernel<false, false, true>), g3, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd2_kernel<false>), g3, dim3(256), 0, st, a);
     return;
   }

@@ -39,7 +39,7 @@ def timed(fn):
 fl_f = 4.0 * B * H * S * S * D
 # forward structures (0: registers, 1: LDS-DMA, 2: ping-pong, 3: 64 rows/wave, 4: persistent), interleaved
 default_fwd = X.attn_fwd_variant()
-FV = (0, 1, 2, 3, 4, 5)
+FV = (0, 1, 2, 3, 4, 5, 6)
 fres, fouts = {v: [] for v in FV}, {}
 for rnd in range(3):
     for var in FV:

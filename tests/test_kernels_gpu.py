@@ -232,7 +232,7 @@ def test_flash_attention(ffC, S, D, causal, variant):
     # priority 1) run the same per-row
     # arithmetic: bitwise equal
     prev_fwd = ffC.attn_fwd_variant()
-    for fv in (0, 1, 2, 3, 4, 5):
+    for fv in (0, 1, 2, 3, 4, 5, 6):
         ffC.attn_set_fwd_variant(fv)
         o2, lse2 = torch.full_like(o, 3.0), torch.full_like(lse, 3.0)
         ffC.attn_fwd(q, st, k, st, v, st, o2, st, lse2, B, H, S, S, D, scale, causal)
