@@ -1527,87 +1527,87 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
   };
   // hook(stage): stage 2 qt after the S / dP MFMAs, 2 qt + 1 after the dV / dK MFMAs of half qt
   auto s_tile = [&](int t, auto hook) {
-      const int qbase = t * QT;
-      const char* tb = smem + (t & 1) * TILE;
-      const char* q_l = tb;
-      const char* do_l = tb + QB;
-      const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
-      const float* dl_l = lse_l + QT;
-      char* ds_l = ds0 + (t & 1) * DS;
+    const int qbase = t * QT;
+    const char* tb = smem + (t & 1) * TILE;
+    const char* q_l = tb;
+    const char* do_l = tb + QB;
+    const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
+    const float* dl_l = lse_l + QT;
+    char* ds_l = ds0 + (t & 1) * DS;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        f32x16 sacc = f32x16{}, pacc = f32x16{};
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 sacc = f32x16{}, pacc = f32x16{};
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          const int row = 32 * qt + (lane & 31);
-          const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
-          const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
-          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
-        }
-        hook(2 * qt);
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
-          const float lv[4] = {L4.x, L4.y, L4.z, L4.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = fast_exp2(sacc[4 * g4 + j] * sl2 - lv[j]);
-        }
-        if (MASK) {
-          const bool need = (kb0 + wave * 32 + 31 >= a.Sk) || (a.causal && kb0 + wave * 32 + 31 > qbase + 32 * qt);
-          if (need) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-              if (key >= a.Sk || (a.causal && key > q)) sacc[r] = 0.f;
-            }
-          }
-        }
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 D4 = *reinterpret_cast<const float4*>(dl_l + 32 * qt + 8 * g4 + 4 * h);
-          const float dv4[4] = {D4.x, D4.y, D4.z, D4.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pacc[4 * g4 + j] = sacc[4 * g4 + j] * (pacc[4 * g4 + j] - dv4[j]);
-        }
-        const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
-        const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt) {
-          const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
-            const bf16x8 ao = cat8(tr_read(do_l, aoff<D>(r0, col)), tr_read(do_l, aoff<D>(r0 + 8, col)));
-            const bf16x8 aq = cat8(tr_read(q_l, aoff<D>(r0, col)), tr_read(q_l, aoff<D>(r0 + 8, col)));
-            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, s2 ? pb1 : pb0, dv[dt], 0, 0, 0);
-            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, s2 ? sb1 : sb0, dk[dt], 0, 0, 0);
-          }
-        }
-        hook(2 * qt + 1);
-        const int krow = wave * 32 + (lane & 31);
-        const bf16x4 parts[4] = {sb0.lo, sb0.hi, sb1.lo, sb1.hi};
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<bf16x4*>(ds_l + dst_off(krow, 32 * qt + 8 * g + 4 * h)) = parts[g];
+      for (int s = 0; s < D / 16; ++s) {
+        const int row = 32 * qt + (lane & 31);
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
       }
-      };
+      hook(2 * qt);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
+        const float lv[4] = {L4.x, L4.y, L4.z, L4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sacc[4 * g4 + j] = fast_exp2(sacc[4 * g4 + j] * sl2 - lv[j]);
+      }
+      if (MASK) {
+        const bool need = (kb0 + wave * 32 + 31 >= a.Sk) || (a.causal && kb0 + wave * 32 + 31 > qbase + 32 * qt);
+        if (need) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= a.Sk || (a.causal && key > q)) sacc[r] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 D4 = *reinterpret_cast<const float4*>(dl_l + 32 * qt + 8 * g4 + 4 * h);
+        const float dv4[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pacc[4 * g4 + j] = sacc[4 * g4 + j] * (pacc[4 * g4 + j] - dv4[j]);
+      }
+      const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
+      const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
+          const bf16x8 ao = cat8(tr_read(do_l, aoff<D>(r0, col)), tr_read(do_l, aoff<D>(r0 + 8, col)));
+          const bf16x8 aq = cat8(tr_read(q_l, aoff<D>(r0, col)), tr_read(q_l, aoff<D>(r0 + 8, col)));
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, s2 ? pb1 : pb0, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, s2 ? sb1 : sb0, dk[dt], 0, 0, 0);
+        }
+      }
+      hook(2 * qt + 1);
+      const int krow = wave * 32 + (lane & 31);
+      const bf16x4 parts[4] = {sb0.lo, sb0.hi, sb1.lo, sb1.hi};
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<bf16x4*>(ds_l + dst_off(krow, 32 * qt + 8 * g + 4 * h)) = parts[g];
+    }
+  };
   // dQ^T (16 d x 16 queries, two tiles) = K^T . dS^T of tile t-1 over key slices [32 k0, 32 k1)
   auto dq_chunk = [&](int t, int k0, int k1) {
-      const char* dsl = ds0 + ((t - 1) & 1) * DS;
-      if (k0 == 0) dqa[0] = dqa[1] = f32x4{};
+    const char* dsl = ds0 + ((t - 1) & 1) * DS;
+    if (k0 == 0) dqa[0] = dqa[1] = f32x4{};
 #pragma unroll
-      for (int ks = k0; ks < k1; ++ks) {
-        const int kr = 32 * ks + 8 * G + qi;
-        const bf16x8 ka = cat8(tr_read(k_l, aoff<D>(kr, dq_d0 + 4 * pi)), tr_read(k_l, aoff<D>(kr + 4, dq_d0 + 4 * pi)));
+    for (int ks = k0; ks < k1; ++ks) {
+      const int kr = 32 * ks + 8 * G + qi;
+      const bf16x8 ka = cat8(tr_read(k_l, aoff<D>(kr, dq_d0 + 4 * pi)), tr_read(k_l, aoff<D>(kr + 4, dq_d0 + 4 * pi)));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int cq = dq_q0 + 16 * j + 4 * pi;
-          const bf16x8 sbq = cat8(tr_read(dsl, dst_off(kr, cq)), tr_read(dsl, dst_off(kr + 4, cq)));
-          dqa[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, sbq, dqa[j], 0, 0, 0);
-        }
+      for (int j = 0; j < 2; ++j) {
+        const int cq = dq_q0 + 16 * j + 4 * pi;
+        const bf16x8 sbq = cat8(tr_read(dsl, dst_off(kr, cq)), tr_read(dsl, dst_off(kr + 4, cq)));
+        dqa[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, sbq, dqa[j], 0, 0, 0);
       }
-      };
+    }
+  };
   auto dq_tile = [&](int t) { dq_chunk(t, 0, KB / 32); };
   // dbp (fused QKV-bias gradient, non-causal chain): column sums of the final dQ (last pass) and of
   // this block's dK / dV, as partials [B*H][2][D] (dQ, per query half of the waves) and
@@ -1616,29 +1616,29 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
   float dqs[4] = {0.f, 0.f, 0.f, 0.f};
   auto dq_store = [&](int t) {  // after the barrier: vmcnt counts stores, the next wait is a tile away
     const int pq = (t - 1) * QT;
-      int last = nkb - 1;
-      if (MASK && a.causal) last = min(last, (pq + QT - 1) / KB);
+    int last = nkb - 1;
+    if (MASK && a.causal) last = min(last, (pq + QT - 1) / KB);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int q = pq + dq_q0 + 16 * j + l16;
-        if (!MASK || q < a.Sq) {
-          f32x4 acc = dqa[j];
-          if (chain && kblk > 0) {
-            acc[0] += prevq[j].x; acc[1] += prevq[j].y; acc[2] += prevq[j].z; acc[3] += prevq[j].w;
+    for (int j = 0; j < 2; ++j) {
+      const int q = pq + dq_q0 + 16 * j + l16;
+      if (!MASK || q < a.Sq) {
+        f32x4 acc = dqa[j];
+        if (chain && kblk > 0) {
+          acc[0] += prevq[j].x; acc[1] += prevq[j].y; acc[2] += prevq[j].z; acc[3] += prevq[j].w;
+        }
+        if (chain && kblk == last) {
+          const unsigned w0 = pack_bf2(acc[0] * a.scale, acc[1] * a.scale), w1 = pack_bf2(acc[2] * a.scale, acc[3] * a.scale);
+          *reinterpret_cast<uint2*>(dQb + (int64_t)q * a.dq_ss + dq_d0 + 4 * G) = make_uint2(w0, w1);
+          if (bsum) {  // the bias gradient sums the stored (bf16) dQ, as the unfused column sum would
+            dqs[0] += __uint_as_float(w0 << 16); dqs[1] += __uint_as_float(w0 & 0xffff0000u);
+            dqs[2] += __uint_as_float(w1 << 16); dqs[3] += __uint_as_float(w1 & 0xffff0000u);
           }
-          if (chain && kblk == last) {
-            const unsigned w0 = pack_bf2(acc[0] * a.scale, acc[1] * a.scale), w1 = pack_bf2(acc[2] * a.scale, acc[3] * a.scale);
-            *reinterpret_cast<uint2*>(dQb + (int64_t)q * a.dq_ss + dq_d0 + 4 * G) = make_uint2(w0, w1);
-            if (bsum) {  // the bias gradient sums the stored (bf16) dQ, as the unfused column sum would
-              dqs[0] += __uint_as_float(w0 << 16); dqs[1] += __uint_as_float(w0 & 0xffff0000u);
-              dqs[2] += __uint_as_float(w1 << 16); dqs[3] += __uint_as_float(w1 & 0xffff0000u);
-            }
-          } else {
-            *reinterpret_cast<float4*>(dq_part + (int64_t)q * D + dq_d0 + 4 * G) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-          }
+        } else {
+          *reinterpret_cast<float4*>(dq_part + (int64_t)q * D + dq_d0 + 4 * G) = make_float4(acc[0], acc[1], acc[2], acc[3]);
         }
       }
-      };
+    }
+  };
   auto finish = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed; older dQ stores done
     lds_barrier();
