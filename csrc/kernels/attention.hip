@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256, DMA ? 4 : 2) attn_fwd_kernel(AttnArgs a) 
 // (708 -> 725-740 TF/s at B32 H16 S512, 794 -> 840 at S4096), -1..7 % at S = 256; taking the row
 // sums on the matrix core (ones x P^T) as well did not help. Bitwise equal to the 4-wave kernel.
 // D = 64; the default for Sq >= 512 (variant 3).
-template <bool MASK, bool PRIO = false, bool KPRE = false>
+template <bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
   constexpr int D = 64, KV = 64, QB = 2, ROWS = 4 * 32 * QB;
   constexpr int TB = KV * D * 2;
@@ -409,35 +409,15 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
     f32x16 sacc[QB][2];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    if constexpr (KPRE) {
-      // KPRE: all 8 K fragments of the tile requested before the first S MFMA (the compiler's
-      // schedule keeps only two reads ahead and waits for each pair)
-      bf16x8 kfr[D / 16][2];
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s)
+    for (int s = 0; s < D / 16; ++s)
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) kfr[s][kt] = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int kt = 0; kt < 2; ++kt) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int qb = 0; qb < QB; ++qb)
-            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[s][kt], qf[qb][s], sacc[qb][kt], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
-#pragma unroll
-          for (int qb = 0; qb < QB; ++qb)
-            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
-        }
-    }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        for (int qb = 0; qb < QB; ++qb)
+          sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
+      }
     const int kbase = t * KV;
     bf16x8 pf[QB][2][2];
 #pragma unroll
@@ -486,7 +466,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) { pf[qb][kt][0] = pack8(sacc[qb][kt], 0); pf[qb][kt][1] = pack8(sacc[qb][kt], 8); }
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -500,7 +479,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
           for (int qb = 0; qb < QB; ++qb)
             oacc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][kt][s2], oacc[qb][dt], 0, 0, 0);
         }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -1057,12 +1035,10 @@ __device__ __forceinline__ unsigned pack_bf2(float x, float y) {
 //    small batch x heads use one launch with per-key-block slabs + attn_dq_finish_kernel.
 //  * 1-D grid through xcd_remap: the key blocks of one (batch, head) share an XCD (and its L2 copy
 //    of Q / dO).
-//  * KREG: the K^T fragments of the wave's dQ tile (constant over the query loop) are read from
-//    the K image once, before the loop, instead of twice per dQ MFMA — half the dQ stage's LDS reads.
 //  * DMA: the next Q / dO tile and its lse2 / delta rows go global -> LDS by buffer_load ... lds
 //    (no staging registers, no ds_write of the tile); vmcnt also counts stores, so the dQ tile's
 //    global stores are issued after the end-of-tile barrier, behind the wait for the DMA.
-template <int D, int NW, bool MASK, bool CHAIN, bool KREG = false, bool DMA = false>
+template <int D, int NW, bool MASK, bool CHAIN, bool DMA = false>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, int nkb, int pass) {
   constexpr int NT = 64 * NW;
   constexpr int QT = 64;       // queries per loop step
@@ -1130,23 +1106,6 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
-  // KREG (one dQ tile per wave: NW >= NTILE): A-operand K^T fragments of this wave's (dt, key part)
-  constexpr int NTILE_ = 2 * (D / 32);
-  constexpr int KSPLIT_ = NW > NTILE_ ? NW / NTILE_ : 1;
-  constexpr int KS_PER_ = KB / 16 / KSPLIT_;
-  static_assert(!KREG || NW >= NTILE_, "KREG needs one dQ tile per wave");
-  bf16x8 kq[KREG ? KS_PER_ : 1];
-  if constexpr (KREG) {
-    const int G_ = lane >> 4, qi_ = (lane & 15) >> 2, pi_ = lane & 3;
-    const int dt = (wave % NTILE_) % (D / 32), part = KSPLIT_ > 1 ? wave / NTILE_ : 0;
-    const int cd = 32 * dt + 16 * (G_ & 1) + 4 * pi_;
-#pragma unroll
-    for (int i = 0; i < KS_PER_; ++i) {
-      const int kr = 16 * (part * KS_PER_ + i) + 8 * h + qi_;
-      kq[i] = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
-    }
-  }
-
   const int qt_begin = (MASK && a.causal) ? kb0 / QT : 0;
   const int nqt = (a.Sq + QT - 1) / QT;
   const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
@@ -1344,13 +1303,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
         const int kr = 16 * ks + 8 * h + qi;
         const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
         const bf16x8 af = cat8(tr_read(ds_l, dst_off(kr, cq)), tr_read(ds_l, dst_off(kr + 4, cq)));
-        bf16x8 bk;
-        if constexpr (KREG) {
-          bk = kq[ks - part * KS_PER];
-        } else {
-          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
-          bk = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
-        }
+        const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
+        const bf16x8 bk = cat8(tr_read(k_l, aoff<D>(kr, cd)), tr_read(k_l, aoff<D>(kr + 4, cd)));
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bk, af, acc, 0, 0, 0);
       }
       if constexpr (KSPLIT > 1) {
@@ -1436,7 +1390,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
 // not depend on its S / dP work of the same iteration. dQ^T runs on 16x16x32 MFMAs: 16 (d x query)
 // tiles of 16 x 16, two per wave sharing the K^T operand, each over all KB keys, so no wave hands
 // a partial sum to another (no exchange buffer: the second dS^T image takes its LDS).
-template <bool MASK, bool CHAIN, bool SB = false, bool PRIO = false>
+template <bool MASK, bool CHAIN, bool SB = false>
 __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb, int pass) {
   constexpr int D = 64, NW = 8, NT = 64 * NW, QT = 64, KB = 32 * NW, QB = QT * D * 2;
   constexpr int TILE = 2 * QB + 2 * QT * 4;  // Q tile, dO tile, lse2, delta
@@ -1643,11 +1597,6 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed; older dQ stores done
     lds_barrier();
   };
-  // PRIO: the younger half of the workgroup (waves 4-7) at priority 1 for the whole loop, so it
-  // does not lose VALU arbitration to the older half at every segment start (guide T5, static form)
-  if constexpr (PRIO) {
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
   if (qt_begin < nqt) {
     if (qt_begin + 1 < nqt) dma_rows(qt_begin + 1);
     s_tile(qt_begin, [](int) {});
@@ -2042,12 +1991,14 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
 // attn_bwd_kernel with 8 waves x 32 keys at D = 64 (4 at D = 128), chained launches when B*H
 // workgroups fill the chip (>= 256) or there is one key block, else slabs; 3 = variant 2 always
 // chained; 4 = variant 2 always with slabs; 5 = 4 waves x 32 keys chained (two independent
-// workgroups per CU instead of one 8-wave workgroup); 6 = variant 2 with KREG (D = 64); 7 = variant
-// 2 with DMA; 8 = variant 2 with KREG and DMA; 9 = attn_bwd1b_kernel (one barrier per query tile);
-// 10 (default) = attn_bwd1b_kernel with its dQ chunks fenced between the S / dP and dV / dK stages
-// when chained (B*H >= 256), else variant 7; without 16-B aligned Q / dO rows the DMA variants
-// fall back to variant 2 (B32 H16 S512 D64: 2 / 7 / 9 / 10 = 162 / 158 / 155 / 154 us,
-// profiles/attn_bwd_r5.txt). Settable for A/B runs in one process
+// workgroups per CU instead of one 8-wave workgroup); 7 = variant 2 with DMA; 9 = attn_bwd1b_kernel
+// (one barrier per query tile); 10 (default) = attn_bwd1b_kernel with its dQ chunks fenced between
+// the S / dP and dV / dK stages when chained (B*H >= 256), else variant 7; without 16-B aligned Q /
+// dO rows the DMA variants fall back to variant 2 (B32 H16 S512 D64: 2 / 7 / 9 / 10 = 161 / 156 /
+// 156 / 151 us, profiles/attn_bwd_r5.txt). Variants measured and removed in round 5: K^T dQ
+// fragments in registers (spilled), a static priority for the younger wave half (null); forward:
+// MFMA clusters at priority 1, all K fragments requested before the S MFMAs (both null,
+// docs/PERFORMANCE.md). Settable for A/B runs in one process
 // (attn_set_bwd_variant); default from FF_ATTN_BWD.
 static int g_bwd_variant = -1;
 int attn_bwd_variant() {
@@ -2131,12 +2082,9 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   }
   // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
   // (half the workgroups), profiles/attn_fwd_variants_r4.txt
-  if ((attn_fwd_variant() == 3 || attn_fwd_variant() == 5 || attn_fwd_variant() == 6) && dma_ok && a.D == 64 &&
-      a.Sq >= 512) {
+  if (attn_fwd_variant() == 3 && dma_ok && a.D == 64 && a.Sq >= 512) {
     const dim3 g3((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
     if (mask) hipLaunchKernelGGL((attn_fwd2_kernel<true>), g3, dim3(256), 0, st, a);
-    else if (attn_fwd_variant() == 5) hipLaunchKernelGGL((attn_fwd2_kernel<false, true>), g3, dim3(256), 0, st, a);
-    else if (attn_fwd_variant() == 6) hipLaunchKernelGGL((attn_fwd2_kernel<false, false, true>), g3, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd2_kernel<false>), g3, dim3(256), 0, st, a);
     return;
   }
@@ -2162,18 +2110,18 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
   }
 }
 
-template <int D, int NW, bool KREG = false, bool DMA = false>
+template <int D, int NW, bool DMA = false>
 static void launch_bwd_main(AttnArgs a, int nkb, bool chain, hipStream_t st) {
   const bool mask = a.causal || a.Sk % (32 * NW) != 0 || a.Sq % 64 != 0;
   const int bh = a.B * a.H;
   if (chain) {
     for (int p = 0; p < nkb; ++p) {
-      if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, true, KREG, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
-      else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, true, KREG, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+      if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, true, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
+      else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, true, DMA>), dim3(bh), dim3(64 * NW), 0, st, a, nkb, p);
     }
   } else {
-    if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, false, KREG, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
-    else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, false, KREG, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+    if (mask) hipLaunchKernelGGL((attn_bwd_kernel<D, NW, true, false, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
+    else hipLaunchKernelGGL((attn_bwd_kernel<D, NW, false, false, DMA>), dim3(bh * nkb), dim3(64 * NW), 0, st, a, nkb, 0);
   }
 }
 
@@ -2186,7 +2134,7 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
   const dim3 gfin(ew_grid(per / 4, 256));
   // (every attn_bwd_kernel launch with a single key block writes the final dQ itself)
-  const bool chain = v == 3 || v == 5 || ((v == 2 || v >= 6) && a.B * a.H >= 256);
+  const bool chain = v == 3 || v == 5 || ((v == 2 || v >= 7) && a.B * a.H >= 256);
   const bool finish = v == 1 || (!chain && nkb > 1);
   // the DMA variants need 16-B aligned Q / dO rows and buffer offsets below 2 GiB
   const bool dma_ok = ((uintptr_t)a.q & 15) == 0 && ((uintptr_t)a.dout & 15) == 0 && a.q_ss % 8 == 0 &&
@@ -2196,9 +2144,7 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
     hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
     if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<64, 2>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
     else if (v == 0 || v == 5) launch_bwd_main<64, 4>(a, nkb, v == 5, st);
-    else if (v == 6) launch_bwd_main<64, 8, true>(a, nkb, chain, st);
-    else if (v == 8 && dma_ok) launch_bwd_main<64, 8, true, true>(a, nkb, chain, st);
-    else if ((v == 9 || ((v == 10 || v == 11) && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
+    else if ((v == 9 || (v == 10 && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
       const bool m = a.causal || a.Sk % 256 != 0 || a.Sq % 64 != 0;
       const int bh = a.B * a.H;
       // fused bias-gradient sums: chained and non-causal (every query tile's last key block is
@@ -2209,7 +2155,6 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
         for (int p = 0; p < nkb; ++p) {
           if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
           else if (v == 10) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
-          else if (v == 11) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
           else hipLaunchKernelGGL((attn_bwd1b_kernel<false, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
         }
       } else {
@@ -2217,7 +2162,7 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
         else hipLaunchKernelGGL((attn_bwd1b_kernel<false, false>), dim3(bh * nkb), dim3(512), 0, st, a, nkb, 0);
       }
     }
-    else if ((v == 7 || v == 10) && dma_ok) launch_bwd_main<64, 8, false, true>(a, nkb, chain, st);
+    else if ((v == 7 || v == 10) && dma_ok) launch_bwd_main<64, 8, true>(a, nkb, chain, st);
     else launch_bwd_main<64, 8>(a, nkb, chain, st);
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
   } else if (a.D == 128) {
