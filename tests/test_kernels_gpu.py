@@ -316,7 +316,8 @@ def test_flash_attention_bwd_default_chain(ffC):
         assert _rel(dqkv[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
 
 
-@pytest.mark.parametrize("S,causal,fused", [(512, False, True), (448, False, True), (512, True, False)])
+@pytest.mark.parametrize("S,causal,fused", [(512, False, True), (448, False, True), (512, True, False),
+                                             (448, True, False)])
 def test_flash_attention_fused_qkv_bias_grad(ffC, S, causal, fused):
     """The chained non-causal backward adds the fused QKV projection's bias gradient (column sums of
     dq / dk / dv, bf16 as stored) into dbias itself and says so; causal: it declines (False) and
@@ -340,6 +341,12 @@ def test_flash_attention_fused_qkv_bias_grad(ffC, S, causal, fused):
                         g[2 * H * D:], sq, wsg[:n], B, H, S, S, D, 0.125, causal, dbias)
     assert done == fused
     assert torch.equal(wsg[n:], torch.full_like(wsg[n:], 7.0)), "attn_bwd wrote past its workspace"
+    # the chained attn_bwd1b_kernel itself (incl. its causal / ragged forms) against fp32 autograd
+    q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3).float().requires_grad_() for i in range(3))
+    ref, _ = _attn_ref(q, k, v, 0.125, causal)
+    ref.backward(do.permute(0, 2, 1, 3).float())
+    for i, t in enumerate((q, k, v)):
+        assert _rel(dqkv[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
     if fused:
         ref = dqkv.float().sum(dim=(0, 1)).reshape(-1) + 0.5
         assert torch.allclose(dbias, ref, rtol=1e-4, atol=1e-2), (dbias - ref).abs().max()
