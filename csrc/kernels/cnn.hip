@@ -887,6 +887,133 @@ __global__ void __launch_bounds__(256) pool_bwd_nhwc_kernel(const bf16_t* __rest
   }
 }
 
+// 3 x 3 / stride 1 / pad 1 average pooling, channel-last (Inception's branch pools): one thread
+// per (image, column, 8-channel chunk) walks the rows with a sliding window of three row sums,
+// so each input row is loaded once per thread (its 3 horizontal taps, neighbours' loads hitting
+// the L1) instead of 9 taps per output from L2. Backward: the same window over dy / divisor
+// (relu: dy only where the output was positive). Divisor = 9 with the pad counted, else
+// (valid rows) x (valid columns).
+__device__ __forceinline__ float avg3_cnt(int i, int n) { return (float)(3 - (i == 0) - (i == n - 1)); }
+
+__global__ void __launch_bounds__(256) pool_avg3s1_fwd_nhwc_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                   int N, int C, int H, int W, int include_pad,
+                                                                   int relu) {
+  const int C8 = C / 8;
+  const unsigned total = (unsigned)N * W * C8;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c8 = (int)(e % (unsigned)C8);
+    const unsigned t = e / (unsigned)C8;
+    const int w = (int)(t % (unsigned)W), n = (int)(t / (unsigned)W);
+    const bf16_t* xp = x + (size_t)n * H * W * C + c8 * 8;
+    bf16_t* yp = y + (size_t)n * H * W * C + c8 * 8;
+    auto rowsum = [&](int h, float* r) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = 0.f;
+#pragma unroll
+      for (int dw = -1; dw <= 1; ++dw) {
+        const int ww = w + dw;
+        if (ww < 0 || ww >= W) continue;
+        float v[8];
+        ld8(xp + ((size_t)h * W + ww) * C, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += v[k];
+      }
+    };
+    float rm[8], r0[8], rp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rm[k] = 0.f;
+    rowsum(0, r0);
+    const float cw = include_pad ? 3.f : avg3_cnt(w, W);
+    for (int h = 0; h < H; ++h) {
+      if (h + 1 < H) rowsum(h + 1, rp);
+      else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rp[k] = 0.f;
+      }
+      const float inv = 1.f / ((include_pad ? 3.f : avg3_cnt(h, H)) * cw);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o[k] = (rm[k] + r0[k] + rp[k]) * inv;
+        if (relu) o[k] = fmaxf(o[k], 0.f);
+        rm[k] = r0[k];
+        r0[k] = rp[k];
+      }
+      st8(yp + ((size_t)h * W + w) * C, o);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) pool_avg3s1_bwd_nhwc_kernel(const bf16_t* __restrict__ y,
+                                                                   const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                                                   int N, int C, int H, int W, int include_pad,
+                                                                   int relu) {
+  const int C8 = C / 8;
+  const unsigned total = (unsigned)N * W * C8;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c8 = (int)(e % (unsigned)C8);
+    const unsigned t = e / (unsigned)C8;
+    const int w = (int)(t % (unsigned)W), n = (int)(t / (unsigned)W);
+    const size_t base = (size_t)n * H * W * C + c8 * 8;
+    // T(oh) = sum over the covering columns ow of dy(oh, ow) / div(oh, ow) (relu-masked)
+    auto rowterm = [&](int oh, float* r) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = 0.f;
+      const float rh = include_pad ? 3.f : avg3_cnt(oh, H);
+#pragma unroll
+      for (int dw = -1; dw <= 1; ++dw) {
+        const int ow = w + dw;
+        if (ow < 0 || ow >= W) continue;
+        const float inv = 1.f / (rh * (include_pad ? 3.f : avg3_cnt(ow, W)));
+        float d[8];
+        ld8(dy + base + ((size_t)oh * W + ow) * C, d);
+        if (relu) {
+          float yv[8];
+          ld8(y + base + ((size_t)oh * W + ow) * C, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) r[k] += yv[k] > 0.f ? d[k] * inv : 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) r[k] += d[k] * inv;
+        }
+      }
+    };
+    float rm[8], r0[8], rp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rm[k] = 0.f;
+    rowterm(0, r0);
+    for (int h = 0; h < H; ++h) {
+      if (h + 1 < H) rowterm(h + 1, rp);
+      else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rp[k] = 0.f;
+      }
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o[k] = rm[k] + r0[k] + rp[k];
+        rm[k] = r0[k];
+        r0[k] = rp[k];
+      }
+      st8(dx + base + ((size_t)h * W + w) * C, o);
+    }
+  }
+}
+
+// FF_POOL_SLIDE=0: the generic channel-last pooling kernels for 3 x 3 / s1 / p1 average pools too
+static bool pool_slide_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FF_POOL_SLIDE");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+static bool avg3s1(const PoolGeom& p, int is_max) {
+  return !is_max && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.ph == 1 && p.pw == 1 && p.ph1 == 1 &&
+         p.pw1 == 1 && p.OH == p.H && p.OW == p.W && p.C % 8 == 0 && pool_slide_on();
+}
+
 void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, int is_max, int include_pad, int relu,
                 int nhwc, hipStream_t st) {
   const PoolGeom p{geom[0], geom[1], geom[2], geom[3], geom[4],  geom[5],  geom[6],
@@ -896,6 +1023,12 @@ void pool2d_fwd(int dt, const void* x, void* y, uint8_t* idx, const int* geom, i
   if (total >= (1ll << 31) || (int64_t)p.N * p.C * p.H * p.W >= (1ll << 31))
     throw std::runtime_error("pool2d: tensors of 2^31 or more elements are not supported");
   if (nhwc) {
+    if (avg3s1(p, is_max)) {
+      const int64_t nt = (int64_t)p.N * p.W * (p.C / 8);
+      hipLaunchKernelGGL(pool_avg3s1_fwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 16384)),
+                         dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, p.N, p.C, p.H, p.W, include_pad, relu);
+      return;
+    }
     const int64_t n8 = total / 8;
     hipLaunchKernelGGL(pool_fwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 16384)), dim3(256), 0,
                        st, (const bf16_t*)x, (bf16_t*)y, idx, p, is_max, include_pad, relu);
@@ -913,6 +1046,13 @@ void pool2d_bwd(int dt, const void* x, const void* y, const void* dy, const uint
   if (total == 0) return;
   if (nhwc) {
     if (total >= (1ll << 31)) throw std::runtime_error("pool2d: tensors of 2^31 or more elements are not supported");
+    if (avg3s1(p, is_max) && (!relu || y)) {
+      const int64_t nt = (int64_t)p.N * p.W * (p.C / 8);
+      hipLaunchKernelGGL(pool_avg3s1_bwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 16384)),
+                         dim3(256), 0, st, (const bf16_t*)y, (const bf16_t*)dy, (bf16_t*)dx, p.N, p.C, p.H, p.W,
+                         include_pad, relu);
+      return;
+    }
     const int64_t n8 = total / 8;
     hipLaunchKernelGGL(pool_bwd_nhwc_kernel, dim3((unsigned)std::min<int64_t>((n8 + 255) / 256, 16384)), dim3(256), 0,
                        st, (const bf16_t*)x, (const bf16_t*)y, (const bf16_t*)dy, idx, (bf16_t*)dx, p, is_max,
