@@ -1680,7 +1680,9 @@ def _conv2d_bwd_dact(x, w, dy, g, dw, wpack, dact):
     if not (native(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16):
         return None
     cg = g[1] // g[13]
-    if cg % 8 or not (is_nhwc(x) and is_nhwc(yp)) or yp.shape != x.shape or yp.dtype != torch.bfloat16:
+    # the same predicate conv2d_bwd's x_nhwc flag is built from (_nhwc_flag): the C++ side applies
+    # the mask only on that path and refuses a dmask otherwise
+    if not (_nhwc_flag(x, cg) and is_nhwc(yp)) or yp.shape != x.shape or yp.dtype != torch.bfloat16:
         return None
     if dbp is not None and (dbp.dtype != torch.float32 or dbp.numel() != g[1]):
         return None

@@ -17,6 +17,8 @@ from ..parallel import boxcopy
 from ..type import DataType, OperatorType
 from .base import OpImpl, register
 
+_CHECK_INDICES = os.environ.get("FF_CHECK_INDICES", "0") == "1"
+
 
 @register(OperatorType.OP_INPUT)
 class Input(OpImpl):
@@ -330,6 +332,10 @@ class Gather(OpImpl):
         ctx.saved.update(shape=x.shape, idx=idx)
         g = self._geom(tuple(x.shape), x.dtype, x.is_cuda, idx)
         if g is not None:
+            # the HIP kernels clamp an out-of-range index into [0, xd) (no out-of-bounds access)
+            # where torch.gather raises; FF_CHECK_INDICES=1 restores the error (one device sync)
+            if _CHECK_INDICES and bool(((idx < 0) | (idx >= g[2])).any()):
+                raise IndexError(f"gather: index out of range for dim size {g[2]}")
             out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
             K.ext().gather_fwd(x.contiguous(), idx.contiguous(), out, *g)
             return [out]

@@ -73,7 +73,7 @@ class BoxPlan:
     srcs: one tensor or a list of up to 16 (a box reads srcs[src_index]); a source stride may be
     negative (Reverse: the box walks that dim backwards from src_off)."""
 
-    def __init__(self, boxes, srcs, dst: torch.Tensor):
+    def __init__(self, boxes, srcs, dst: torch.Tensor, disjoint_dst: bool = False):
         srcs = list(srcs) if isinstance(srcs, (list, tuple)) else [srcs]
         if not 1 <= len(srcs) <= _MAX_SRCS:
             raise ValueError("box_copy: 1..16 source tensors")
@@ -82,6 +82,7 @@ class BoxPlan:
         self.dims = []
         spans = [_span(t) for t in srcs]
         dspan = _span(dst)
+        dspans = []
         for bx in boxes:
             so, ss, do, ds, ext = bx[:5]
             si = bx[5] if len(bx) > 5 else 0
@@ -102,6 +103,7 @@ class BoxPlan:
             if lo_s < 0 or lo_d < 0 or hi_s >= spans[si] or hi_d >= dspan:
                 raise ValueError(f"box_copy: box {so}/{do} {ext} outside its tensors ({spans[si]}, {dspan})")
             self.dims.append((si, so, do, dims))
+            dspans.append((lo_d, hi_d))
         if len(self.dims) > _MAX_BOXES:
             raise ValueError("box_copy: too many boxes for one launch")
         self.vec = 1
@@ -115,12 +117,31 @@ class BoxPlan:
                 break
         self._desc: Dict[tuple, torch.Tensor] = {}
         self.device = dst.device
+        # Add mode read-modify-writes dst without atomics (one workgroup row per box), so boxes whose
+        # destinations may overlap go to different launches: layers of boxes with pairwise-disjoint
+        # destination element spans (first fit). disjoint_dst=True: the caller guarantees disjoint
+        # destination regions (comm.py layers by exact region test), one launch.
+        if disjoint_dst:
+            self.add_layers = [list(range(len(self.dims)))]
+        else:
+            self.add_layers, ends = [], []
+            for i in sorted(range(len(dspans)), key=lambda i: dspans[i]):
+                lo, hi = dspans[i]
+                for li, end in enumerate(ends):
+                    if lo > end:
+                        self.add_layers[li].append(i)
+                        ends[li] = hi
+                        break
+                else:
+                    self.add_layers.append([i])
+                    ends.append(hi)
 
-    def _descriptors(self, v: int):
-        key = (v,)
+    def _descriptors(self, v: int, layer=None):
+        key = (v, layer)
         if key not in self._desc:
             rows, mx = [], 0
-            for si, so, do, dims in self.dims:
+            sel = self.dims if layer is None else [self.dims[i] for i in self.add_layers[layer]]
+            for si, so, do, dims in sel:
                 ext = [e for e, _, _ in dims]
                 ss = [a for _, a, _ in dims]
                 ds = [b for _, _, b in dims]
@@ -135,7 +156,9 @@ class BoxPlan:
             t = torch.tensor(rows if rows else [[0] * _WORDS], dtype=torch.int64).to(self.device)
             # 32-bit index math in the kernel when every reachable offset and box size fits
             lim = (1 << 31) - 1
-            idx32 = all(abs(x) < lim for r in rows for x in r) and all(
+            # (the kernel's grid-stride counter also stays below 2^31: max box + one whole grid,
+            # at most 8192 blocks x 256 threads, box_copy in transfer.hip)
+            idx32 = mx + 8192 * 256 < lim and all(abs(x) < lim for r in rows for x in r) and all(
                 max(r[1], r[2]) + sum((r[4 + k] - 1) * max(abs(r[4 + _DIMS + k]), abs(r[4 + 2 * _DIMS + k]))
                                       for k in range(_DIMS)) < lim for r in rows)
             self._desc[key] = (t, mx, idx32)
@@ -172,8 +195,13 @@ class BoxPlan:
         vb = v * self.elem
         if not add and (dst.data_ptr() % vb or any(t.data_ptr() % vb for t in srcs)):
             v, vb = 1, self.elem
+        if add:
+            for li, lay in enumerate(self.add_layers):
+                desc, mx, idx32 = self._descriptors(v, li)
+                K.ext().box_copy(srcs, dst, desc, len(lay), mx, vb, True, False)
+            return dst
         desc, mx, idx32 = self._descriptors(v)
-        K.ext().box_copy(srcs, dst, desc, len(self.dims), mx, vb, add, idx32 and not add)
+        K.ext().box_copy(srcs, dst, desc, len(self.dims), mx, vb, add, idx32)
         return dst
 
 

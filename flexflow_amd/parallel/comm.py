@@ -499,12 +499,12 @@ class Transfer:
 
 
     # ------------------------------------------------------------------ box-copy kernels (GPU)
-    def _box_plan(self, role, src, dst, build):
+    def _box_plan(self, role, src, dst, build, disjoint_dst=False):
         """The cached BoxPlan of one side of this transfer for these tensor geometries."""
         plans = self.__dict__.setdefault("_plans", {})
         key = boxcopy.plan_key(role, src, dst)
         if key not in plans:
-            plans[key] = boxcopy.BoxPlan(build(), src, dst)
+            plans[key] = boxcopy.BoxPlan(build(), src, dst, disjoint_dst=disjoint_dst)
         return plans[key]
 
     def _generic_boxes(self, comm, x, out, ref):
@@ -523,11 +523,13 @@ class Transfer:
                 recvs.append(it)
         for mode in (False, True):
             loc = [it for it in local if bool(it.reduce) == mode]
-            if loc:
-                self._box_plan(f"local{int(mode)}", x, out, lambda loc=loc: [
+            # add mode: one launch per layer of pairwise-disjoint destination regions (the add kernel
+            # read-modify-writes dst with no atomics, so two boxes on one region would race)
+            for li, lay in enumerate(_disjoint_layers(loc) if mode else ([loc] if loc else [])):
+                self._box_plan(f"local{int(mode)}.{li}", x, out, lambda lay=lay: [
                     boxcopy.region_box(x, rel_slices_lohi(it.region, S.region(it.src_part)))[:2]
-                    + boxcopy.region_box(out, rel_slices_lohi(it.region, D.region(it.dst_part))) for it in loc
-                ]).run(x, out, add=mode)
+                    + boxcopy.region_box(out, rel_slices_lohi(it.region, D.region(it.dst_part))) for it in lay
+                ], disjoint_dst=True).run(x, out, add=mode)
         ops = []
         sbuf = None
         if sends:
@@ -556,14 +558,36 @@ class Transfer:
                     off += _numel(it.region)
                 for mode in (False, True):
                     sel = [(o, it) for o, it in zip(offs, recvs) if bool(it.reduce) == mode]
-                    if sel:
-                        self._box_plan(f"gunpack{int(mode)}", rbuf, out, lambda sel=sel: [
+                    lays = _disjoint_layers(sel, key=lambda oi: oi[1]) if mode else ([sel] if sel else [])
+                    for li, lay in enumerate(lays):
+                        self._box_plan(f"gunpack{int(mode)}.{li}", rbuf, out, lambda lay=lay: [
                             boxcopy.flat_box(o, [hi - lo for lo, hi in it.region])[:2]
                             + boxcopy.region_box(out, rel_slices_lohi(it.region, D.region(it.dst_part)))
-                            for o, it in sel]).run(rbuf, out, add=mode)
+                            for o, it in lay], disjoint_dst=True).run(rbuf, out, add=mode)
             return out
         return Pending(reqs, finish, kind="generic", nbytes=(sbuf.numel() * sbuf.element_size()) if sbuf is not None
                        else 0)
+
+
+def _regions_overlap(a, b) -> bool:
+    return all(lo1 < hi2 and lo2 < hi1 for (lo1, hi1), (lo2, hi2) in zip(a, b))
+
+
+def _disjoint_layers(items, key=lambda it: it):
+    """Greedy first-fit split of transfer items into layers whose destination regions are pairwise
+    disjoint (same destination part): each layer can be one add-mode box launch without a race.
+    Partial-sum replicas all target one region and 2-D halo gradients overlap at the corners, so
+    these plans do produce overlapping adds (layout.plan_transfer)."""
+    layers = []
+    for e in items:
+        it = key(e)
+        for lay in layers:
+            if not any(key(o).dst_part == it.dst_part and _regions_overlap(key(o).region, it.region) for o in lay):
+                lay.append(e)
+                break
+        else:
+            layers.append([e])
+    return layers
 
 
 def _numel(region) -> int:

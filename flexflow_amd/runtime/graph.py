@@ -5,11 +5,11 @@ A BERT-Large step is ~1.5k kernel launches; eager Python dispatch would dominate
 After three eager warm-up steps (so every buffer of the torch caching allocator exists), the
 zero-grad + forward + backward of one step is captured once into a hipGraph and replayed; the
 optimizer update (one fused kernel per arena, with host-side bias-corrected scalars) runs after
-the replay. Multi-rank steps are captured too (RCCL supports stream capture): the activation
-collectives and the bucketed gradient all-reduces are part of the graph, joined back into the
-captured stream before it ends; the timing decision below is agreed over all ranks.
-FF_GRAPH_COLLECTIVES=0 keeps multi-rank steps eager (backward-overlapped bucketed all-reduce),
-and a capture error falls back to eager loudly.
+the replay. Multi-rank steps are captured only on request (FF_GRAPH_COLLECTIVES=1; RCCL supports
+stream capture): the activation collectives and the bucketed gradient all-reduces are then part of
+the graph, joined back into the captured stream before it ends, and the timing decision below is
+agreed over all ranks. By default (FF_GRAPH_COLLECTIVES=0) multi-rank steps run eagerly with the
+backward-overlapped bucketed all-reduce; a capture error falls back to eager loudly.
 
 Policy (config.hip_graphs = "auto", the default): the eager warm-up steps are timed; a step whose
 GPU work is long (>= config.graph_min_step_ms, e.g. BERT-Large: 55 ms) keeps running eagerly —

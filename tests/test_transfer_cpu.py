@@ -99,3 +99,36 @@ def test_concat_backward_dense_split(monkeypatch, cl):
     for a, b in zip(outs, torch.split(dy, [3, 5, 2], 1)):
         assert torch.equal(a, b)
         assert a.is_contiguous(memory_format=torch.channels_last) if cl else a.is_contiguous()
+
+
+def test_add_boxes_are_layered_by_disjoint_destinations():
+    """overlapping add boxes must not share one launch. comm._disjoint_layers
+    splits transfer items by exact region test; BoxPlan layers any add plan by destination spans."""
+    from types import SimpleNamespace as NS
+
+    from flexflow_amd.parallel import boxcopy
+    from flexflow_amd.parallel.comm import _disjoint_layers
+    it = lambda r, q=0: NS(region=r, dst_part=q)  # noqa: E731
+    same = [it([(0, 4), (0, 6)]) for _ in range(3)]
+    lays = _disjoint_layers(same)
+    assert [len(l) for l in lays] == [1, 1, 1]
+    corners = [it([(0, 5), (0, 5)]), it([(3, 8), (0, 5)]), it([(0, 5), (3, 8)]), it([(5, 8), (5, 8)])]
+    lays = _disjoint_layers(corners)
+    for lay in lays:
+        for a in lay:
+            for b in lay:
+                assert a is b or not all(l1 < h2 and l2 < h1 for (l1, h1), (l2, h2) in zip(a.region, b.region))
+    assert sum(len(l) for l in lays) == 4 and len(lays) >= 2
+    assert len(_disjoint_layers([it([(0, 4)], 0), it([(0, 4)], 1)])) == 1  # different parts never clash
+    # BoxPlan: the same overlapping boxes, emulated on CPU, give the sequential sum; spans layered
+    x = torch.zeros(8, 8)
+    flat = torch.ones(4 * 25)
+    boxes = [boxcopy.flat_box(25 * i, (5, 5))[:2] + boxcopy.region_box(x, [(lo, lo + 5), (lo, lo + 5)])
+             for i, lo in enumerate((0, 3, 0, 3))]
+    plan = boxcopy.BoxPlan(boxes, flat, x)
+    assert len(plan.add_layers) >= 2 and sorted(i for l in plan.add_layers for i in l) == [0, 1, 2, 3]
+    plan.run(flat, x, add=True)
+    ref = torch.zeros(8, 8)
+    for lo in (0, 3, 0, 3):
+        ref[lo:lo + 5, lo:lo + 5] += 1
+    assert torch.equal(x, ref)

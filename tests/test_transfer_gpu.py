@@ -83,6 +83,32 @@ def test_add_mode_sums_partials(dtype):
     assert torch.allclose(x.float(), ref.float(), atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_add_mode_overlapping_boxes_do_not_race(dtype):
+    """Partial-sum replicas all add into ONE region and 2-D halo gradients overlap at the corners:
+    the plan splits such boxes into launches with disjoint destinations (one launch
+    read-modify-wrote the same elements from different workgroups and lost updates)."""
+    torch.manual_seed(4)
+    x = torch.randn(64, 256, device=DEV).to(dtype)
+    parts = [torch.randn(48, 192, device=DEV).to(dtype) for _ in range(6)]
+    flat = torch.cat([p.reshape(-1) for p in parts])
+    regs = [[(0, 48), (0, 192)]] * 4 + [[(16, 64), (64, 256)], [(8, 56), (32, 224)]]
+    boxes, off = [], 0
+    for r, p in zip(regs, parts):
+        boxes.append(boxcopy.flat_box(off, p.shape)[:2] + boxcopy.region_box(x, r))
+        off += p.numel()
+    ref = x.float().clone()
+    for r, p in zip(regs, parts):
+        ref[tuple(slice(lo, hi) for lo, hi in r)] += p.float()
+    plan = boxcopy.BoxPlan(boxes, flat, x)
+    assert len(plan.add_layers) >= 4
+    for _ in range(3):  # a race would lose a random subset of adds: compare every run
+        y = x.clone()
+        plan.run(flat, y, add=True)
+        tol = 1e-5 if dtype == torch.float32 else 3e-2
+        assert torch.allclose(y.float(), ref, atol=tol, rtol=tol)
+
+
 def test_out_of_range_box_is_refused_on_the_host():
     x = torch.zeros(4, 8, device=DEV)
     flat = torch.zeros(16, device=DEV)
