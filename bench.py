@@ -154,6 +154,7 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     verify = None
+    t_start = time.perf_counter()
     if world > 1 and args.search not in ("dp", "none") and args.verify_steps > 0:
         # measurement-verified search: the simulator's pick is timed against data parallel on the
         # real machine and the faster one is kept (FlexFlow's search also trusts measured op costs)
@@ -175,6 +176,7 @@ def main():
                 del ff_dp
     else:
         ff, gb, info = build(args, args.search)
+    setup_s = time.perf_counter() - t_start  # build(s) + compile + search + verification
     el = timed(ff, args.steps, args.warmup, world)
     ms = el / args.steps * 1e3
     sps = gb * args.steps / el
@@ -195,6 +197,7 @@ def main():
                         "parallelism": describe(ff, world), "search": (ff.search_report or {}).get("algo"),
                         "optimizer": args.optimizer, "params": info["params"]}, **info["extra"]),
     }
+    res["setup_s"] = round(setup_s, 1)
     sg = getattr(ff, "_step_graph", None)
     res["hip_graph"] = bool(sg is not None and sg.graph is not None)  # step replayed from a hipGraph
     if info["flops_per_sample"]:
@@ -202,7 +205,8 @@ def main():
     rep = ff.search_report or {}
     if rep.get("predicted_speedup_vs_dp") is not None:
         res["search"] = {k: rep[k] for k in ("predicted_ms", "predicted_dp_ms", "predicted_speedup_vs_dp",
-                                             "candidates", "search_s", "measured_costs") if k in rep}
+                                             "candidates", "search_s", "search_wall_s", "graphs_costed",
+                                             "timed_out", "measured_costs") if k in rep}
     if verify is not None:
         res["search_verification"] = verify
         if "dp_ms" in verify:

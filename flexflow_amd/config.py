@@ -39,6 +39,9 @@ class FFConfig:
         self.dataset_path = ""
         self.search_budget = -1
         self.search_alpha = 1.2
+        # wall-clock bound (s) of the joint graph search loop on rank 0 (the other ranks wait in a
+        # broadcast meanwhile); <= 0: unbounded. FF_SEARCH_TIME_S overrides.
+        self.search_time_s = float(os.environ.get("FF_SEARCH_TIME_S", "120"))
         self.search_overlap_backward_update = False
         self.computation_mode = CompMode.TRAINING
         self.only_data_parallel = False
@@ -142,6 +145,8 @@ class FFConfig:
                     self.dataset_path = nxt()
                 elif a in ("--budget", "--search-budget"):
                     self.search_budget = int(nxt())
+                elif a == "--search-time-s":
+                    self.search_time_s = float(nxt())
                 elif a in ("--alpha", "--search-alpha"):
                     self.search_alpha = float(nxt())
                 elif a in ("--import", "--import-strategy"):

@@ -649,7 +649,16 @@ def joint_search(model, algo: str = "unity", budget: Optional[int] = None, alpha
     evals = 1
     pops = 0
     rejected = set()  # rewrites that did not beat the graph they were applied to
+    tlimit = float(getattr(cfg, "search_time_s", 0) or 0)
+    timed_out = False
+
+    def out_of_time():
+        return tlimit > 0 and time.perf_counter() - t0 > tlimit
+
     while queue and pops < budget and evals < max_graphs:
+        if out_of_time():
+            timed_out = True
+            break
         cost, _, seq = heapq.heappop(queue)
         pops += 1
         if cost > best[0] * alpha:
@@ -659,10 +668,13 @@ def joint_search(model, algo: str = "unity", budget: Optional[int] = None, alpha
         cur = snapshot(model)
         cur_ids = {id(L) for L in model.layers}
         for x in xfers:
-            if evals >= max_graphs:
+            if evals >= max_graphs or timed_out:
                 break
             for m in x.matches(model)[:4]:
                 if evals >= max_graphs:
+                    break
+                if out_of_time():
+                    timed_out = True
                     break
                 ck = _class_key(x, m)
                 if ck in rejected:
@@ -703,6 +715,7 @@ def joint_search(model, algo: str = "unity", budget: Optional[int] = None, alpha
     rep = dict(rep)
     # the starting graph's full search result, for the report's speedup against data parallel
     rep.update({"joint": True, "graphs_costed": evals, "graphs_popped": pops, "budget": budget,
+                "time_limit_s": tlimit, "timed_out": timed_out,
                 "xfers": len(xfers), "joint_s": round(time.perf_counter() - t0, 3),
                 "rewrites": [{"xfer": n, "match": _jsonable(m)} for n, m in best[1]],
                 "start_graph_ms": round(rep0["predicted_ms"], 4),

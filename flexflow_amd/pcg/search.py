@@ -94,11 +94,17 @@ def choose_strategy(model):
             replay_broadcast(model, obj[2])
         return {k: OpConfig.from_json(v) for k, v in obj[0].items()}, obj[1]
     seq = []
+    import time
+    t0 = time.perf_counter()
     if joint:
         from .joint import joint_search
         strat, report, seq = joint_search(model, algo)
     else:
         strat, report = native_search(model, algo)
+    report = dict(report or {})
+    report["search_wall_s"] = round(time.perf_counter() - t0, 2)  # measurement + search, rank 0
+    from .costmodel import save_cost_table
+    save_cost_table()
     if distributed:
         dist.broadcast_object_list([{k: v.to_json() for k, v in strat.items()}, report, seq], src=0)
     return strat, report
