@@ -518,452 +518,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd2_kernel(AttnArgs a) {
   }
 }
 
-// ------------------------------------------------------- forward, 64 rows per wave, persistent
-// attn_fwd2_kernel's tile loop with the per-block fixed costs overlapped: two workgroups per CU
-// walk their 256-row query blocks (block = blockIdx.x, + gridDim.x, ... in xcd_remap order, so a
-// (batch, head)'s blocks stay on one XCD), the K/V tile stream continues across block seams (the
-// last tile of a block requests the next block's first tile), the next block's Q is loaded while
-// this block's O leaves through its own 32-KiB staging image, and those stores drain under the
-// next block's first tile. Why: at S = 512 one K/V tile per workgroup runs at ~1400 TF/s and eight
-// at ~650 (profiles/attn_fwd_lab_r2.txt) — the Q load, first tile and O store of every block were
-// paid by all workgroups at once. Non-causal, Sq % 256 == 0, Sk % 128 == 0, D = 64; bitwise equal to
-// attn_fwd2_kernel.
-__global__ void __launch_bounds__(256, 2) attn_fwd2p_kernel(AttnArgs a, int nblocks) {
-  constexpr int D = 64, KV = 64, QB = 2, ROWS = 256;
-  constexpr int TB = KV * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + ROWS * D * 2];
-  char* epi = smem + 4 * TB;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int nqb = a.Sq / ROWS;
-  const int nkv = a.Sk / KV;  // even
-  const int nmine = (nblocks - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const float sl2 = a.scale * LOG2E;
-  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
-  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
-
-  struct Blk {
-    int bh, b, hh, qblk0;
-  };
-  auto mk = [&](int i) {
-    Blk r;
-    const int lid = xcd_remap((int)blockIdx.x + i * (int)gridDim.x, nblocks);
-    r.bh = lid / nqb;
-    r.b = r.bh / a.H;
-    r.hh = r.bh % a.H;
-    r.qblk0 = (lid % nqb) * ROWS;
-    return r;
-  };
-  auto rsrc_k = [&](const Blk& k) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.k + (int64_t)k.b * a.k_sb + (int64_t)k.hh * a.k_sh), (short)0, kb,
-                                             0x00020000);
-  };
-  auto rsrc_v = [&](const Blk& k) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.v + (int64_t)k.b * a.v_sb + (int64_t)k.hh * a.v_sh), (short)0, vb,
-                                             0x00020000);
-  };
-  auto load_q = [&](const Blk& k, bf16x8 (&q)[QB][D / 16]) {
-    const bf16_t* Q = a.q + (int64_t)k.b * a.q_sb + (int64_t)k.hh * a.q_sh;
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const int qrow = k.qblk0 + wave * 32 * QB + 32 * qb + (lane & 31);
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-        q[qb][s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
-    }
-  };
-
-  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
-  int ko[D / 16], vo[D / 32][2][2];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
-    asm volatile("" : "+v"(ko[s]));
-  }
-#pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int hi = 0; hi < 2; ++hi) {
-        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
-        asm volatile("" : "+v"(vo[dt][s2][hi]));
-      }
-
-  Blk cur = mk(0);
-  __amdgpu_buffer_rsrc_t rk = rsrc_k(cur), rv = rsrc_v(cur);
-  bf16x8 qf[QB][D / 16];
-  load_q(cur, qf);
-  dma_tile<D, 4>(rk, smem, a.k_ss, 0, wave, lane);
-  dma_tile<D, 4>(rv, smem + TB, a.v_ss, 0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int i = 0; i < nmine; ++i) {
-    const bool has_next = i + 1 < nmine;
-    f32x16 oacc[QB][D / 32];
-    float m[QB], lsum[QB];
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-#pragma unroll
-      for (int j = 0; j < D / 32; ++j) oacc[qb][j] = f32x16{};
-      m[qb] = -INFINITY;
-      lsum[qb] = 0.f;
-    }
-    auto tile = [&](auto par, int t) {
-      constexpr int PAR = decltype(par)::value;
-      const char* kl = smem + PAR * 2 * TB;
-      const char* vl = kl + TB;
-      char* nk = smem + (PAR ^ 1) * 2 * TB;
-      // the tile stream: the next tile of this block, or the next block's first
-      bool more = true;
-      if (t + 1 < nkv) {
-        dma_tile<D, 4>(rk, nk, a.k_ss, (t + 1) * KV, wave, lane);
-        dma_tile<D, 4>(rv, nk + TB, a.v_ss, (t + 1) * KV, wave, lane);
-      } else if (has_next) {  // rk / rv move on to the next block: this one's tiles are all in LDS
-        const Blk nb = mk(i + 1);
-        rk = rsrc_k(nb);
-        rv = rsrc_v(nb);
-        dma_tile<D, 4>(rk, nk, a.k_ss, 0, wave, lane);
-        dma_tile<D, 4>(rv, nk + TB, a.v_ss, 0, wave, lane);
-      } else {
-        more = false;
-      }
-      f32x16 sacc[QB][2];
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) sacc[qb][0] = sacc[qb][1] = f32x16{};
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
-#pragma unroll
-          for (int qb = 0; qb < QB; ++qb)
-            sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], sacc[qb][kt], 0, 0, 0);
-        }
-      // this block's Q is dead after its last S tile: the next block's Q loads land in its registers
-      if (t + 1 == nkv && has_next) load_q(mk(i + 1), qf);
-      bf16x8 pf[QB][2][2];
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[qb][kt][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-        if (!__all(mx <= m[qb] + a.rescale_thr)) {
-          const float mnew = fmaxf(m[qb], mx);
-          const float alpha = fast_exp2(m[qb] - (mnew == -INFINITY ? 0.f : mnew));
-          lsum[qb] *= alpha;
-#pragma unroll
-          for (int j = 0; j < D / 32; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[qb][j][r] *= alpha;
-          m[qb] = mnew;
-        }
-        const float msafe = m[qb] == -INFINITY ? 0.f : m[qb];
-        float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = fast_exp2(__builtin_fmaf(sacc[qb][kt][r], sl2, -msafe));
-            sacc[qb][kt][r] = p;
-            if (r & 1) rs1 += p;
-            else rs0 += p;
-          }
-        float rs = rs0 + rs1;
-        rs += __shfl_xor(rs, 32, 64);
-        lsum[qb] += rs;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) { pf[qb][kt][0] = pack8(sacc[qb][kt], 0); pf[qb][kt][1] = pack8(sacc[qb][kt], 8); }
-      }
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
-            const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
-            const bf16x8 vf = cat8(lo, hi);
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-              oacc[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb][kt][s2], oacc[qb][dt], 0, 0, 0);
-          }
-      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    };
-    for (int t = 0; t < nkv; t += 2) {
-      tile(std::integral_constant<int, 0>{}, t);
-      tile(std::integral_constant<int, 1>{}, t + 1);
-    }
-    // epilogue through the block's own staging image (the K/V ring holds the next block's tile 0)
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const float inv = lsum[qb] > 0.f ? 1.f / lsum[qb] : 0.f;
-      const int row = wave * 32 * QB + 32 * qb + (lane & 31);
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = 4 * dt + g;
-          *reinterpret_cast<uint2*>(epi + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
-              make_uint2((unsigned)f2bf(oacc[qb][dt][4 * g] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 1] * inv) << 16),
-                         (unsigned)f2bf(oacc[qb][dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[qb][dt][4 * g + 3] * inv) << 16));
-        }
-      const int qrow = cur.qblk0 + wave * 32 * QB + 32 * qb + (lane & 31);
-      if (h == 0 && a.lse)
-        a.lse[(int64_t)cur.bh * a.Sq + qrow] = lsum[qb] > 0.f ? (m[qb] * LN2 + __logf(lsum[qb])) : INFINITY;
-    }
-    // LDS-only barrier: the previous block's O stores need not drain
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    {
-      constexpr int CPR = D / 8;
-      bf16_t* Ob = a.o + (int64_t)cur.b * a.o_sb + (int64_t)cur.hh * a.o_sh;
-#pragma unroll
-      for (int j = 0; j < ROWS * CPR / 256; ++j) {
-        const int id = tid + j * 256, r = id / CPR, c = id % CPR;
-        *reinterpret_cast<uint4*>(Ob + (int64_t)(cur.qblk0 + r) * a.o_ss + 8 * c) =
-            *reinterpret_cast<const uint4*>(epi + r * (D * 2) + ((c ^ (r & 7)) << 4));
-      }
-    }
-    if (!has_next) break;
-    cur = mk(i + 1);
-  }
-}
-
-// ------------------------------------------------------------------------ forward, ping-pong
-// 8 waves, 256 query rows per workgroup: group A = waves 0-3 (rows 0-127), group B = waves 4-7
-// (rows 128-255), one wave of each group per SIMD. Each K/V tile is two barrier-separated
-// segments in which the two groups do opposite work, so one wave of every SIMD issues MFMAs while
-// its partner runs the softmax VALU (cdna_hip_programming.md 'Two waves per SIMD'):
-//   segment 1 of tile t:  A: softmax(t)                   B: [P(t-1) V(t-1)], S(t) = Q K(t)^T
-//   segment 2 of tile t:  A: P(t) V(t), S(t+1)            B: softmax(t)
-// The one-group-per-segment structure of the 4-wave kernel above left the MFMA pipe idle while a
-// wave's softmax ran (its waves only overlapped by chance across workgroups). K and V slots rotate
-// independently (V(t+1) and K(t+2) are requested at the start of segment 2 of tile t, into the
-// slots their predecessors left in segment 1, and waited for at the end of segment 1 of t+1), so
-// one 32-KiB double-buffered image serves both groups. The per-wave softmax, T13 deferred max, LDS
-// images and fragment offsets are those of attn_fwd_kernel.
-// Measured (profiles/attn_fwd_pingpong_r4.txt): bitwise equal to the 4-wave kernel but 5-20 %
-// slower at D = 64 for S = 256..4096 (one or two 256-row workgroups per CU pay the per-block Q load
-// and first K/V tiles in more rounds, and each segment lasts as long as its slower group); at
-// D = 128 (spills at 128 registers) 3-4x slower, so only D = 64 is built. Opt-in: variant 2.
-template <int D, bool MASK>
-__global__ void __launch_bounds__(512, 4) attn_fwd_pp_kernel(AttnArgs a) {
-  constexpr int KV = 64;
-  constexpr int TB = KV * D * 2;
-  constexpr int QB = 256;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // K slots at 0, TB; V slots at 2TB, 3TB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const bool grpB = wave >= 4;
-  const int nqb = (a.Sq + QB - 1) / QB;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = lid / nqb, b = bh / a.H, hh = bh % a.H;
-  const int qblk0 = (lid % nqb) * QB;
-  const int q0 = qblk0 + wave * 32;
-  const int qrow = q0 + (lane & 31);
-  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
-  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
-  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
-
-  bf16x8 qf[D / 16];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (qrow < a.Sq) qf[s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * a.q_ss + 16 * s + 8 * h);
-    else qf[s] = bf16x8{};
-  }
-  f32x16 oacc[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{};
-  float m = -INFINITY, lsum = 0.f;
-  const float sl2 = a.scale * LOG2E;
-
-  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
-  int ko[D / 16], vo[D / 32][2][2];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    ko[s] = aoff<D>(lane & 31, 16 * s + 8 * h);
-    asm volatile("" : "+v"(ko[s]));
-  }
-#pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int hi = 0; hi < 2; ++hi) {
-        vo[dt][s2][hi] = aoff<D>(16 * s2 + 4 * h + qi + 8 * hi, dt * 32 + 16 * (G & 1) + 4 * pi);
-        asm volatile("" : "+v"(vo[dt][s2][hi]));
-      }
-
-  int nkv = (a.Sk + KV - 1) / KV;
-  if (a.causal) nkv = min(nkv, (min(qblk0 + QB, a.Sq) + KV - 1) / KV);
-  const int kb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.k_ss + D) * 2);
-  const int vb = (int)min((int64_t)0x7fffffff, ((int64_t)(a.Sk - 1) * a.v_ss + D) * 2);
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, kb, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, vb, 0x00020000);
-
-  f32x16 sacc[2];
-  bf16x8 pf[2][2];
-  // S(t) = Q K(t)^T from K slot KS
-  auto qk = [&](auto ks_c) __attribute__((always_inline)) {
-    constexpr int KS = decltype(ks_c)::value;
-    const char* kl = smem + KS * TB;
-    sacc[0] = f32x16{};
-    sacc[1] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + ko[s] + kt * 32 * 2 * D);
-        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kt], 0, 0, 0);
-      }
-  };
-  // O += P(t) V(t) from V slot VS
-  auto pv = [&](auto vs_c) __attribute__((always_inline)) {
-    constexpr int VS = decltype(vs_c)::value;
-    const char* vl = smem + (2 + VS) * TB;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x4 lo = tr_read(vl, vo[dt][s2][0] + kt * 32 * 2 * D);
-          const bf16x4 hi = tr_read(vl, vo[dt][s2][1] + kt * 32 * 2 * D);
-          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(lo, hi), pf[kt][s2], oacc[dt], 0, 0, 0);
-        }
-  };
-  // online softmax of sacc (tile t) -> pf
-  auto softmax = [&](int t) __attribute__((always_inline)) {
-    const int kbase = t * KV;
-    const bool need_mask = MASK && ((kbase + KV > a.Sk) || (a.causal && kbase + KV - 1 > q0));
-    if (need_mask) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kbase + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (key >= a.Sk || (a.causal && key > qrow)) sacc[kt][r] = -INFINITY;
-        }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kt][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sl2;
-    if (!__all(mx <= m + a.rescale_thr)) {
-      const float mnew = fmaxf(m, mx);
-      const float alpha = fast_exp2(m - (mnew == -INFINITY ? 0.f : mnew));
-      lsum *= alpha;
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-      m = mnew;
-    }
-    const float msafe = m == -INFINITY ? 0.f : m;
-    float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(__builtin_fmaf(sacc[kt][r], sl2, -msafe));
-        sacc[kt][r] = p;
-        if (r & 1) rs1 += p;
-        else rs0 += p;
-      }
-    float rs = rs0 + rs1;
-    rs += __shfl_xor(rs, 32, 64);
-    lsum += rs;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) { pf[kt][0] = pack8(sacc[kt], 0); pf[kt][1] = pack8(sacc[kt], 8); }
-  };
-  auto dma_k = [&](int slot, int t) __attribute__((always_inline)) {
-    dma_tile<D, 8>(rk, smem + slot * TB, a.k_ss, t * KV, wave, lane);
-  };
-  auto dma_v = [&](int slot, int t) __attribute__((always_inline)) {
-    dma_tile<D, 8>(rv, smem + (2 + slot) * TB, a.v_ss, t * KV, wave, lane);
-  };
-  auto raw_barrier = []() __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (nkv > 0) {
-    dma_k(0, 0);
-    dma_v(0, 0);
-    if (nkv > 1) dma_k(1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    raw_barrier();
-    if (!grpB) qk(std::integral_constant<int, 0>());
-  }
-  // tile t with PAR = t & 1 (K(t), V(t) in slot PAR)
-  auto tile = [&](auto par_c, int t) __attribute__((always_inline)) {
-    constexpr int PAR = decltype(par_c)::value;
-    // segment 1
-    if (!grpB) {
-      softmax(t);
-    } else {
-      if (t > 0) pv(std::integral_constant<int, PAR ^ 1>());
-      qk(std::integral_constant<int, PAR>());
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V(t) and K(t+1), requested in segment 2 of t-1
-    raw_barrier();
-    // segment 2: V(t+1) into the slot V(t-1) left, K(t+2) into K(t)'s
-    if (t + 1 < nkv) dma_v(PAR ^ 1, t + 1);
-    if (t + 2 < nkv) dma_k(PAR, t + 2);
-    if (!grpB) {
-      pv(std::integral_constant<int, PAR>());
-      if (t + 1 < nkv) qk(std::integral_constant<int, PAR ^ 1>());
-    } else {
-      softmax(t);
-    }
-    raw_barrier();
-  };
-  for (int t = 0; t < nkv; t += 2) {
-    tile(std::integral_constant<int, 0>(), t);
-    if (t + 1 < nkv) tile(std::integral_constant<int, 1>(), t + 1);
-  }
-  if (grpB && nkv > 0) {
-    if ((nkv - 1) & 1) pv(std::integral_constant<int, 1>());
-    else pv(std::integral_constant<int, 0>());
-  }
-  // epilogue: as attn_fwd_kernel, 256 rows through the (now free) 32-KiB image
-  __syncthreads();
-  {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    const int row = wave * 32 + (lane & 31);
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = 4 * dt + g;
-        *reinterpret_cast<uint2*>(smem + row * (D * 2) + ((c ^ (row & 7)) << 4) + 8 * h) =
-            make_uint2((unsigned)f2bf(oacc[dt][4 * g] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 1] * inv) << 16),
-                       (unsigned)f2bf(oacc[dt][4 * g + 2] * inv) | ((unsigned)f2bf(oacc[dt][4 * g + 3] * inv) << 16));
-      }
-    if (h == 0 && a.lse && qrow < a.Sq) a.lse[(int64_t)bh * a.Sq + qrow] = lsum > 0.f ? (m * LN2 + __logf(lsum)) : INFINITY;
-  }
-  __syncthreads();
-  {
-    constexpr int CPR = D / 8;
-    bf16_t* Ob = a.o + (int64_t)b * a.o_sb + (int64_t)hh * a.o_sh;
-#pragma unroll
-    for (int i = 0; i < QB * CPR / 512; ++i) {
-      const int id = tid + i * 512, r = id / CPR, c = id % CPR;
-      if (qblk0 + r < a.Sq)
-        *reinterpret_cast<uint4*>(Ob + (int64_t)(qblk0 + r) * a.o_ss + 8 * c) =
-            *reinterpret_cast<const uint4*>(smem + r * (D * 2) + ((c ^ (r & 7)) << 4));
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------ backward
 // delta[bh][q] = sum_d dO[q][d] * O[q][d]
 template <int D>
@@ -1382,7 +936,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_bwd_kernel(AttnArgs a, i
   }
 }
 
-// Backward, one barrier per query tile (variant 9; D = 64, 8 waves x 32 keys, LDS-DMA tiles):
+// Backward, one barrier per query tile (the default backward, variant 10; D = 64, 8 waves x 32 keys, LDS-DMA tiles):
 // attn_bwd_kernel software-pipelined over the query tiles. Iteration t computes S / dP / dV / dK
 // of tile t (its dS^T into one of two LDS images) and the dQ of tile t-1 from the other image, so
 // the one end-of-iteration barrier orders the tile buffers, both dS^T images and the DMA of tile
@@ -1728,240 +1282,6 @@ __global__ void __launch_bounds__(1024) attn_bias_fold_kernel(const float* __res
   }
 }
 
-// Backward, one wave per SIMD: each wave owns KG groups of 32 keys (KG = 2 at D = 64 -> 256 keys
-// per workgroup, so at S = 512 only two fp32 dQ partial slabs are written and re-read instead of
-// four — the slab round trip was the dominant HBM traffic of attn_bwd_kernel). The Q/dO fragment
-// reads (ds_read_b128) and the transposed dO/Q reads of the dV/dK products are shared by the KG
-// key groups, so each LDS byte feeds KG x the MFMAs. 1-D grid through the XCD remap so that the key
-// blocks of one (batch, head) run on one XCD and share its L2 copy of Q / dO / lse / delta.
-template <int D, int KG>
-__global__ void __launch_bounds__(256, 1) attn_bwd_kg_kernel(AttnArgs a, int nkb) {
-  constexpr int NW = 4, NT = 256, QT = 64;
-  constexpr int KB = 32 * KG * NW;  // keys per workgroup
-  constexpr int QB = QT * D * 2;
-  constexpr int TILE = 2 * QB + 2 * QT * 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE + KB * D * 2 + KB * QT * 2];
-  char* k_l = smem + 2 * TILE;
-  char* ds_l = k_l + KB * D * 2;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int lid = xcd_remap(blockIdx.x, nkb * a.B * a.H);
-  const int bh = lid / nkb, kblk = lid % nkb;
-  const int b = bh / a.H, hh = bh % a.H;
-  const int kb0 = kblk * KB;
-  const int kw0 = kb0 + wave * KG * 32;  // first key of this wave
-  const bf16_t* Q = a.q + (int64_t)b * a.q_sb + (int64_t)hh * a.q_sh;
-  const bf16_t* K = a.k + (int64_t)b * a.k_sb + (int64_t)hh * a.k_sh;
-  const bf16_t* V = a.v + (int64_t)b * a.v_sb + (int64_t)hh * a.v_sh;
-  const bf16_t* dO = a.dout + (int64_t)b * a.do_sb + (int64_t)hh * a.do_sh;
-  const float* LSE = a.lse + (int64_t)bh * a.Sq;
-  const float* DL = a.delta + (int64_t)bh * a.Sq;
-  const float sl2 = a.scale * LOG2E;
-
-  {
-    TileStage<D, KB, NT> st;
-    st.load(K, a.k_ss, kb0, a.Sk, tid);
-    st.store(k_l, tid);
-  }
-  bf16x8 kf[KG][D / 16], vf[KG][D / 16];
-#pragma unroll
-  for (int g = 0; g < KG; ++g) {
-    const int key = kw0 + g * 32 + (lane & 31);
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      if (key < a.Sk) {
-        kf[g][s] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * a.k_ss + 16 * s + 8 * h);
-        vf[g][s] = *reinterpret_cast<const bf16x8*>(V + (int64_t)key * a.v_ss + 16 * s + 8 * h);
-      } else {
-        kf[g][s] = bf16x8{};
-        vf[g][s] = bf16x8{};
-      }
-    }
-  }
-  f32x16 dk[KG][D / 32], dv[KG][D / 32];
-#pragma unroll
-  for (int g = 0; g < KG; ++g)
-#pragma unroll
-    for (int i = 0; i < D / 32; ++i) { dk[g][i] = f32x16{}; dv[g][i] = f32x16{}; }
-
-  const int qt_begin = a.causal ? kb0 / QT : 0;
-  const int nqt = (a.Sq + QT - 1) / QT;
-  const int G = lane >> 4, qi = (lane & 15) >> 2, pi = lane & 3;
-  float* dq_part = a.dq_acc + (int64_t)kblk * a.B * a.H * a.Sq * D + (int64_t)bh * a.Sq * D;
-
-  TileStage<D, QT, NT> sq, sd;
-  float lse_r = INFINITY, dl_r = 0.f;
-  auto fetch = [&](int t) {
-    const int qbase = t * QT;
-    sq.load(Q, a.q_ss, qbase, a.Sq, tid);
-    sd.load(dO, a.do_ss, qbase, a.Sq, tid);
-    if (tid < QT) {
-      const int q = qbase + tid;
-      lse_r = q < a.Sq ? LSE[q] * LOG2E : INFINITY;
-      dl_r = q < a.Sq ? DL[q] : 0.f;
-    }
-  };
-  auto stash = [&](int t) {
-    char* tb = smem + (t & 1) * TILE;
-    sq.store(tb, tid);
-    sd.store(tb + QB, tid);
-    if (tid < QT) {
-      reinterpret_cast<float*>(tb + 2 * QB)[tid] = lse_r;
-      reinterpret_cast<float*>(tb + 2 * QB)[QT + tid] = dl_r;
-    }
-  };
-  if (qt_begin < nqt) {
-    fetch(qt_begin);
-    stash(qt_begin);
-  }
-  __syncthreads();
-
-  for (int t = qt_begin; t < nqt; ++t) {
-    const int qbase = t * QT;
-    char* tb = smem + (t & 1) * TILE;
-    const char* q_l = tb;
-    const char* do_l = tb + QB;
-    const float* lse_l = reinterpret_cast<const float*>(tb + 2 * QB);
-    const float* dl_l = lse_l + QT;
-    const bool more = t + 1 < nqt;
-    if (more) fetch(t + 1);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      f32x16 sacc[KG], pacc[KG];
-#pragma unroll
-      for (int g = 0; g < KG; ++g) { sacc[g] = f32x16{}; pacc[g] = f32x16{}; }
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        const int row = 32 * qt + (lane & 31);
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(q_l + aoff<D>(row, 16 * s + 8 * h));
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(do_l + aoff<D>(row, 16 * s + 8 * h));
-#pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          sacc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[g][s], sacc[g], 0, 0, 0);
-          pacc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[g][s], pacc[g], 0, 0, 0);
-        }
-      }
-      bf16x8 pb[KG][2], sb[KG][2];
-#pragma unroll
-      for (int g = 0; g < KG; ++g) {
-        const int key = kw0 + g * 32 + (lane & 31);
-        // wave-uniform: does this 32x32 block cross the sequence end or the causal diagonal?
-        const bool need_mask = (kw0 + g * 32 + 31 >= a.Sk) || (a.causal && kw0 + g * 32 + 31 > qbase + 32 * qt);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float p = fast_exp2(__builtin_fmaf(sacc[g][r], sl2, -lse_l[ql]));
-          if (need_mask && (key >= a.Sk || (a.causal && key > qbase + ql))) p = 0.f;
-          sacc[g][r] = p;
-          pacc[g][r] = p * (pacc[g][r] - dl_l[ql]);
-        }
-        pb[g][0] = pack8(sacc[g], 0); pb[g][1] = pack8(sacc[g], 8);
-        sb[g][0] = pack8(pacc[g], 0); sb[g][1] = pack8(pacc[g], 8);
-      }
-      // dV^T[d][key] += dO^T[d][q] . P[q][key];  dK^T[d][key] += Q^T[d][q] . dS[q][key]
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) {
-        const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int r0 = 32 * qt + 16 * s2 + 4 * h + qi;
-          bf16x8 ao, aq;
-          {
-            const bf16x4 lo = tr_read(do_l, aoff<D>(r0, col));
-            const bf16x4 hi = tr_read(do_l, aoff<D>(r0 + 8, col));
-            ao[0] = lo[0]; ao[1] = lo[1]; ao[2] = lo[2]; ao[3] = lo[3];
-            ao[4] = hi[0]; ao[5] = hi[1]; ao[6] = hi[2]; ao[7] = hi[3];
-          }
-          {
-            const bf16x4 lo = tr_read(q_l, aoff<D>(r0, col));
-            const bf16x4 hi = tr_read(q_l, aoff<D>(r0 + 8, col));
-            aq[0] = lo[0]; aq[1] = lo[1]; aq[2] = lo[2]; aq[3] = lo[3];
-            aq[4] = hi[0]; aq[5] = hi[1]; aq[6] = hi[2]; aq[7] = hi[3];
-          }
-#pragma unroll
-          for (int g = 0; g < KG; ++g) {
-            dv[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ao, pb[g][s2], dv[g][dt], 0, 0, 0);
-            dk[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, sb[g][s2], dk[g][dt], 0, 0, 0);
-          }
-        }
-      }
-      // dS^T image rows = local key index
-#pragma unroll
-      for (int g = 0; g < KG; ++g) {
-        const int krow = (wave * KG + g) * 32 + (lane & 31);
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const int ql = 32 * qt + 8 * q4 + 4 * h;
-          ushort4 o;
-          o.x = f2bf(pacc[g][4 * q4 + 0]); o.y = f2bf(pacc[g][4 * q4 + 1]);
-          o.z = f2bf(pacc[g][4 * q4 + 2]); o.w = f2bf(pacc[g][4 * q4 + 3]);
-          *reinterpret_cast<ushort4*>(ds_l + dst_off(krow, ql)) = o;
-        }
-      }
-    }
-    lds_barrier();
-    // dQ_partial[q][d] = dS[q][key] . K[key][d] over this block's KB keys; wave -> (qt, dt) tiles
-#pragma unroll
-    for (int tile = wave; tile < 2 * (D / 32); tile += NW) {
-      const int qt = tile / (D / 32), dt = tile % (D / 32);
-      f32x16 acc = f32x16{};
-#pragma unroll 4
-      for (int ks = 0; ks < KB / 16; ++ks) {
-        bf16x8 af, bk;
-        {
-          const int cq = 32 * qt + 16 * (G & 1) + 4 * pi;
-          const int kr = 16 * ks + 8 * h + qi;
-          const bf16x4 lo = tr_read(ds_l, dst_off(kr, cq));
-          const bf16x4 hi = tr_read(ds_l, dst_off(kr + 4, cq));
-          af[0] = lo[0]; af[1] = lo[1]; af[2] = lo[2]; af[3] = lo[3];
-          af[4] = hi[0]; af[5] = hi[1]; af[6] = hi[2]; af[7] = hi[3];
-        }
-        {
-          const int cd = 32 * dt + 16 * (G & 1) + 4 * pi;
-          const int kr = 16 * ks + 8 * h + qi;
-          const bf16x4 lo = tr_read(k_l, aoff<D>(kr, cd));
-          const bf16x4 hi = tr_read(k_l, aoff<D>(kr + 4, cd));
-          bk[0] = lo[0]; bk[1] = lo[1]; bk[2] = lo[2]; bk[3] = lo[3];
-          bk[4] = hi[0]; bk[5] = hi[1]; bk[6] = hi[2]; bk[7] = hi[3];
-        }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qbase + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int d = 32 * dt + (lane & 31);
-        if (q < a.Sq) dq_part[(int64_t)q * D + d] = acc[r];
-      }
-    }
-    if (more) stash(t + 1);
-    lds_barrier();
-  }
-  if (a.causal) {
-    for (int64_t i = tid; i < (int64_t)min(qt_begin * QT, a.Sq) * D; i += NT) dq_part[i] = 0.f;
-  }
-#pragma unroll
-  for (int g = 0; g < KG; ++g) {
-    const int key = kw0 + g * 32 + (lane & 31);
-    if (key >= a.Sk) continue;
-    bf16_t* dK = a.dk + (int64_t)b * a.dk_sb + (int64_t)hh * a.dk_sh + (int64_t)key * a.dk_ss;
-    bf16_t* dV = a.dv + (int64_t)b * a.dv_sb + (int64_t)hh * a.dv_sh + (int64_t)key * a.dv_ss;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt) {
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const int d = dt * 32 + 8 * q4 + 4 * h;
-        ushort4 o;
-        o.x = f2bf(dk[g][dt][4 * q4 + 0] * a.scale); o.y = f2bf(dk[g][dt][4 * q4 + 1] * a.scale);
-        o.z = f2bf(dk[g][dt][4 * q4 + 2] * a.scale); o.w = f2bf(dk[g][dt][4 * q4 + 3] * a.scale);
-        *reinterpret_cast<ushort4*>(dK + d) = o;
-        o.x = f2bf(dv[g][dt][4 * q4 + 0]); o.y = f2bf(dv[g][dt][4 * q4 + 1]);
-        o.z = f2bf(dv[g][dt][4 * q4 + 2]); o.w = f2bf(dv[g][dt][4 * q4 + 3]);
-        *reinterpret_cast<ushort4*>(dV + d) = o;
-      }
-    }
-  }
-}
-
 // dq[q][d] = scale * sum_kb dq_part[kb][bh][q][d]
 template <int D>
 __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
@@ -1986,36 +1306,27 @@ __global__ void attn_dq_finish_kernel(AttnArgs a, int nkb) {
   }
 }
 
-// Backward variant: 0 = attn_bwd_kernel with 4 waves x 32 keys and per-key-block slabs; 1 = the
-// one-wave-per-SIMD attn_bwd_kg_kernel (KG = 2 key groups per wave at D = 64); 2 (default) =
-// attn_bwd_kernel with 8 waves x 32 keys at D = 64 (4 at D = 128), chained launches when B*H
-// workgroups fill the chip (>= 256) or there is one key block, else slabs; 3 = variant 2 always
-// chained; 4 = variant 2 always with slabs; 5 = 4 waves x 32 keys chained (two independent
-// workgroups per CU instead of one 8-wave workgroup); 7 = variant 2 with DMA; 9 = attn_bwd1b_kernel
-// (one barrier per query tile); 10 (default) = attn_bwd1b_kernel with its dQ chunks fenced between
-// the S / dP and dV / dK stages when chained (B*H >= 256), else variant 7; without 16-B aligned Q /
-// dO rows the DMA variants fall back to variant 2 (B32 H16 S512 D64: 2 / 7 / 9 / 10 = 161 / 156 /
-// 156 / 151 us, profiles/attn_bwd_r5.txt). Variants measured and removed in round 5: K^T dQ
-// fragments in registers (spilled), a static priority for the younger wave half (null); forward:
-// MFMA clusters at priority 1, all K fragments requested before the S MFMAs (both null,
-// docs/PERFORMANCE.md). Settable for A/B runs in one process
-// (attn_set_bwd_variant); default from FF_ATTN_BWD.
+// Backward variant: 10 (default) = attn_bwd1b_kernel (one barrier per query tile, fenced dQ
+// chunks, LDS-DMA tiles) chained per key block when B*H workgroups fill the chip (>= 256), else
+// attn_bwd_kernel with LDS-DMA Q / dO tiles (one launch with per-key-block dQ slabs + finishing
+// pass); 2 = attn_bwd_kernel without DMA (also what every variant falls back to without 16-B
+// aligned Q / dO rows; D = 128 always takes it with 4 waves). B32 H16 S512 D64: 2 / 10 = 161 / 151 us
+// (profiles/attn_bwd_r5.txt). Round 6 removed the structures measured slower (4-wave slabs and
+// 4-wave chained, the one-wave-per-SIMD key-group kernel, the unfenced and the slab forms of
+// attn_bwd1b_kernel); rounds 1-5 measurements: docs/PERFORMANCE.md. Settable for A/B runs in one
+// process (attn_set_bwd_variant); default from FF_ATTN_BWD; other values mean 10.
 static int g_bwd_variant = -1;
 int attn_bwd_variant() {
   if (g_bwd_variant < 0) {
     const char* e = getenv("FF_ATTN_BWD");
-    g_bwd_variant = e ? atoi(e) : 10;
+    g_bwd_variant = (e && atoi(e) == 2) ? 2 : 10;
   }
   return g_bwd_variant;
 }
-void attn_set_bwd_variant(int v) { g_bwd_variant = v; }
+void attn_set_bwd_variant(int v) { g_bwd_variant = v == 2 ? 2 : 10; }
 
 // keys per backward workgroup
-static int bwd_keys(int D) {
-  const int v = attn_bwd_variant();
-  if (v == 0 || v == 5) return 128;
-  return D == 64 ? 256 : 128;
-}
+static int bwd_keys(int D) { return D == 64 ? 256 : 128; }
 
 int64_t attn_bwd_slab_floats(int B, int H, int Sq, int Sk, int D) {
   const int nkb = (Sk + bwd_keys(D) - 1) / bwd_keys(D);
@@ -2028,20 +1339,22 @@ int64_t attn_bwd_workspace_floats(int B, int H, int Sq, int Sk, int D) {
   return (int64_t)nkb * B * H * Sq * D + 2 * (int64_t)B * H * Sq + (int64_t)B * H * D * (2 + 2 * nkb);
 }
 
-// Forward structure: 4 = persistent 64 rows per wave (attn_fwd2p_kernel; D = 64, non-causal,
-// Sq % 256 == 0, Sk % 128 == 0, else 1), 3 = 64 rows per wave (attn_fwd2_kernel, D = 64 and
-// Sq >= 512, else 1; default), 2 = 8-wave ping-pong (attn_fwd_pp_kernel, D = 64), 1 = 4-wave with
-// LDS-DMA K/V staging, 0 = 4-wave through registers (attn_set_fwd_variant; default from
-// FF_ATTN_FWD).
+// Forward structure: 3 (default) = 64 rows per wave (attn_fwd2_kernel; D = 64 and Sq >= 512, else
+// 1), 1 = 4 waves with LDS-DMA K/V staging, 0 = 4 waves through registers (also the fallback
+// without 16-B aligned K / V rows, and D = 128). All three run the same per-row arithmetic (bitwise
+// equal outputs). Removed in round 6 as measured slower: the persistent 64-rows-per-wave kernel
+// and the 8-wave ping-pong (profiles/attn_fwd_variants_r4.txt, attn_fwd_pingpong_r4.txt).
+// attn_set_fwd_variant; default from FF_ATTN_FWD; other values mean 3.
 static int g_fwd_variant = -1;
 int attn_fwd_variant() {
   if (g_fwd_variant < 0) {
     const char* e = getenv("FF_ATTN_FWD");
-    g_fwd_variant = e ? atoi(e) : 3;
+    const int v = e ? atoi(e) : 3;
+    g_fwd_variant = (v == 0 || v == 1) ? v : 3;
   }
   return g_fwd_variant;
 }
-void attn_set_fwd_variant(int v) { g_fwd_variant = v; }
+void attn_set_fwd_variant(int v) { g_fwd_variant = (v == 0 || v == 1) ? v : 3; }
 
 // Deferred-max threshold of the forward (log2 units; 0 = rescale whenever a row max grows, the
 // textbook online softmax). Default 8 (P <= 256 in bf16 between rescales), FF_ATTN_RESCALE_THR.
@@ -2064,22 +1377,6 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
                       a.v_ss % 8 == 0 && (int64_t)(a.Sk + 64) * a.k_ss * 2 < 0x7fffffffLL &&
                       (int64_t)(a.Sk + 64) * a.v_ss * 2 < 0x7fffffffLL;
   const bool dma = attn_fwd_variant() >= 1 && dma_ok;
-  // persistent 64-rows-per-wave kernel (attn_fwd2p_kernel): two workgroups per CU walk the query
-  // blocks with the K/V stream running across block seams
-  if (attn_fwd_variant() == 4 && dma_ok && a.D == 64 && !a.causal && a.Sq % 256 == 0 && a.Sk % 128 == 0) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (cus <= 0) cus = 256;
-    }
-    const int nblocks = a.Sq / 256 * a.B * a.H;
-    int g = std::min(nblocks, 2 * cus);
-    if (g > 8) g -= g % 8;  // equal residues mod 8: a workgroup's blocks stay on its XCD's chunk
-    hipLaunchKernelGGL(attn_fwd2p_kernel, dim3((unsigned)g), dim3(256), 0, st, a, nblocks);
-    return;
-  }
   // 64 query rows per wave (attn_fwd2_kernel): 2-6 % faster from S = 512 up, slower at S = 256
   // (half the workgroups), profiles/attn_fwd_variants_r4.txt
   if (attn_fwd_variant() == 3 && dma_ok && a.D == 64 && a.Sq >= 512) {
@@ -2087,14 +1384,6 @@ void attn_fwd(AttnArgs a, hipStream_t st) {
     if (mask) hipLaunchKernelGGL((attn_fwd2_kernel<true>), g3, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd2_kernel<false>), g3, dim3(256), 0, st, a);
     return;
-  }
-  if (attn_fwd_variant() == 2 && dma_ok) {  // 8-wave ping-pong (attn_fwd_pp_kernel), D = 64 only
-    const dim3 g2((unsigned)((a.Sq + 255) / 256 * a.B * a.H));
-    if (a.D == 64) {
-      if (mask) hipLaunchKernelGGL((attn_fwd_pp_kernel<64, true>), g2, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_fwd_pp_kernel<64, false>), g2, dim3(512), 0, st, a);
-      return;
-    }
   }
   if (a.D == 64) {
     if (dma) {
@@ -2133,42 +1422,36 @@ bool attn_bwd(AttnArgs a, hipStream_t st) {
   const dim3 gpre((unsigned)((rows * (a.D / 8) + 255) / 256));
   const int64_t per = (int64_t)a.B * a.H * a.Sq * a.D;
   const dim3 gfin(ew_grid(per / 4, 256));
-  // (every attn_bwd_kernel launch with a single key block writes the final dQ itself)
-  const bool chain = v == 3 || v == 5 || ((v == 2 || v >= 7) && a.B * a.H >= 256);
-  const bool finish = v == 1 || (!chain && nkb > 1);
-  // the DMA variants need 16-B aligned Q / dO rows and buffer offsets below 2 GiB
-  const bool dma_ok = ((uintptr_t)a.q & 15) == 0 && ((uintptr_t)a.dout & 15) == 0 && a.q_ss % 8 == 0 &&
+  // chained launches (one per key block, the fp32 dQ sum carried between them) once B*H
+  // workgroups fill the chip; every attn_bwd_kernel launch with a single key block writes the
+  // final dQ itself, so only the slab form with several key blocks needs the finishing pass
+  const bool chain = a.B * a.H >= 256;
+  const bool finish = !chain && nkb > 1;
+  // the DMA paths need 16-B aligned Q / dO rows and buffer offsets below 2 GiB
+  const bool dma_ok = v == 10 && ((uintptr_t)a.q & 15) == 0 && ((uintptr_t)a.dout & 15) == 0 && a.q_ss % 8 == 0 &&
                       a.do_ss % 8 == 0 && (int64_t)(a.Sq + 64) * a.q_ss * 2 < 0x7fffffffLL &&
                       (int64_t)(a.Sq + 64) * a.do_ss * 2 < 0x7fffffffLL;
   if (a.D == 64) {
     hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, gpre, dim3(256), 0, st, a);
-    if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<64, 2>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
-    else if (v == 0 || v == 5) launch_bwd_main<64, 4>(a, nkb, v == 5, st);
-    else if ((v == 9 || (v == 10 && chain)) && dma_ok) {  // (the slab form of attn_bwd1b_kernel spills)
+    if (chain && dma_ok) {
       const bool m = a.causal || a.Sk % 256 != 0 || a.Sq % 64 != 0;
       const int bh = a.B * a.H;
-      // fused bias-gradient sums: chained and non-causal (every query tile's last key block is
-      // the last launch)
-      if (!(chain && !a.causal)) a.dbp = nullptr;
+      // fused bias-gradient sums: non-causal (every query tile's last key block is the last launch)
+      if (a.causal) a.dbp = nullptr;
       bias_done = a.dbp != nullptr;
-      if (chain) {
-        for (int p = 0; p < nkb; ++p) {
-          if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
-          else if (v == 10) hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
-          else hipLaunchKernelGGL((attn_bwd1b_kernel<false, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
-        }
-      } else {
-        if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, false>), dim3(bh * nkb), dim3(512), 0, st, a, nkb, 0);
-        else hipLaunchKernelGGL((attn_bwd1b_kernel<false, false>), dim3(bh * nkb), dim3(512), 0, st, a, nkb, 0);
+      for (int p = 0; p < nkb; ++p) {
+        if (m) hipLaunchKernelGGL((attn_bwd1b_kernel<true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
+        else hipLaunchKernelGGL((attn_bwd1b_kernel<false, true, true>), dim3(bh), dim3(512), 0, st, a, nkb, p);
       }
+    } else if (dma_ok) {
+      launch_bwd_main<64, 8, true>(a, nkb, chain, st);
+    } else {
+      launch_bwd_main<64, 8>(a, nkb, chain, st);
     }
-    else if ((v == 7 || v == 10) && dma_ok) launch_bwd_main<64, 8, true>(a, nkb, chain, st);
-    else launch_bwd_main<64, 8>(a, nkb, chain, st);
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gfin, dim3(256), 0, st, a, nkb);
   } else if (a.D == 128) {
     hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, gpre, dim3(256), 0, st, a);
-    if (v == 1) hipLaunchKernelGGL((attn_bwd_kg_kernel<128, 1>), dim3(nkb * a.B * a.H), dim3(256), 0, st, a, nkb);
-    else launch_bwd_main<128, 4>(a, nkb, v != 0 && chain, st);
+    launch_bwd_main<128, 4>(a, nkb, chain, st);
     if (finish) hipLaunchKernelGGL(attn_dq_finish_kernel<128>, gfin, dim3(256), 0, st, a, nkb);
   }
   if (bias_done)

@@ -101,7 +101,7 @@ bool gemm_dact(Tensor A, Tensor B, Tensor C, Tensor zin, optional<Tensor> dbias,
     part = at::empty({rows * N}, C.options().dtype(at::kFloat));
     p.colpart = part.data_ptr<float>();
   }
-  (void)impl;  // one fused-dgrad kernel (gemm_dact.hip); the argument stays for call-site stability
+  p.impl = (int)impl;  // 6: the ping-pong kernel's DACT epilogue; else the 256-row kernel's
   if (!ffk::gemm_dact_bf16(p, cur_stream())) return false;
   if (has_db) ffk::col_reduce_add(p.colpart, dbias->data_ptr<float>(), (int)rows, (int)N, cur_stream());
   return true;

@@ -194,6 +194,9 @@ bool gemm_dact_bf16(GemmArgs p, hipStream_t stream) {
   p.dact = true;
   p.splitk = 1;
   p.ws = nullptr;
+  // impl 6: the ping-pong kernel's DACT epilogue (NN dgrad layout; gemm_pp.hip), else the 256-row
+  // kernel's
+  if (p.impl == 6) return gemm_pp_bf16(p, p.a_bytes, p.b_bytes, stream);
   return gemm256_bf16(p, p.a_bytes, p.b_bytes, stream);
 }
 

@@ -94,25 +94,32 @@ __device__ __forceinline__ int opaque_lane() {
 
 // VMEM ops of one epilogue: 2 bias loads (one wasted for a bf16 bias keeps the count fixed) + 16 row
 // stores (bf16) or 32 (fp32).
-// (A fused-dgrad variant — the producer's stored act'(z) multiplied in here, bias-gradient column
-// sums beside it — was tried in round 5 and removed: its 16 extra loads and column sums spilled
-// ~150 VGPRs into scratch, the spill traffic forced vmcnt(0) into every memory phase, and it was
-// numerically wrong in the last row pass; gemm_dact's impl-2 kernel and the library GEMM + pass
-// pair cover that op.)
 // ACT (bf16 output only): activation in the epilogue, the pre-activation (z + bias) stored to Z in
 // the same pass (16 more stores; issued out of range when Z is null so the count stays fixed)
-template <bool F32OUT, bool ACT = false>
-constexpr int epi_ops() { return (F32OUT ? 32 : 16) + 2 + (ACT ? 16 : 0); }
+// DACT (bf16 output only; round 6): the dgrad of a Linear fused with its producer's activation
+// backward — C = (alpha A.B) * act'(zin), zin read in C's layout (16 more loads, two per row pass,
+// each pass's pair requested one pass ahead so that no wait covers the previous pass's stores),
+// plus the per-128-row fp32 column sums of that product for the producer's bias gradient (2 more
+// stores). (Round 5's first attempt loaded every zin row up front and summed columns per element
+// pass: ~150 VGPRs spilled; here the sums are 8 registers folded across lanes once per tile.)
+template <bool F32OUT, bool ACT = false, bool DACT = false>
+constexpr int epi_ops() { return DACT ? 16 + 14 + 2 : (F32OUT ? 32 : 16) + 2 + (ACT ? 16 : 0); }
 
 // ACTK: 0, or the activation (ACT_RELU / ACT_GELU) as a compile-time constant: one code path per
-// instantiation (a run-time switch over every activation cost ~10 more VGPR spills)
-template <bool A_K, bool B_K, bool F32OUT, bool SPLIT, int ACTK = 0>
+// instantiation (a run-time switch over every activation cost ~10 more VGPR spills). DK: 0, or
+// ACT_GRADMUL for the DACT epilogue (zin already holds act'(z), stored by the producer's forward).
+// (Evaluating GELU' from z here was tried: ~14 VALU per element in the memory phase, 96 B/lane of
+// spills, and wrong results on 1/3 of the elements on gfx950 — not built.)
+template <bool A_K, bool B_K, bool F32OUT, bool SPLIT, int ACTK = 0, int DK = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096];
+  constexpr bool DACT = DK != 0;
+  // DACT: + 32 B per lane of running column sums (8 waves x 2 KiB, 160 KiB in all)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096 + (DACT ? 8 * 2048 : 0)];
   constexpr bool ACT = ACTK != 0;
-  constexpr int EPI = epi_ops<F32OUT, ACT>();
+  constexpr int EPI = epi_ops<F32OUT, ACT, DACT>();
   static_assert(!ACT || (!F32OUT && !SPLIT), "activation epilogue: bf16 output, no split-K");
+  static_assert(!DACT || (!F32OUT && !SPLIT && !ACT), "dgrad-activation epilogue: bf16 output, no split-K");
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -330,6 +337,16 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(ACT && p.Z ? p.Z : p.C), (short)0,
                                                                 ACT && p.Z ? (int)min(c_bytes, (int64_t)0x7fffffff) : 0,
                                                                 0x00020000);
+  // DACT: zin (bf16, C's layout) and the column-sum partials [2 * ceil(M / 256)][N] (a null colpart
+  // gets an empty range: its stores are dropped)
+  const int64_t zin_bytes = (int64_t)p.M * p.ldc * 2;
+  const int64_t cp_bytes = DACT && p.colpart ? (int64_t)2 * ((p.M + BM - 1) / BM) * p.N * 4 : 0;
+  __amdgpu_buffer_rsrc_t rzin = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT ? p.zin : p.C), (short)0,
+                                                                  DACT ? (int)min(zin_bytes, (int64_t)0x7fffffff) : 0,
+                                                                  0x00020000);
+  __amdgpu_buffer_rsrc_t rcp = __builtin_amdgcn_make_buffer_rsrc((void*)(DACT && p.colpart ? (void*)p.colpart : p.C),
+                                                                 (short)0, (int)min(cp_bytes, (int64_t)0x7fffffff),
+                                                                 0x00020000);
   // Epilogue through a wave-private fp32 staging image (16 rows x 64 columns, 4 KiB, outside the
   // ring): the accumulator layout puts 4 consecutive columns of one row in a lane, so direct 8-B
   // stores leave a wave as 16 scattered 32-B row pieces per instruction, store-issue bound at
@@ -347,7 +364,9 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
     const int n = tni * BN + wj * 64 + 8 * cc;  // this lane's 8 read-back columns
     const bool nin = n < p.N;
     float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (p.bias_bf16) {
+    if constexpr (DACT) {
+      // no bias (dgrad): no bias registers live across the passes
+    } else if (p.bias_bf16) {
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -362,6 +381,26 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
         bb[e] = __uint_as_float(v0[e]);
         bb[4 + e] = __uint_as_float(v1[e]);
       }
+    }
+    // DACT: zin rows of pass i (rows m0 + 16 i + rr8 + 8 h, columns n..n+7), requested one pass
+    // ahead (after pass i - 1 consumed its pair, before its stores: the wait for them covers no
+    // store); cs: this lane's column sums over its rows. Waiting for zin pair 0 also retires every
+    // DMA piece older than the epilogue, so the memory phase's counted wait stays correct whatever
+    // the epilogue's VMEM count.
+    auto zin_off = [&](int i, int h) __attribute__((always_inline)) {
+      const int m = m0 + 16 * i + (opaque_lane() >> 3) + 8 * h;
+      return (m < p.M && nin) ? (int)(((int64_t)m * p.ldc + n) * 2) : -16;
+    };
+    u32x4 zq[2];
+    // the lane's running column sums live in its own 32 B of LDS between passes (in registers,
+    // next to the 128 accumulators, they spilled ~16 VGPRs to scratch): read, add, write per pass;
+    // a wave's LDS operations execute in order
+    const unsigned csa = sbase + 2 * STAGE + 4 * 4096 + wave * 2048 + (lane << 5);
+    if constexpr (DACT) {
+      const f32x4 zz = {0.f, 0.f, 0.f, 0.f};
+      asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %1 offset:16" ::"v"(csa), "v"(zz) : "memory");
+      zq[0] = __builtin_amdgcn_raw_buffer_load_b128(rzin, zin_off(0, 0), 0, 0);
+      zq[1] = __builtin_amdgcn_raw_buffer_load_b128(rzin, zin_off(0, 1), 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -385,6 +424,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
       }
       lgkm0();
       __builtin_amdgcn_sched_barrier(0);
+      u32x4 ov[2];  // DACT: this pass's two output rows, stored after the next zin pair is requested
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int m = m0 + 16 * i + rr8 + 8 * h;
@@ -402,6 +442,28 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           __builtin_amdgcn_raw_buffer_store_b128(o0, rc, off, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b128(o1, rc, in ? off + 16 : off, 0, 0);
         } else {
+          if constexpr (DACT) {
+            const u32x4 zv = zq[h];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float z0 = __uint_as_float(zv[e] << 16), z1 = __uint_as_float(zv[e] & 0xffff0000u);
+              // the GEMM result rounded to bf16 first, as the unfused GEMM + bias_act_bwd pair
+              // does: the autotuner's pick changes the numerics by summation order only
+              x[2 * e] = bf2f(f2bf(x[2 * e])) * act_grad(DK, z0);
+              x[2 * e + 1] = bf2f(f2bf(x[2 * e + 1])) * act_grad(DK, z1);
+            }
+            {  // running column sums += this row (in LDS; see csa)
+              f32x4 c0, c1;
+              asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                           : "=&v"(c0), "=&v"(c1) : "v"(csa) : "memory");
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                c0[e] += x[e];
+                c1[e] += x[4 + e];
+              }
+              asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:16" ::"v"(csa), "v"(c0), "v"(c1) : "memory");
+            }
+          }
           if constexpr (ACT) {
             u32x4 zo;
 #pragma unroll
@@ -413,9 +475,50 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
           u32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (uint32_t)f2bf(x[2 * e]) | ((uint32_t)f2bf(x[2 * e + 1]) << 16);
-          __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
+          if constexpr (DACT) ov[h] = o;
+          else __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
         }
       }
+      if constexpr (DACT) {
+        if (i < 7) {  // the next pass's zin pair, then this pass's stores
+          zq[0] = __builtin_amdgcn_raw_buffer_load_b128(rzin, zin_off(i + 1, 0), 0, 0);
+          zq[1] = __builtin_amdgcn_raw_buffer_load_b128(rzin, zin_off(i + 1, 1), 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int m = m0 + 16 * i + rr8 + 8 * h;
+          const int off = (m < p.M && nin) ? (int)(((int64_t)m * ldo + n) * 2) : -16;
+          __builtin_amdgcn_raw_buffer_store_b128(ov[h], rc, off, 0, 0);
+        }
+      }
+    }
+    if constexpr (DACT) {
+      // fold the 8 row lanes of each column group (lane bits 3-5), then lanes 0-7 store this wave's
+      // 64 column sums of its 128 rows: colpart row 2 * tile_m + group
+      float cs[8];
+      {
+        f32x4 c0, c1;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(c0), "=&v"(c1) : "v"(csa) : "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          cs[e] = c0[e];
+          cs[4 + e] = c1[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], 8);
+        cs[e] += __shfl_xor(cs[e], 16);
+        cs[e] += __shfl_xor(cs[e], 32);
+      }
+      const bool st0 = nin && (opaque_lane() >> 3) == 0;
+      const int co = st0 ? (int)(((int64_t)(2 * tmi + grp) * p.N + n) * 4) : -16;
+      const u32x4 c0 = {__float_as_uint(cs[0]), __float_as_uint(cs[1]), __float_as_uint(cs[2]), __float_as_uint(cs[3])};
+      const u32x4 c1 = {__float_as_uint(cs[4]), __float_as_uint(cs[5]), __float_as_uint(cs[6]), __float_as_uint(cs[7])};
+      __builtin_amdgcn_raw_buffer_store_b128(c0, rcp, co, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(c1, rcp, st0 ? co + 16 : co, 0, 0);
     }
   };
 
@@ -502,6 +605,13 @@ static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int6
   else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
 }
 
+// the DACT epilogue is built for the dgrad layout only: A = dY [M][K] K-contiguous, B = W [K][N]
+// N-contiguous (the weight of the consumer Linear as stored)
+template <int DK>
+static void launch_dact(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
+  hipLaunchKernelGGL((gemm_pp_kernel<true, false, false, false, 0, DK>), grid, dim3(NTHR), 0, s, p, ab, bb);
+}
+
 }  // namespace pp
 
 static int g_pp_cus = 0;
@@ -509,8 +619,14 @@ static int g_pp_cus = 0;
 bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
   using namespace pp;
   // activation epilogue (bias + act, optional pre-activation store): bf16 output, no split-K
-  const bool act = p.Z || p.act != ACT_NONE;
-  if (p.dact) return false;
+  const bool act = !p.dact && (p.Z || p.act != ACT_NONE);
+  if (p.dact) {  // dgrad-activation epilogue (gemm_dact_bf16 sets it): NN layout, bf16 out, no bias
+    if (!p.zin || p.out_f32 || p.bias || p.Z || p.beta != 0.f || p.batch != 1 || (p.splitk > 1 && p.ws) ||
+        !p.a_kcontig || p.b_kcontig || p.act != ACT_GRADMUL ||
+        ((uintptr_t)p.zin & 15) || (p.colpart && ((uintptr_t)p.colpart & 15)) ||
+        (int64_t)p.M * p.ldc * 2 > 0x7fffff00LL || (int64_t)2 * ((p.M + BM - 1) / BM) * p.N * 4 > 0x7fffff00LL)
+      return false;
+  }
   if (act && (p.out_f32 || (p.act != ACT_NONE && p.act != ACT_RELU && p.act != ACT_GELU) || (p.splitk > 1 && p.ws) ||
               ((uintptr_t)p.Z & 15)))
     return false;
@@ -535,7 +651,9 @@ bool gemm_pp_bf16(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, hipStream
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * (split ? p.splitk : 1);
   dim3 grid(std::min(tiles, g_pp_cus));
-  if (split) launch<true, true>(p, grid, stream, a_bytes, b_bytes);  // split-K: fp32 slabs only
+  if (p.dact) {
+    launch_dact<ACT_GRADMUL>(p, grid, stream, a_bytes, b_bytes);
+  } else if (split) launch<true, true>(p, grid, stream, a_bytes, b_bytes);  // split-K: fp32 slabs only
   else if (p.out_f32) launch<true, false>(p, grid, stream, a_bytes, b_bytes);
   else if (act && p.act == ACT_GELU) launch<false, false, ACT_GELU>(p, grid, stream, a_bytes, b_bytes);
   else if (act && p.act == ACT_RELU) launch<false, false, ACT_RELU>(p, grid, stream, a_bytes, b_bytes);

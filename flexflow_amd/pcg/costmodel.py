@@ -188,7 +188,8 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
     need_dx0 = bool(layer.inputs) and layer.inputs[0].owner_layer is not None and \
         layer.inputs[0].owner_layer.op_type != OperatorType.OP_INPUT
     key = (layer.op_type, layer.impl.params_key(), tuple(l.local_shape(0) for l in lo.inputs),
-           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0, tuple(_hot_inputs(layer)))
+           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0, tuple(_hot_inputs(layer)),
+           (dact_fusion_partner(layer) or (None,))[0])
     if key in _measured:
         return _measured[key]
     hit = _disk_get(key, device)
@@ -234,6 +235,20 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
     ln_fused = ln_bias_fusion_producer(layer)
     ln_db = torch.zeros(layer.inputs[0].dims[-1], device=device, dtype=torch.float32) if ln_fused is not None else None
     bias_fused = bias_grad_fused_away(layer)
+    # backward act' fusion across two Linears (executor._plan_dact_fusion): the producer's backward
+    # skips its act' pass and bias gradient; the consumer's dgrad applies them (kernels.gemm_dact)
+    dact = dact_fusion_partner(layer)
+    dact_src = None
+    if dact is not None and dact[0] == "consumer":
+        from ..ops import OpCtx as _Ctx
+        P = dact[1]
+        rows = math.prod(lo.inputs[0].local_shape(0)[:-1])
+        kin = lo.inputs[0].local_shape(0)[-1]
+        pctx = _Ctx(layer=P, part_coords=(0,) * len(cfg.degrees), degrees=cfg.degrees, compute_dtype=compute_dtype)
+        pctx.saved.update(z=torch.randn(rows, kin, device=device, dtype=ct), has_b=len(P.weights) > 1,
+                          z_is_grad=False)
+        pctx.wgrads = [torch.zeros(1, device=device), torch.zeros(kin, device=device, dtype=torch.float32)]
+        dact_src = (pctx, P.impl.act)
 
     def make_ctx():
         ctx = OpCtx(layer=layer, part_coords=(0,) * len(cfg.degrees), degrees=cfg.degrees,
@@ -246,6 +261,10 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
             ctx.extra["colsum_out"] = ln_db
         if bias_fused:
             ctx.extra["bias_grad_fused"] = True
+        if dact is not None and dact[0] == "producer":
+            ctx.extra["dact_fused"] = True
+        if dact_src is not None:
+            ctx.extra["dact_src"] = dact_src
         return ctx
 
     try:
@@ -422,6 +441,33 @@ def ln_bias_fusion_producer(layer):
             return P
         if P.op_type == OperatorType.OP_MULTIHEAD_ATTENTION and P.attrs.get("bias", True):
             return P
+    return None
+
+
+def dact_fusion_partner(layer):
+    """The executor's backward act' fusion (_plan_dact_fusion), decided from the graph alone:
+    ("consumer", P) when this Linear's dgrad applies its producing Linear P's act' (and sums P's
+    bias gradient), ("producer", C) when this Linear's act' / bias gradient are done by its sole
+    consumer C's dgrad, else None. r5 priced BERT's FFN1 backward with its own bias_act_bwd pass
+    (+31 %) and FFN2's without it — errors that cancelled per class but steered per-op choices."""
+    m = getattr(layer, "model", None)
+    if m is None or layer.op_type != OperatorType.OP_LINEAR or os.environ.get("FF_NO_DACT_FUSION") == "1":
+        return None
+    out = m.output_tensor()
+
+    def fusable(P, C):
+        if P is None or C is None or P.op_type != OperatorType.OP_LINEAR or C.op_type != OperatorType.OP_LINEAR:
+            return False
+        if getattr(P.impl, "act", 10) == 10 or not C.inputs or C.inputs[0].owner_layer is not P:
+            return False
+        t = C.inputs[0]
+        return _sole_reader(t, m) and not (out is not None and out.guid == t.guid)
+    P = layer.inputs[0].owner_layer if layer.inputs else None
+    if fusable(P, layer):
+        return ("consumer", P)
+    for L in m.layers:
+        if L.inputs and L.inputs[0].owner_layer is layer and fusable(layer, L):
+            return ("producer", L)
     return None
 
 

@@ -37,9 +37,9 @@ def timed(fn):
 
 
 fl_f = 4.0 * B * H * S * S * D
-# forward structures (0: registers, 1: LDS-DMA, 2: ping-pong, 3: 64 rows/wave, 4: persistent), interleaved
+# forward structures (0: registers, 1: LDS-DMA, 3: 64 rows/wave), interleaved
 default_fwd = X.attn_fwd_variant()
-FV = (0, 1, 2, 3, 4)
+FV = (0, 1, 3)
 fres, fouts = {v: [] for v in FV}, {}
 for rnd in range(3):
     for var in FV:
@@ -71,7 +71,7 @@ X.attn_set_rescale_thr(default_thr)
 lse = Kn.flash_attn_fwd(q, sq, k, sq, v, sq, o, so, B, H, S, S, D, scale, False)
 # backward variants A/B'd in this one process, interleaved rounds (guide rule 24)
 default_variant = X.attn_bwd_variant()
-BV = tuple(int(x) for x in (sys.argv[6].split(',') if len(sys.argv) > 6 else '0,1,2,5,7,9,10'.split(',')))
+BV = tuple(int(x) for x in (sys.argv[6].split(',') if len(sys.argv) > 6 else '2,10'.split(',')))
 res = {v: [] for v in BV}
 outs = {}
 for rnd in range(3):

@@ -114,7 +114,19 @@ det.sort(reverse=True)
 print("largest per-op disagreements (ms): name op pred_fwd meas_fwd pred_bwd meas_bwd")
 for d, name, op, f, mf, b, mb in det[:12]:
     print(f"  {name:34s} {op:24s} {f:8.3f} {mf:8.3f} {b:8.3f} {mb:8.3f}")
+# the 20 largest ops by measured time, per-op fwd / bwd error
+big = sorted(pred.items(), key=lambda kv: -(meas.get(kv[0], {}).get("fwd_ms", 0.0) + meas.get(kv[0], {}).get("bwd_ms", 0.0)))
+print("20 largest ops (measured): name op pred_fwd meas_fwd err_fwd pred_bwd meas_bwd err_bwd")
+worst = 0.0
+for name, (op, f, b) in big[:20]:
+    m = meas.get(name, {"fwd_ms": 0.0, "bwd_ms": 0.0})
+    ef = 100 * (f / max(m["fwd_ms"], 1e-9) - 1)
+    eb = 100 * (b / max(m["bwd_ms"], 1e-9) - 1) if m["bwd_ms"] > 0 else 0.0
+    worst = max(worst, abs(ef), abs(eb))
+    print(f"  {name:34s} {op:24s} {f:8.3f} {m['fwd_ms']:8.3f} {ef:+6.1f}% {b:8.3f} {m['bwd_ms']:8.3f} {eb:+6.1f}%")
+print(f"worst per-op error among the 20 largest: {worst:.1f}%")
 print(json.dumps({"model": model, "batch": batch, "measured_step_ms": round(step_ms, 3),
+                  "worst_top20_op_error_pct": round(worst, 1),
                   "simulated_step_ms": round(sim.makespan_ms, 3),
                   "error_pct": round(100 * (sim.makespan_ms / step_ms - 1), 2),
                   "pred_ops_ms": round(tot_pred_ops, 3), "measured_ops_ms": round(tot_meas_ops, 3),

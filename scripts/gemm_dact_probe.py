@@ -29,6 +29,7 @@ def lib_pass(act, zz):
 
 fns = {
     "pp(g)": lambda: X.gemm_dact(dy, w, C, g, db, M, N, K, K, N, N, True, False, 15, 6),
+    "pp(g) no db": lambda: X.gemm_dact(dy, w, C, g, None, M, N, K, K, N, N, True, False, 15, 6),
     "k256(gelu)": lambda: X.gemm_dact(dy, w, C, z, db, M, N, K, K, N, N, True, False, 14, 2),
     "lib+pass(gelu)": lambda: lib_pass(14, z),
     "lib+pass(g)": lambda: lib_pass(15, g),

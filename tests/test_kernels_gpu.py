@@ -205,15 +205,15 @@ def _attn_ref(q, k, v, scale, causal):
     return torch.einsum("bhqk,bhkd->bhqd", p, v), torch.logsumexp(s, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 7, 9, 10])
+@pytest.mark.parametrize("variant", [2, 10])
 @pytest.mark.parametrize("S,D,causal", [(512, 64, False), (200, 64, False), (256, 128, False), (384, 64, True),
                                         (640, 64, True), (300, 128, True), (1024, 64, True), (512, 128, False)])
 def test_flash_attention(ffC, S, D, causal, variant):
-    """Every backward structure (0: 4 waves x 32 keys + slabs; 1: one wave per SIMD, 64 keys per
-    wave at D = 64; 2: default; 3: chained per-key-block launches carrying the fp32 dQ sum; 4:
-    8 waves + slabs; 5: 4 waves chained; 7: LDS-DMA Q / dO tiles; 9: one barrier per query tile,
-    dQ on 16x16x32; 10: 9 with fenced dQ chunks, the default) against an fp32 PyTorch reference,
-    incl. ragged and causal key blocks."""
+    """Both backward structures (2: attn_bwd_kernel through registers, chained or with dQ slabs;
+    10, the default: the one-barrier-per-query-tile attn_bwd1b_kernel chained at B*H >= 256, else
+    attn_bwd_kernel with LDS-DMA Q / dO tiles and slabs) against an fp32 PyTorch reference, incl.
+    ragged and causal key blocks (B*H = 6 here: the slab forms; the chained forms are covered at
+    B*H = 256 by the tests below)."""
     torch.manual_seed(3)
     prev_variant = ffC.attn_bwd_variant()
     ffC.attn_set_bwd_variant(variant)
@@ -226,11 +226,10 @@ def test_flash_attention(ffC, S, D, causal, variant):
     st = [H * S * D, S * D, D]
     scale = 1.0 / math.sqrt(D)
     ffC.attn_fwd(q, st, k, st, v, st, o, st, lse, B, H, S, S, D, scale, causal)
-    # the forward structures (0: 4 waves, register-staged K/V; 1: 4 waves, LDS-DMA; 2: 8-wave
-    # ping-pong; 3: 64 rows per wave; 4: persistent 64 rows per wave) run the same per-row
-    # arithmetic: bitwise equal
+    # the forward structures (0: 4 waves, register-staged K/V; 1: 4 waves, LDS-DMA; 3: 64 rows
+    # per wave) run the same per-row arithmetic: bitwise equal
     prev_fwd = ffC.attn_fwd_variant()
-    for fv in (0, 1, 2, 3, 4):
+    for fv in (0, 1, 3):
         ffC.attn_set_fwd_variant(fv)
         o2, lse2 = torch.full_like(o, 3.0), torch.full_like(lse, 3.0)
         ffC.attn_fwd(q, st, k, st, v, st, o2, st, lse2, B, H, S, S, D, scale, causal)
@@ -289,12 +288,15 @@ def test_flash_attention_deferred_max(ffC, thr, ramp, causal):
         ffC.attn_set_rescale_thr(prev)
 
 
-def test_flash_attention_bwd_default_chain(ffC):
-    """B*H >= 256 takes the chained backward by default (no dQ slabs, no finishing pass): BERT-Large
-    attention shape with the fused [B,S,3,H,D] projection layout, against fp32 autograd."""
+@pytest.mark.parametrize("variant", [10, 2])
+def test_flash_attention_bwd_default_chain(ffC, variant):
+    """B*H >= 256 takes the chained backward (no dQ slabs, no finishing pass): BERT-Large attention
+    shape with the fused [B,S,3,H,D] projection layout, against fp32 autograd; variant 10 (default,
+    attn_bwd1b_kernel) and 2 (attn_bwd_kernel chained, the fallback for unaligned rows)."""
     torch.manual_seed(6)
     B, S, H, D = 16, 512, 16, 64
     assert ffC.attn_bwd_variant() == 10
+    ffC.attn_set_bwd_variant(variant)
     qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
     o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B * H * S, device=DEV)
@@ -312,6 +314,7 @@ def test_flash_attention_bwd_default_chain(ffC):
     q, k, v = (qkv[:, :, i].permute(0, 2, 1, 3).float().requires_grad_() for i in range(3))
     ref, _ = _attn_ref(q, k, v, scale, False)
     ref.backward(do.permute(0, 2, 1, 3).float())
+    ffC.attn_set_bwd_variant(10)
     for i, t in enumerate((q, k, v)):
         assert _rel(dqkv[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
 
@@ -493,9 +496,11 @@ def test_bias_act_bwd(ffC, rows, cols, act):
 @pytest.mark.parametrize("a_k,b_k", [(True, False), (True, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (300, 136, 72), (1000, 4096, 1024), (256, 200, 64)])
 @pytest.mark.parametrize("act", [14, 11, 15])  # GELU, RELU, stored act' (GRADMUL)
-def test_gemm_dact(ffC, a_k, b_k, M, N, K, act):
+@pytest.mark.parametrize("impl", [2, 6])
+def test_gemm_dact(ffC, a_k, b_k, M, N, K, act, impl):
     """Consumer dgrad GEMM with the producer's act' and bias-gradient column sums in the epilogue
-    (gemm256.hip dact mode) against fp32 torch."""
+    (impl 2: gemm256.hip dact mode; impl 6: gemm_pp.hip DACT epilogue, dgrad layout only) against
+    fp32 torch."""
     from flexflow_amd.kernels import act_grad_ref
     torch.manual_seed(3)
     Am = torch.randn(M, K, device=DEV).bfloat16()
@@ -505,8 +510,11 @@ def test_gemm_dact(ffC, a_k, b_k, M, N, K, act):
     z = torch.randn(M, N, device=DEV).bfloat16()
     C = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
     db = torch.ones(N, device=DEV)
-    ok = ffC.gemm_dact(A, B, C, z, db, M, N, K, A.shape[-1], B.shape[-1], N, a_k, b_k, act, 2)
-    assert ok == (N % 8 == 0 and K % 64 == 0 and (a_k or M % 8 == 0))
+    ok = ffC.gemm_dact(A, B, C, z, db, M, N, K, A.shape[-1], B.shape[-1], N, a_k, b_k, act, impl)
+    if impl == 6:  # the ping-pong kernel's DACT epilogue: stored act' (GRADMUL), dgrad layout
+        assert ok == (act == 15 and a_k and not b_k and N % 8 == 0 and K % 64 == 0)
+    else:
+        assert ok == (N % 8 == 0 and K % 64 == 0 and (a_k or M % 8 == 0))
     if not ok:
         return
     ref = (Am.float() @ Bn.float().t()) * act_grad_ref(z.float(), act)
@@ -523,14 +531,15 @@ def test_gemm_dact_dispatch_matches_unfused():
     w = torch.randn(Kd, N, device=DEV).bfloat16()
     z = torch.randn(M, N, device=DEV).bfloat16()
     outs = []
-    for fused in (True, False):
-        K._tuned[("dact", M, N, Kd, True, False, Kd, N, N, 14, True)] = "fused" if fused else "unfused"
+    for fused in ("fused_pp", "fused", "unfused"):
+        K._tuned[("dact", M, N, Kd, True, False, Kd, N, N, 14, True)] = fused
         C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         db = torch.zeros(N, device=DEV)
         K.gemm_dact(dy, w, C, z, db, M, N, Kd, True, False, Kd, N, N, 14)
         outs.append((C.float(), db))
-    assert _rel(outs[0][0], outs[1][0]) < 1e-2
-    assert _rel(outs[0][1], outs[1][1]) < 1e-2
+    for o in outs[:2]:
+        assert _rel(o[0], outs[2][0]) < 1e-2
+        assert _rel(o[1], outs[2][1]) < 1e-2
 
 
 def test_adam_sgd_embedding_dropout(ffC):
