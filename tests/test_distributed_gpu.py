@@ -118,3 +118,82 @@ def test_bert_two_ranks_match_single(single, search):
         assert d <= 2 * 3 * 1e-3 + 2e-2 * np.abs(b).max(), f"{search}: {k} max diff {d}"
         rel = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-12)
         assert rel < 2e-2, f"{search}: {k} relative difference {rel}"
+
+
+def _train_cnn(strategy_file, steps=3):
+    """Two 3x3 convs on a 16x16 map, max pool, dense head; SGD. With a strategy file: conv1 split
+    along H and conv2 along W over the 2 ranks (halo'd input blocks, halo input gradients summed)."""
+    import torch
+    from flexflow_amd.core import ActiMode, DataType, FFConfig, FFModel, LossType, MetricsType, PoolType, SGDOptimizer
+    flags = ["--dtype", "bf16", "--no-hip-graphs"] + (["--import-strategy", strategy_file] if strategy_file else
+                                                      ["--only-data-parallel"])
+    cfg = FFConfig(flags)
+    cfg.batch_size = B
+    ff = FFModel(cfg)
+    x = ff.create_tensor([B, 16, 16, 16], DataType.DT_FLOAT, name="x")
+    t = ff.conv2d(x, 32, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = ff.conv2d(t, 32, 3, 3, 1, 1, 1, 1, name="c2")
+    t = ff.pool2d(t, 2, 2, 2, 2, 0, 0, PoolType.POOL_MAX, name="p")
+    t = ff.flat(t, name="f")
+    t = ff.dense(t, 10, name="d")
+    ff.softmax(t, name="sm")
+    ff.optimizer = SGDOptimizer(ff, 0.05)
+    ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+    rng = np.random.default_rng(5)
+    x.set_tensor(ff, rng.standard_normal((B, 16, 16, 16)).astype(np.float32))
+    ff.label_tensor.set_tensor(ff, rng.integers(0, 10, (B, 1)).astype(np.int32))
+    for _ in range(steps):
+        ff.train_step()
+    torch.cuda.synchronize()
+    res = {f"{L.name}.{i}": np.asarray(w.get_weights(ff), dtype=np.float32) for L in ff.layers
+           for i, w in enumerate(L.weights)}
+    res["__strategy__"] = np.array([str({k: v.degrees for k, v in ff.strategy.items()})])
+    return res
+
+
+def _cnn_worker(rank, world, port, strategy_file, out_file):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), FF_DIST_BACKEND="gloo",
+                      FF_GEMM_TUNE="0", FF_CONV_IMPL="ours")
+    sys.path.insert(0, ROOT)
+    res = _train_cnn(strategy_file)
+    import torch.distributed as dist
+    if rank == 0:
+        np.savez(out_file, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_halo_conv_two_ranks_match_single():
+    """Attribute (spatial) parallelism on the GPU: the HIP conv kernels on halo'd H / W blocks of
+    2 ranks sharing the MI355X (gloo), the halo exchange and the summed input-gradient halos,
+    against one process running the unsplit convs (BASELINE config #3's mechanism; reference
+    model.cc:3627, substitution.cc:1826-1850)."""
+    import torch.multiprocessing as mp
+    from flexflow_amd.pcg.strategy import OpConfig, save_strategy
+    tmp = tempfile.mkdtemp()
+    sf = os.path.join(tmp, "halo.json")
+    dp = lambda n: OpConfig(tuple([2] + [1] * (n - 1)), (0, 1))  # noqa: E731
+    st = {"x": dp(4), "c1": OpConfig((1, 1, 2, 1, 1), (0, 1)), "c2": OpConfig((1, 1, 1, 2, 1), (0, 1)),
+          "p": dp(4), "f": dp(2), "d": dp(3), "sm": dp(2)}
+    save_strategy(sf, st, 2)
+    out = os.path.join(tmp, "out.npz")
+    mp.start_processes(_cnn_worker, args=(2, _free_port(), sf, out), nprocs=2, join=True, start_method="spawn")
+    par = dict(np.load(out))
+    assert "(1, 1, 2, 1, 1)" in str(par["__strategy__"]) and "(1, 1, 1, 2, 1)" in str(par["__strategy__"])
+    old = {k: os.environ.pop(k, None) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    from flexflow_amd import kernels as K
+    tune, tuned, impl = K._TUNE, K._tuned, K._CONV_IMPL
+    K._TUNE, K._tuned, K._CONV_IMPL = False, {}, "ours"  # the ranks' FF_GEMM_TUNE=0 / FF_CONV_IMPL=ours
+    try:
+        ref = _train_cnn(None)
+    finally:
+        K._TUNE, K._tuned, K._CONV_IMPL = tune, tuned, impl
+        for k, v in old.items():
+            if v is not None:
+                os.environ[k] = v
+    for k, v in ref.items():
+        if k.startswith("__"):
+            continue
+        rel = np.linalg.norm(par[k] - v) / (np.linalg.norm(v) + 1e-12)
+        assert rel < 3e-2, f"halo conv: {k} relative difference {rel}"  # bf16, different split points

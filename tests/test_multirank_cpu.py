@@ -112,6 +112,19 @@ def _strategy(case, ff, world):
         h = world // 2
         return {"x": cfg("x", [world]), "da": cfg("da", [h], range(h)), "db": cfg("db", [h], range(h, world)),
                 "sum": cfg("sum", [world]), "head": cfg("head", [world]), "sm": cfg("sm", [world])}
+    if case == "inception_halo":
+        # attribute parallelism forced (BASELINE config #3's halo exchange): the first convs that
+        # allow it split H and W 2 x 2 (x 2 samples) over the 8 ranks, everything else data parallel
+        from flexflow_amd.pcg.strategy import data_parallel_strategy, valid_config
+        from flexflow_amd.type import OperatorType as OT
+        st = data_parallel_strategy(ff.layers, world)
+        n = 0
+        for l in ff.layers:
+            if l.op_type == OT.OP_CONV2D and n < 3 and valid_config(l, cfg(l.name, [world // 4, 1, 2, 2])):
+                st[l.name] = cfg(l.name, [world // 4, 1, 2, 2])
+                n += 1
+        assert n > 0
+        return st
     if case == "mlp2d" and world == 4:
         return {"x": cfg("x", [4]), "d1": cfg("d1", [2, 2]), "d2": cfg("d2", [1, 2, 2]),
                 "d3": cfg("d3", [2, 2], [3, 2, 1, 0]), "sm": cfg("sm", [2], [2, 3])}
@@ -258,6 +271,22 @@ def test_inception_attribute_parallel_plan_world8(monkeypatch):
     print("inception attr@8 rewrites", [r["xfer"] for r in search["rewrites"]], "degree vectors", sorted(kinds),
           {k: rep.get(k) for k in ("predicted_ms", "predicted_dp_ms", "graphs_costed")})
     assert rep["predicted_ms"] <= rep["predicted_dp_ms"], rep
+
+
+@pytest.mark.parametrize("boxes", [False, True])
+def test_inception_halo_plan_world8(boxes, monkeypatch):
+    """A spatially split (halo-exchanging) Inception plan at world 8 executes and matches one
+    process: convs split 2 (N) x 2 (H) x 2 (W), their halo'd input blocks assembled by the generic
+    transfer, their input-gradient halos summed back — boxes=True through the box-copy plans the
+    GPU runs (emulated on CPU), whose add-mode boxes overlap at the 2-D halo corners."""
+    if boxes:
+        monkeypatch.setenv("FF_BOXCOPY_EMULATE", "1")
+    par, search, _ = _run("inception_small", 8, strat_case="inception_halo")
+    spatial = [k for k, v in search["strategy"].items() if len(v["degrees"]) >= 4 and
+               (v["degrees"][2] > 1 or v["degrees"][3] > 1)]
+    assert spatial, search["strategy"]
+    ref = _single("inception_small")
+    _compare(par, ref, "inception_small@8 halo")
 
 
 @pytest.mark.parametrize("world", [4, 8])
