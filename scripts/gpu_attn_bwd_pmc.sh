@@ -11,5 +11,5 @@ for v in "$@"; do
   timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
     -d $OUT/b$v -o run --output-format csv -- python3 $R/scripts/attn_bwd_only.py 32 16 512 64 $v 5 > $OUT/b$v.log 2>&1 || exit 1
   echo "variant $v"
-  python3 $R/scripts/pmc_summary.py 'attn_bwd_kernel' $(find $OUT/a$v $OUT/b$v -name '*counter_collection.csv')
+  python3 $R/scripts/pmc_summary.py 'attn_bwd' $(find $OUT/a$v $OUT/b$v -name '*counter_collection.csv')
 done
