@@ -130,7 +130,15 @@ void sgd_sparse_rows(const int64_t* idx, int n, int64_t rows, int dim, int* mark
 
 // max_blocks > 0 caps the grid (an update overlapped with the backward on a side stream leaves CU
 // slots to the compute stream's kernels; the grid-stride loops keep enough bytes in flight).
+// max_blocks < 0: short-lived workgroups instead of a grid-stride sweep — each thread updates about
+// -max_blocks float4 groups and exits, so the CU slots of an overlapped update are handed back to
+// the compute stream every few microseconds (a 2048-block sweep held every wave slot of every CU
+// for its whole ~95 us and starved the backward's small-grid kernels, ~1.4 ms/step of BERT-Large).
 static int opt_grid(int64_t n, int max_blocks) {
+  if (max_blocks < 0) {
+    const int64_t per = 256 * (int64_t)(-max_blocks);
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + per - 1) / per, 1 << 30));
+  }
   const int g = ew_grid(n / 4 + 1, 256);
   return max_blocks > 0 ? std::min(g, max_blocks) : g;
 }

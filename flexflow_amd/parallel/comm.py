@@ -390,12 +390,26 @@ class Transfer:
         sdev, ddev = _a2a_devices(S, D, blk, a, b, k)
         grp = sorted(sdev)
         chunks = x.chunk(k, dim=b)  # chunk j belongs to the rank holding dst block j along b
-        inp = torch.stack([chunks[ddev.index(g)] for g in grp], 0).contiguous()
+        boxes = boxcopy.available(x)
+        if boxes:  # one launch: every chunk into its group-rank slot of the send buffer
+            inp = torch.empty((k,) + tuple(chunks[0].shape), dtype=x.dtype, device=x.device)
+            self._box_plan("a2a_pack", x, inp, lambda: _view_boxes(
+                [(chunks[ddev.index(g)], inp[i]) for i, g in enumerate(grp)], x, inp)).run(x, inp)
+        else:
+            inp = torch.stack([chunks[ddev.index(g)] for g in grp], 0).contiguous()
         out = torch.empty_like(inp)
         h = dist.all_to_all_single(out, inp, group=comm.group(grp), async_op=True)
 
         def finish():
             # out[q] came from group rank q, which holds src block sdev.index(grp[q]) along a
+            if boxes:  # one launch: each received block into its slice along a
+                shp = list(out.shape[1:])
+                shp[a] *= k
+                res = torch.empty(shp, dtype=out.dtype, device=out.device)
+                ca = out.shape[1 + a]
+                self._box_plan("a2a_unpack", out, res, lambda: _view_boxes(
+                    [(out[grp.index(sdev[i])], res.narrow(a, i * ca, ca)) for i in range(k)], out, res)).run(out, res)
+                return res
             return torch.cat([out[grp.index(sdev[i])] for i in range(k)], dim=a).contiguous()
         del me
         return Pending([h], finish, kind="all_to_all", nbytes=self.bytes_moved(x.element_size()))
@@ -414,7 +428,16 @@ class Transfer:
         xm = x.movedim(d, 0)
         chunks = list(xm.chunk(k, 0))
         order = [sub_dev.index(g) for g in grp]  # chunk for group-rank i
-        inp = torch.cat([chunks[j] for j in order], 0).contiguous() if order != list(range(k)) else xm.contiguous()
+        boxes = boxcopy.available(x)
+        if order == list(range(k)) and xm.is_contiguous():
+            inp = xm
+        elif boxes:  # one launch: the chunks, dim d first, in group-rank order
+            inp = torch.empty(tuple(xm.shape), dtype=x.dtype, device=x.device)
+            m0 = chunks[0].shape[0]
+            self._box_plan("rs_pack", x, inp, lambda: _view_boxes(
+                [(chunks[j], inp.narrow(0, i * m0, m0)) for i, j in enumerate(order)], x, inp)).run(x, inp)
+        else:
+            inp = torch.cat([chunks[j] for j in order], 0).contiguous() if order != list(range(k)) else xm.contiguous()
         out_shape = list(inp.shape)
         out_shape[0] //= k
         out = torch.empty(out_shape, dtype=x.dtype, device=x.device)
@@ -422,7 +445,17 @@ class Transfer:
         nb = self.bytes_moved(x.element_size())
         # one code path for every backend: RCCL on the GPU, gloo in the CPU multi-rank tests
         h = dist.reduce_scatter_tensor(out, inp, group=g, async_op=True)
-        return Pending([h], lambda: out.movedim(0, d).contiguous(), kind="reduce_scatter", nbytes=nb)
+
+        def finish():
+            if d == 0:
+                return out
+            if boxes:  # one launch: dim d back in place
+                res = torch.empty(tuple(out.movedim(0, d).shape), dtype=out.dtype, device=out.device)
+                self._box_plan("rs_unpack", out, res, lambda: _view_boxes([(out.movedim(0, d), res)], out, res)
+                               ).run(out, res)
+                return res
+            return out.movedim(0, d).contiguous()
+        return Pending([h], finish, kind="reduce_scatter", nbytes=nb)
 
     def _all_gather(self, comm, x):
         S, D, d, r = self.src, self.dst, self.dim, self.rank
@@ -434,7 +467,15 @@ class Transfer:
             fb = list(qblk)
             fb[d] = qblk[d] * k + j
             sub_dev.append(S.devices[S.part_index(fb, 0)])
-        xm = x.movedim(d, 0).contiguous()
+        boxes = boxcopy.available(x)
+        xv = x.movedim(d, 0)
+        if xv.is_contiguous():
+            xm = xv
+        elif boxes:  # one launch: dim d first (the collective's contiguous send buffer)
+            xm = torch.empty(tuple(xv.shape), dtype=x.dtype, device=x.device)
+            self._box_plan("ag_pack", x, xm, lambda: _view_boxes([(xv, xm)], x, xm)).run(x, xm)
+        else:
+            xm = xv.contiguous()
         g = comm.group(grp)
         nb = self.bytes_moved(x.element_size())
         out = torch.empty((k * xm.shape[0],) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
@@ -443,7 +484,19 @@ class Transfer:
 
         def finish():
             # chunks[i] came from group-rank i == device grp[i]; reorder to dim order
-            ordered = [chunks[grp.index(dev)] for dev in sub_dev]
+            order = [grp.index(dev) for dev in sub_dev]
+            if d == 0 and order == list(range(k)):
+                return out
+            if boxes:  # one launch: every block into its slice along d, in dim order
+                shp = list(x.shape)
+                shp[d] *= k
+                res = torch.empty(shp, dtype=out.dtype, device=out.device)
+                m0 = xv.shape[0]
+                self._box_plan("ag_unpack", out, res, lambda: _view_boxes(
+                    [(chunks[c].movedim(0, d), res.narrow(d, j * m0, m0)) for j, c in enumerate(order)], out, res)
+                ).run(out, res)
+                return res
+            ordered = [chunks[c] for c in order]
             return torch.cat(ordered, 0).movedim(0, d).contiguous()
         return Pending([h], finish, kind="all_gather", nbytes=nb)
 
@@ -567,6 +620,19 @@ class Transfer:
             return out
         return Pending(reqs, finish, kind="generic", nbytes=(sbuf.numel() * sbuf.element_size()) if sbuf is not None
                        else 0)
+
+
+def _view_boxes(pairs, src, dst):
+    """Boxes moving each (source view, destination view) pair of equal shape: views of `src` /
+    `dst` built with ordinary view ops (movedim / narrow / chunk / index), their storage offsets
+    and strides taken relative to the base tensors the plan is run on — the collective reorders
+    (one launch each instead of ATen cat / stack / movedim copies)."""
+    boxes = []
+    for sv, dv in pairs:
+        assert tuple(sv.shape) == tuple(dv.shape), (sv.shape, dv.shape)
+        boxes.append((sv.storage_offset() - src.storage_offset(), tuple(sv.stride()),
+                      dv.storage_offset() - dst.storage_offset(), tuple(dv.stride()), tuple(sv.shape)))
+    return boxes
 
 
 def _regions_overlap(a, b) -> bool:

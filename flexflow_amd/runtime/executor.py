@@ -279,7 +279,8 @@ class Executor:
         self._opt_next_done = None  # the optimizer whose next() the overlapped backward already ran
         self._bwd_since_update = 0   # backward passes since the last update (row-sparse SGD guard)
         self.bucketer.on_ready = self._on_bucket_ready
-        # workgroup cap of the overlapped update launches (FF_UPD_BLOCKS; 0 = the full 2048 grid)
+        # workgroup cap of the overlapped update launches (FF_UPD_BLOCKS; 0 = the full 2048-block
+        # sweep; < 0 = short-lived workgroups of -N float4 groups per thread, see optimizer.hip)
         self._upd_blocks = int(os.environ.get("FF_UPD_BLOCKS", "0"))
         self._sparse, self._sparse_key = {}, None  # row-sparse SGD plan (_sparse_plan)
         self._sparse_cleared = {}  # arena group -> [(lo, hi)] whose gradient the sparse update cleared
@@ -602,7 +603,7 @@ class Executor:
         if ar is None or b["hi"] <= b["lo"]:
             return
         if self._upd_stream is None:
-            self._upd_stream = torch.cuda.Stream(device=self.device)
+            self._upd_stream = self._make_upd_stream()
         ev = torch.cuda.Event()
         ev.record()
         with torch.cuda.stream(self._upd_stream):
@@ -614,6 +615,22 @@ class Executor:
             else:  # plain call: user optimizers may implement step_range(arena, lo, hi) only
                 self.model.optimizer.step_range(ar, b["lo"], b["hi"])
         self._upd_done.add(id(b))
+
+    def _make_upd_stream(self):
+        """The overlapped update's side stream, at the LOWEST priority the device offers
+        (FF_UPD_PRIO overrides; torch's default streams sit at 0): when both streams have work
+        ready, the hardware scheduler hands freed CU slots to the backward's kernels first."""
+        prio = os.environ.get("FF_UPD_PRIO", "low")
+        p = 0
+        if prio == "low":
+            try:
+                least, greatest = torch.cuda.Stream.priority_range()
+                p = max(least, greatest)  # numerically larger = lower priority
+            except Exception:
+                p = 0
+        elif prio != "default":
+            p = int(prio)
+        return torch.cuda.Stream(device=self.device, priority=p)
 
     def backward(self, overlap_update: bool = False):
         """overlap_update: update each gradient bucket as soon as it is final (see
@@ -632,7 +649,7 @@ class Executor:
                  and os.environ.get("FF_DEFER_FOLDS", "0") == "1")
         if defer:
             if self._upd_stream is None:
-                self._upd_stream = torch.cuda.Stream(device=self.device)
+                self._upd_stream = self._make_upd_stream()
             K.set_reduce_stream(self._upd_stream)
             self._folds_pending = True
         try:

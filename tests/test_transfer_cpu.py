@@ -26,6 +26,12 @@ CASES = [
     (Layout((8, 6), (1, 1), 4, (0, 1, 2, 3)), Layout((8, 6), (2, 2), 1, (3, 1, 2, 0)), True, "generic"),
     (Layout((8, 6), (1, 1), 4, (0, 1, 2, 3)), Layout((8, 6), (4, 1), 1, (0, 1, 2, 3)), True, "reduce_scatter"),
     (Layout((8, 6), (4, 1), 1, (0, 1, 2, 3)), Layout((8, 6), (1, 1), 4, (0, 1, 2, 3)), False, "all_gather"),
+    # the reorders around the collectives: split dim != 0 (dim moved first and back) and permuted
+    # device order (chunks out of group-rank order)
+    (Layout((6, 8), (1, 1), 4, (0, 1, 2, 3)), Layout((6, 8), (1, 4), 1, (3, 1, 2, 0)), True, "reduce_scatter"),
+    (Layout((6, 8), (1, 4), 1, (2, 0, 3, 1)), Layout((6, 8), (1, 1), 4, (0, 1, 2, 3)), False, "all_gather"),
+    (Layout((4, 6, 8), (1, 1, 4), 1, (0, 1, 2, 3)), Layout((4, 6, 8), (1, 1, 1), 4, (0, 1, 2, 3)), False,
+     "all_gather"),
 ]
 
 
@@ -77,7 +83,10 @@ def test_transfers_over_gloo(tmp_path, monkeypatch, boxes):
         d = dict(np.load(tmp_path / f"r{r}.npz"))
         for i in range(len(CASES)):
             assert bool(d[f"kind{i}"][0]), (r, i, "kind")
-            if CASES[i][3] == "exchange":  # every rank packs and unpacks through box plans
+            if CASES[i][3] in ("exchange", "all_to_all") or i >= 9:
+                # every rank packs / unpacks (exchange) or reorders around the collective (all-to-
+                # all; reduce-scatter / all-gather along dim != 0 or out of group-rank order)
+                # through box plans, not ATen cat / stack / movedim copies
                 assert bool(d[f"plans{i}"][0]) == boxes, (r, i, "box plans")
             if f"ok{i}" in d:
                 assert bool(d[f"ok{i}"][0]), (r, i, "value")

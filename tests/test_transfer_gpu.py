@@ -162,3 +162,53 @@ def test_gather_kernels_match_torch(ffC, dtype, itype, dim):
     ffC.gather_bwd(dy, idx, dx, ishp[dim], inner, shp[dim])
     ref = torch.zeros(shp, device=DEV).scatter_add_(dim, idx.long(), dy.float())
     assert torch.allclose(dx, ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("d", [0, 1, 2])
+def test_collective_reorder_plans_match_torch(dtype, d):
+    """The box plans around the collectives (parallel/comm.py _view_boxes): the all-gather send
+    buffer (dim d first) and its unpack (blocks into their slices along d, out of group-rank order),
+    the reduce-scatter pack (chunks in group-rank order) and the all-to-all pack / unpack — each one
+    transfer.hip launch — against the ATen movedim / cat / stack they replace."""
+    from flexflow_amd.parallel.comm import _view_boxes
+    torch.manual_seed(5)
+    k = 4
+    x = torch.randn(8, 12, 16, device=DEV).to(dtype)
+    order = [2, 0, 3, 1]
+    # all-gather: send buffer, then k received blocks unpacked in `order`
+    xv = x.movedim(d, 0)
+    xm = torch.empty(tuple(xv.shape), device=DEV, dtype=dtype)
+    boxcopy.BoxPlan(_view_boxes([(xv, xm)], x, xm), x, xm).run(x, xm)
+    assert torch.equal(xm, xv.contiguous())
+    out = torch.stack([xm * (i + 1) for i in range(k)], 0).reshape((k * xm.shape[0],) + tuple(xm.shape[1:]))
+    chunks = list(out.chunk(k, 0))
+    shp = list(x.shape)
+    shp[d] *= k
+    res = torch.empty(shp, device=DEV, dtype=dtype)
+    m0 = xv.shape[0]
+    boxcopy.BoxPlan(_view_boxes([(chunks[c].movedim(0, d), res.narrow(d, j * m0, m0)) for j, c in enumerate(order)],
+                                out, res), out, res).run(out, res)
+    assert torch.equal(res, torch.cat([chunks[c] for c in order], 0).movedim(0, d).contiguous())
+    # reduce-scatter pack: x's chunks along d, dim d first, in group-rank order
+    if x.shape[d] % k == 0:
+        ch = list(xv.chunk(k, 0))
+        inp = torch.empty(tuple(xv.shape), device=DEV, dtype=dtype)
+        c0 = ch[0].shape[0]
+        boxcopy.BoxPlan(_view_boxes([(ch[j], inp.narrow(0, i * c0, c0)) for i, j in enumerate(order)], x, inp),
+                        x, inp).run(x, inp)
+        assert torch.equal(inp, torch.cat([ch[j] for j in order], 0))
+    # all-to-all pack along dim d, unpack along dim (d + 1) % 3
+    if x.shape[d] % k == 0:
+        a = (d + 1) % 3
+        ch = x.chunk(k, dim=d)
+        inp = torch.empty((k,) + tuple(ch[0].shape), device=DEV, dtype=dtype)
+        boxcopy.BoxPlan(_view_boxes([(ch[order[i]], inp[i]) for i in range(k)], x, inp), x, inp).run(x, inp)
+        assert torch.equal(inp, torch.stack([ch[order[i]] for i in range(k)], 0))
+        s2 = list(inp.shape[1:])
+        s2[a] *= k
+        res = torch.empty(s2, device=DEV, dtype=dtype)
+        ca = inp.shape[1 + a]
+        boxcopy.BoxPlan(_view_boxes([(inp[order[i]], res.narrow(a, i * ca, ca)) for i in range(k)], inp, res),
+                        inp, res).run(inp, res)
+        assert torch.equal(res, torch.cat([inp[order[i]] for i in range(k)], dim=a))
