@@ -617,10 +617,11 @@ class Executor:
         self._upd_done.add(id(b))
 
     def _make_upd_stream(self):
-        """The overlapped update's side stream, at the LOWEST priority the device offers
-        (FF_UPD_PRIO overrides; torch's default streams sit at 0): when both streams have work
-        ready, the hardware scheduler hands freed CU slots to the backward's kernels first."""
-        prio = os.environ.get("FF_UPD_PRIO", "low")
+        """The overlapped update's side stream. FF_UPD_PRIO=low puts it at the lowest priority the
+        device offers (torch's default streams sit at 0), so that when both streams have work ready
+        the hardware scheduler hands freed CU slots to the backward's kernels first; "default" (the
+        default) or an integer priority otherwise."""
+        prio = os.environ.get("FF_UPD_PRIO", "default")
         p = 0
         if prio == "low":
             try:
