@@ -28,6 +28,7 @@ struct AttnArgs {
   float scale = 1.f;
   int causal = 0;
   float rescale_thr = 8.f;  // forward: deferred-max threshold, log2 units (attn_set_rescale_thr)
+  int stagger = 0;  // backward (attn_bwd1b_kernel): waves 4-7 run each dQ chunk after the softmax
 };
 
 void attn_fwd(AttnArgs a, hipStream_t st);
@@ -39,6 +40,8 @@ void attn_set_bwd_variant(int v);
 int attn_fwd_variant();
 void attn_set_fwd_variant(int v);
 float attn_rescale_thr();
+int attn_stagger();
+void attn_set_stagger(int v);
 void attn_set_rescale_thr(float t);
 
 }  // namespace ffk

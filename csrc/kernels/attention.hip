@@ -955,6 +955,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
   char* ds0 = k_l + KB * D * 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bool late = a.stagger && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
   const int groups = CHAIN ? 1 : nkb;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int bh = lid / groups, b = bh / a.H, hh = bh % a.H;
@@ -1053,7 +1054,11 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
       }
-      hook(2 * qt);
+      // stagger (a.stagger): waves w and w + 4 share a SIMD and would otherwise reach the
+      // softmax VALU together; waves 4-7 run the dQ chunk after it instead, so one wave of each
+      // pair issues MFMAs while its partner runs the exp / dS arithmetic (MI355X_MICROARCH.md,
+      // 'Two waves per SIMD', item 9)
+      if (!late) hook(2 * qt);
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 L4 = *reinterpret_cast<const float4*>(lse_l + 32 * qt + 8 * g4 + 4 * h);
@@ -1080,6 +1085,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
       }
       const bf16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
       const bf16x8 sb0 = pack8(pacc, 0), sb1 = pack8(pacc, 8);
+      if (late) hook(2 * qt);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
         const int col = dt * 32 + 16 * (G & 1) + 4 * pi;
@@ -1368,6 +1374,17 @@ float attn_rescale_thr() {
 }
 void attn_set_rescale_thr(float t) { g_rescale_thr = fmaxf(0.f, t); }
 
+// attn_bwd1b_kernel wave stagger (AttnArgs.stagger): FF_ATTN_STAGGER, attn_set_stagger (A/B)
+static int g_stagger = -1;
+int attn_stagger() {
+  if (g_stagger < 0) {
+    const char* e = getenv("FF_ATTN_STAGGER");
+    g_stagger = e ? (atoi(e) != 0) : 0;
+  }
+  return g_stagger;
+}
+void attn_set_stagger(int v) { g_stagger = v != 0; }
+
 void attn_fwd(AttnArgs a, hipStream_t st) {
   const dim3 grid((unsigned)((a.Sq + 127) / 128 * a.B * a.H));
   const bool mask = a.causal || a.Sk % 64 != 0;
@@ -1416,6 +1433,7 @@ static void launch_bwd_main(AttnArgs a, int nkb, bool chain, hipStream_t st) {
 
 bool attn_bwd(AttnArgs a, hipStream_t st) {
   bool bias_done = false;
+  a.stagger = attn_stagger();
   const int v = attn_bwd_variant();
   const int nkb = (a.Sk + bwd_keys(a.D) - 1) / bwd_keys(a.D);
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;

@@ -865,6 +865,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd_variant", []() { return ffk::attn_fwd_variant(); });
   m.def("attn_set_fwd_variant", [](int v) { ffk::attn_set_fwd_variant(v); });
   m.def("attn_bwd_variant", []() { return ffk::attn_bwd_variant(); });
+  m.def("attn_stagger", []() { return ffk::attn_stagger(); });
+  m.def("attn_set_stagger", [](int v) { ffk::attn_set_stagger(v); });
   m.def("attn_rescale_thr", []() { return ffk::attn_rescale_thr(); });
   m.def("attn_set_rescale_thr", [](double t) { ffk::attn_set_rescale_thr((float)t); });
   m.def("batchnorm_fwd", &batchnorm_fwd);

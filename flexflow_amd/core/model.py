@@ -577,13 +577,33 @@ class FFModel:
         from ..runtime.graph import run_train_step
         if self.watchdog is not None:
             self.watchdog.arm()
-        run_train_step(self)
+        hi = self._compute_stream()
+        if hi is None:
+            run_train_step(self)
+        else:  # the step's kernels on a high-priority stream, joined both ways with the caller's
+            cur = torch.cuda.current_stream()
+            hi.wait_stream(cur)
+            with torch.cuda.stream(hi):
+                run_train_step(self)
+            cur.wait_stream(hi)
         if self.watchdog is not None:
             self.watchdog.disarm()
         if self.profiler is not None:
             self.profiler.next_step()
         if self.guard is not None:
             self.guard.after_step(self.executor._metric_acc[0])
+
+    def _compute_stream(self):
+        """FF_COMPUTE_PRIO=high: train steps run on a stream of the device's highest priority, so
+        that the overlapped optimizer update (a default-priority side stream) yields freed CU slots
+        to the backward's kernels. None (the caller's stream) otherwise, or without a GPU."""
+        if os.environ.get("FF_COMPUTE_PRIO", "default") != "high" or not torch.cuda.is_available():
+            return None
+        st = getattr(self, "_hi_stream", None)
+        if st is None:
+            _, greatest = torch.cuda.Stream.priority_range()
+            st = self._hi_stream = torch.cuda.Stream(priority=greatest)
+        return st
 
     # ---- checkpoint / profiling
     def save_checkpoint(self, path):
