@@ -206,7 +206,7 @@ def main():
     if rep.get("predicted_speedup_vs_dp") is not None:
         res["search"] = {k: rep[k] for k in ("predicted_ms", "predicted_dp_ms", "predicted_speedup_vs_dp",
                                              "candidates", "search_s", "search_wall_s", "graphs_costed",
-                                             "timed_out", "measured_costs") if k in rep}
+                                             "timed_out", "measured_costs", "cost_lookups") if k in rep}
     if verify is not None:
         res["search_verification"] = verify
         if "dp_ms" in verify:

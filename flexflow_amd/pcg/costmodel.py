@@ -36,6 +36,7 @@ _measured: Dict[tuple, Tuple[float, float]] = {}
 # (measured on MI355X by scripts/gpu_cost_table.sh) is read, never written. FF_COST_CACHE=0: off.
 _SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "op_costs_mi355x.json")
 _disk = {"path": None, "table": None, "dirty": False}
+STATS = {"table_hits": 0, "timed": 0, "timed_s": 0.0}  # this process's measured-cost lookups
 
 
 def _cache_path():
@@ -195,7 +196,10 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
     hit = _disk_get(key, device)
     if hit is not None:
         _measured[key] = hit
+        STATS["table_hits"] += 1
         return hit
+    STATS["timed"] += 1
+    t_start = time.perf_counter()
     ct = torch.bfloat16 if compute_dtype == DataType.DT_BF16 else torch.float32
 
     hot = _hot_inputs(layer)
@@ -317,6 +321,7 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
         tf = max(med["df"], med["hf"])
         tb = max(med["db"], med["hb"])
         _disk_put(key, device, tf, tb)
+        STATS["timed_s"] += time.perf_counter() - t_start
         del ctxs, xs_all, ws_all
     except Exception:
         tf, tb = analytic_cost(layer, cfg, compute_dtype)

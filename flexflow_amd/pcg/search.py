@@ -103,6 +103,8 @@ def choose_strategy(model):
         strat, report = native_search(model, algo)
     report = dict(report or {})
     report["search_wall_s"] = round(time.perf_counter() - t0, 2)  # measurement + search, rank 0
+    from .costmodel import STATS
+    report["cost_lookups"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in STATS.items()}
     from .costmodel import save_cost_table
     save_cost_table()
     if distributed:

@@ -36,6 +36,7 @@ from flexflow_amd.pcg.substitutions import optimize_graph  # noqa: E402
 for n in a.n:
     costmodel._measured.clear()  # every N (and every repeat) measures or reads the table afresh
     costmodel._disk["table"] = None
+    costmodel.STATS.update(table_hits=0, timed=0, timed_s=0.0)
     cfg = FFConfig(["--dtype", "bf16", "--search", "unity", "--search-num-workers", str(n)])
     gb = a.batch_per_gpu * n
     cfg.batch_size = gb
@@ -55,6 +56,7 @@ for n in a.n:
     print(json.dumps({"n": n, "model": a.model, "global_batch": gb, "wall_s": round(wall, 1),
                       "cost_cache": os.environ.get("FF_COST_CACHE", "(shipped, read-only)"),
                       **{k: rep.get(k) for k in ("predicted_ms", "predicted_dp_ms", "predicted_speedup_vs_dp",
-                                                 "graphs_costed", "timed_out", "search_wall_s", "measured_costs")},
+                                                 "graphs_costed", "timed_out", "search_wall_s", "measured_costs",
+                                                 "cost_lookups")},
                       "rewrites": len(rep.get("rewrites") or []), "non_dp_degree_vectors": [list(d) for d in multi][:8]}),
           flush=True)
