@@ -136,6 +136,33 @@ void box_copy(std::vector<Tensor> srcs, Tensor dst, Tensor desc, int64_t nbox, i
                 (int)vec_bytes, add ? 1 : 0, dt, idx32 ? 1 : 0, cur_stream());
 }
 
+// out [outer][sum lens] (vec units) = concat of srcs [outer][lens[i]]; sizes and alignment checked here
+void concat_rows(std::vector<Tensor> srcs, std::vector<int64_t> lens, Tensor out, int64_t outer, int64_t vec_bytes) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ffk::kBoxSrcs && srcs.size() == lens.size(), "concat_rows: 1..16 inputs");
+  TORCH_CHECK(vec_bytes == 2 || vec_bytes == 4 || vec_bytes == 8 || vec_bytes == 16, "concat_rows: vector width");
+  check_dev(out, "out");
+  const int64_t esz = out.element_size();
+  TORCH_CHECK(vec_bytes % esz == 0 && (reinterpret_cast<uintptr_t>(out.data_ptr()) % vec_bytes) == 0,
+              "concat_rows: output alignment");
+  int64_t row = 0;
+  std::vector<const void*> ptrs;
+  std::vector<int> l32;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& t = srcs[i];
+    check_dev(t, "src");
+    TORCH_CHECK(t.scalar_type() == out.scalar_type(), "concat_rows: one dtype");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) % vec_bytes) == 0, "concat_rows: input alignment");
+    TORCH_CHECK(lens[i] > 0 && t.numel() * esz == outer * lens[i] * vec_bytes, "concat_rows: input size");
+    // 32-bit grid-stride index: the last step (at most 8192 x 256 past the end) stays below 2^31
+    TORCH_CHECK(outer * lens[i] + 8192LL * 256 < (1LL << 31), "concat_rows: input too large for 32-bit indexing");
+    row += lens[i];
+    ptrs.push_back(t.data_ptr());
+    l32.push_back((int)lens[i]);
+  }
+  TORCH_CHECK(out.numel() * esz == outer * row * vec_bytes && outer < (1LL << 31), "concat_rows: output size");
+  ffk::concat_rows(ptrs.data(), l32.data(), (int)ptrs.size(), out.data_ptr(), (int)outer, (int)vec_bytes, cur_stream());
+}
+
 // x [.., xd, inner] and idx / out [.., dsz, inner], contiguous, other dims equal (checked by caller)
 void gather_fwd(Tensor x, Tensor idx, Tensor out, int64_t dsz, int64_t inner, int64_t xd) {
   check_dev(x, "x"); check_dev(idx, "idx"); check_dev(out, "out");
@@ -844,6 +871,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("init_normal", &init_normal);
   m.def("fill", &fill);
   m.def("slab_sum", &slab_sum);
+  m.def("concat_rows", &concat_rows);
   m.def("gemm_f32", &gemm_f32);
   m.def("causal_mask_f32", &causal_mask_f32);
   m.def("topk_fwd", &topk_fwd);

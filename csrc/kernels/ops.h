@@ -57,6 +57,9 @@ int box_words();
 int box_dims();
 void box_copy(const void* const* srcs, int nsrc, void* dst, const int64_t* desc, int nbox, int64_t max_n,
               int vec_bytes, int add, int dt, int idx32, hipStream_t st);
+// out [outer][sum lens] = concat of x_i [outer][lens[i]] (units of vec_bytes; transfer.hip)
+void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, int outer, int vec_bytes,
+                 hipStream_t st);
 
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
 // on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.

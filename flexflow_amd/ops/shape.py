@@ -180,15 +180,20 @@ class Concat(OpImpl):
         return [tuple(range(n)) for _ in self.layer.inputs]
 
     def forward(self, ctx, xs, ws):
-        ctx.saved["sizes"] = [x.shape[self.attrs["axis"]] for x in xs]
-        # the forward stays on torch.cat (one ATen launch) unless FF_BOX_CONCAT=1: the box-kernel
-        # concat measured 12.5 -> 12.9 ms per Inception-v3 b64 step (profiles/concat_box_ab_r5.txt)
-        if len(xs) > 1 and _box_ok(xs[0]) and os.environ.get("FF_BOX_CONCAT", "0") == "1" \
-                and all(x.dtype == xs[0].dtype for x in xs):
-            out = boxcopy.concat(self.__dict__.setdefault("_box_plans", {}), list(xs), self.attrs["axis"])
+        ax = self.attrs["axis"]
+        ctx.saved["sizes"] = [x.shape[ax] for x in xs]
+        if len(xs) > 1 and xs[0].is_cuda and os.environ.get("FF_CAT_KERNEL", "1") == "1":
+            out = _concat_rows(list(xs), ax)
             if out is not None:
                 return [out]
-        return [torch.cat(xs, self.attrs["axis"])]
+        # FF_BOX_CONCAT=1: the generic box-kernel concat (measured 12.5 -> 12.9 ms per Inception-v3
+        # b64 step, profiles/concat_box_ab_r5.txt)
+        if len(xs) > 1 and _box_ok(xs[0]) and os.environ.get("FF_BOX_CONCAT", "0") == "1" \
+                and all(x.dtype == xs[0].dtype for x in xs):
+            out = boxcopy.concat(self.__dict__.setdefault("_box_plans", {}), list(xs), ax)
+            if out is not None:
+                return [out]
+        return [torch.cat(xs, ax)]
 
     def backward(self, ctx, douts):
         sizes = ctx.saved.pop("sizes")
@@ -196,6 +201,42 @@ class Concat(OpImpl):
         if len(sizes) > 1 and _box_ok(dy) and os.environ.get("FF_BOX_SPLIT", "1") == "1":
             return _split_dense(self, dy, sizes, self.attrs["axis"])
         return list(torch.split(dy, sizes, self.attrs["axis"]))
+
+
+def _concat_rows(xs, ax):
+    """torch.cat(xs, ax) by transfer.hip's concat_rows kernel (one launch, up to 16 inputs): dense
+    inputs of one dtype, either all contiguous (rows = the dims before ax) or all channel-last 4-D
+    concatenated along C (rows = N*H*W pixels). None when that does not apply (the caller falls
+    back). Reference: src/ops/kernels/concat_kernels.cu (one copy per input)."""
+    if len(xs) > 16 or any(x.dtype != xs[0].dtype or x.dim() != xs[0].dim() for x in xs):
+        return None
+    n = xs[0].dim()
+    shp = list(xs[0].shape)
+    shp[ax] = sum(x.shape[ax] for x in xs)
+    if all(x.is_contiguous() for x in xs):
+        outer = math.prod(shp[:ax])
+        lens = [x.shape[ax] * math.prod(x.shape[ax + 1:]) for x in xs]
+        out = torch.empty(shp, dtype=xs[0].dtype, device=xs[0].device)
+    elif n == 4 and ax == 1 and all(K.is_nhwc(x) for x in xs):
+        outer = shp[0] * shp[2] * shp[3]
+        lens = [x.shape[1] for x in xs]
+        # (allocated channel-last directly: empty(...).contiguous(channels_last) is a full copy)
+        out = torch.empty(shp, dtype=xs[0].dtype, device=xs[0].device, memory_format=torch.channels_last)
+    else:
+        return None
+    if outer == 0 or min(lens) == 0:
+        return None
+    es = xs[0].element_size()
+    for vb in (16, 8, 4, 2):
+        if vb % es == 0 and all((l * es) % vb == 0 for l in lens) and \
+                all(t.data_ptr() % vb == 0 for t in list(xs) + [out]):
+            break
+    else:
+        return None
+    if outer * max(lens) * es // vb + 8192 * 256 >= (1 << 31):
+        return None
+    K.ext().concat_rows(list(xs), [l * es // vb for l in lens], out, outer, vb)
+    return out
 
 
 def _split_dense(op, dy, sizes, ax):

@@ -213,8 +213,10 @@ def plan_key(role, *tensors) -> tuple:
 def _dense_like(shape, like: torch.Tensor, device=None, dtype=None):
     """An uninitialised tensor of `shape` in like's memory format (channel-last 4-D stays so)."""
     cl = like.dim() == 4 and not like.is_contiguous() and like.is_contiguous(memory_format=torch.channels_last)
-    t = torch.empty(shape, dtype=dtype or like.dtype, device=device or like.device)
-    return t.contiguous(memory_format=torch.channels_last) if cl and len(shape) == 4 else t
+    # allocated in the target format directly (empty(...).contiguous(channels_last) launched a full
+    # copy kernel per call: the r5 box-kernel concat A/B paid it, profiles/concat_box_ab_r5.txt)
+    fmt = torch.channels_last if cl and len(shape) == 4 else torch.contiguous_format
+    return torch.empty(shape, dtype=dtype or like.dtype, device=device or like.device, memory_format=fmt)
 
 
 def _cached(cache: dict, key, build):

@@ -212,3 +212,37 @@ def test_collective_reorder_plans_match_torch(dtype, d):
         boxcopy.BoxPlan(_view_boxes([(inp[order[i]], res.narrow(a, i * ca, ca)) for i in range(k)], inp, res),
                         inp, res).run(inp, res)
         assert torch.equal(res, torch.cat([inp[order[i]] for i in range(k)], dim=a))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["nhwc_c", "contig_0", "contig_1", "contig_3", "many"])
+def test_concat_rows_kernel_matches_torch_cat(dtype, case):
+    """Concat forward on transfer.hip's concat_rows (one launch, grid.y = input) against torch.cat:
+    Inception's channel-last channel concat, contiguous concats along several dims, 16 inputs;
+    widths that do not vectorize fall back (None)."""
+    from flexflow_amd.ops.shape import _concat_rows
+    torch.manual_seed(6)
+    if case == "nhwc_c":
+        xs = [torch.randn(8, c, 17, 17, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+              for c in (64, 96, 192, 32)]
+        ax = 1
+    elif case == "many":
+        xs = [torch.randn(5, 8 * (i + 1), device=DEV).to(dtype) for i in range(16)]
+        ax = 1
+    else:
+        ax = int(case[-1])
+        base = [6, 10, 4, 8]
+        xs = []
+        for c in (2, 3, 1):
+            s = list(base)
+            s[ax] = c * 8 if ax == 3 else c
+            xs.append(torch.randn(s, device=DEV).to(dtype))
+    out = _concat_rows(xs, ax)
+    assert out is not None
+    ref = torch.cat(xs, ax)
+    assert torch.equal(out, ref)
+    if case == "nhwc_c":
+        assert out.is_contiguous(memory_format=torch.channels_last)
+    odd = [torch.randn(3, 5, device=DEV).to(dtype), torch.randn(3, 7, device=DEV).to(dtype)]
+    r = _concat_rows(odd, 1)
+    assert r is None or torch.equal(r, torch.cat(odd, 1))
