@@ -176,6 +176,32 @@ def _hot_inputs(layer) -> list:
     return out
 
 
+def cost_params_key(layer) -> tuple:
+    """The op attributes that can change its cost, as stable strings: initializers are left out
+    (they run once, not per step) and object addresses are stripped — the r6 measured-cost table
+    missed 25 of BERT-Large's N = 8 entries in a fresh process because repr() of an initializer
+    object carries its address."""
+    import re
+    out = []
+    for k, v in layer.impl.params_key():
+        if k.endswith("_init") or k.endswith("initializer"):
+            continue
+        out.append((k, re.sub(r" at 0x[0-9a-fA-F]+", "", v)))
+    return tuple(out)
+
+
+def cost_key(layer, cfg: OpConfig, compute_dtype: DataType) -> tuple:
+    """What a measured cost depends on: op, cost-relevant attributes, shard shapes of inputs and
+    weights, degrees, dtype, whether the input gradient is needed, the inputs' cache temperature
+    and the op's role in a cross-op backward fusion (also the on-disk table's key, as repr)."""
+    lo = op_layouts(layer, cfg)
+    need_dx0 = bool(layer.inputs) and layer.inputs[0].owner_layer is not None and \
+        layer.inputs[0].owner_layer.op_type != OperatorType.OP_INPUT
+    return (layer.op_type, cost_params_key(layer), tuple(l.local_shape(0) for l in lo.inputs),
+            tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0,
+            tuple(_hot_inputs(layer)), (dact_fusion_partner(layer) or (None,))[0])
+
+
 def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: int = 8) -> Tuple[float, float]:
     """Time the op's own forward/backward on this GPU with the shard shapes of `cfg`, the way a
     training step runs it (reference simulator.cu measure_operator_cost; model.cu:38-75):
@@ -188,9 +214,7 @@ def measure_cost(layer, cfg: OpConfig, compute_dtype: DataType, device, reps: in
     lo = op_layouts(layer, cfg)
     need_dx0 = bool(layer.inputs) and layer.inputs[0].owner_layer is not None and \
         layer.inputs[0].owner_layer.op_type != OperatorType.OP_INPUT
-    key = (layer.op_type, layer.impl.params_key(), tuple(l.local_shape(0) for l in lo.inputs),
-           tuple(l.local_shape(0) for l in lo.weights), cfg.degrees, compute_dtype, need_dx0, tuple(_hot_inputs(layer)),
-           (dact_fusion_partner(layer) or (None,))[0])
+    key = cost_key(layer, cfg, compute_dtype)
     if key in _measured:
         return _measured[key]
     hit = _disk_get(key, device)
