@@ -163,6 +163,19 @@ void concat_rows(std::vector<Tensor> srcs, std::vector<int64_t> lens, Tensor out
   ffk::concat_rows(ptrs.data(), l32.data(), (int)ptrs.size(), out.data_ptr(), (int)outer, (int)vec_bytes, cur_stream());
 }
 
+// dst [cols][rows] = src [rows][cols]^T (2-byte elements, both contiguous, dims multiples of 8)
+void transpose2d(Tensor src, Tensor dst, int64_t max_blocks) {
+  check_dev(src, "src"); check_dev(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.is_contiguous() && dst.is_contiguous() &&
+              src.element_size() == 2 && dst.scalar_type() == src.scalar_type(), "transpose2d: contiguous 2-D 16-bit");
+  const int64_t r = src.size(0), c = src.size(1);
+  TORCH_CHECK(dst.size(0) == c && dst.size(1) == r, "transpose2d: dst must be [cols][rows]");
+  TORCH_CHECK(r % 8 == 0 && c % 8 == 0 && r * c < (1LL << 31), "transpose2d: dims multiples of 8, < 2^31 elements");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16) == 0,
+              "transpose2d: 16-B aligned");
+  ffk::transpose16(src.data_ptr(), dst.data_ptr(), (int)r, (int)c, (int)max_blocks, cur_stream());
+}
+
 // x [.., xd, inner] and idx / out [.., dsz, inner], contiguous, other dims equal (checked by caller)
 void gather_fwd(Tensor x, Tensor idx, Tensor out, int64_t dsz, int64_t inner, int64_t xd) {
   check_dev(x, "x"); check_dev(idx, "idx"); check_dev(out, "out");
@@ -872,6 +885,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill", &fill);
   m.def("slab_sum", &slab_sum);
   m.def("concat_rows", &concat_rows);
+  m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("dst"), py::arg("max_blocks") = 0);
   m.def("gemm_f32", &gemm_f32);
   m.def("causal_mask_f32", &causal_mask_f32);
   m.def("topk_fwd", &topk_fwd);

@@ -60,6 +60,8 @@ void box_copy(const void* const* srcs, int nsrc, void* dst, const int64_t* desc,
 // out [outer][sum lens] = concat of x_i [outer][lens[i]] (units of vec_bytes; transfer.hip)
 void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, int outer, int vec_bytes,
                  hipStream_t st);
+// dst [cols][rows] = src [rows][cols]^T, 2-byte elements, rows % 8 == cols % 8 == 0 (transfer.hip)
+void transpose16(const void* src, void* dst, int rows, int cols, int max_blocks, hipStream_t st);
 
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
 // on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.

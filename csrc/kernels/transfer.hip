@@ -162,6 +162,57 @@ void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, 
   }
 }
 
+// ------------------------------------------------------------------------------- transpose
+// dst [cols][rows] = src [rows][cols]^T for 2-byte elements, rows % 8 == 0 and cols % 8 == 0 (host
+// check). The Linear layers keep a transposed bf16 copy of each weight, refreshed every training
+// forward, so the input-gradient GEMM dx = dy . W reads W^T K-contiguous ("TN") instead of
+// N-contiguous ("NN"): on MI355X the library's TN GEMM of BERT-Large's dgrad shapes is 14-25 %
+// faster than its NN form (tuning/tunableop_gfx950.csv) and our ping-pong kernel's K-contiguous
+// B path avoids the transposing LDS reads altogether. One 64 x 64 tile per workgroup through LDS:
+// 16-B loads along source rows, 16-B stores along destination rows; the LDS row pitch of 72
+// elements (144 B) keeps every 16-B chunk aligned and spreads the column reads over the banks.
+// Grid: one workgroup per tile, or (max_blocks > 0) at most max_blocks workgroups striding over the
+// tiles — a refresh on a side stream then holds only that many CU slots beside the compute stream's
+// GEMMs (a full grid of 1024 workgroups per weight slowed the concurrent forward GEMMs by more than
+// the transposes cost on the compute stream).
+__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ src,
+                                                          uint16_t* __restrict__ dst, int rows, int cols) {
+  constexpr int P = 72;
+  __shared__ __attribute__((aligned(16))) uint16_t t[64 * P];
+  const int tc = (cols + 63) / 64, ntiles = tc * ((rows + 63) / 64);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int c0 = (tile % tc) * 64, r0 = (tile / tc) * 64;
+    if (tile != (int)blockIdx.x) __syncthreads();  // the previous tile's reads of t are done
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int id = threadIdx.x + 256 * j, r = id >> 3, ch = id & 7;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (r0 + r < rows && c0 + 8 * ch < cols)
+        v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + r) * cols + c0 + 8 * ch);
+      *reinterpret_cast<uint4*>(t + r * P + 8 * ch) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int id = threadIdx.x + 256 * j, oc = id >> 3, ch = id & 7;
+      if (c0 + oc >= cols || r0 + 8 * ch >= rows) continue;
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w[e] = (uint32_t)t[(8 * ch + 2 * e) * P + oc] | ((uint32_t)t[(8 * ch + 2 * e + 1) * P + oc] << 16);
+      *reinterpret_cast<uint4*>(dst + (int64_t)(c0 + oc) * rows + r0 + 8 * ch) = uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+
+void transpose16(const void* src, void* dst, int rows, int cols, int max_blocks, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return;
+  int tiles = ((cols + 63) / 64) * ((rows + 63) / 64);
+  if (max_blocks > 0) tiles = std::min(tiles, max_blocks);
+  hipLaunchKernelGGL(transpose16_kernel, dim3((unsigned)tiles), dim3(256), 0, st, (const uint16_t*)src, (uint16_t*)dst,
+                     rows, cols);
+}
+
 // ------------------------------------------------------------------------------- gather
 // torch.gather along one dim of contiguous tensors whose other dims match (reference
 // src/ops/gather.cc / kernels): out[o][j][i] = x[o][idx[o][j][i]][i]; the backward adds dy into an

@@ -671,13 +671,64 @@ def linear_fwd(x2d, w, bias, act, save_z, store_grad=False):
     return y, z
 
 
-def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None, on_dx=None):
+# Transposed weight copies (FF_WT_COPY, default on). The input-gradient GEMM dx = dy . W reads the
+# [out, in] weight N-contiguous ("NN"); on MI355X that form is 14-25 % slower than the K-contiguous
+# "TN" GEMM of the same M / N / K for BERT-Large's dgrad shapes, in the library (shipped TunableOp
+# table: nn_1024_16384_4096 0.0967 ms vs tn_1024_16384_4096 0.0726) and in our ping-pong kernel
+# (its MN-contiguous B path reads LDS through ds_read_b64_tr_b16). So every training forward of a
+# Linear whose input gradient is needed refreshes a persistent W^T [in, out] (transpose16 kernel,
+# ~4 B moved per weight element) on a side stream forked from the compute stream — it overlaps
+# the forward's GEMMs — and the backward waits for it before its dgrad. Refreshing every forward
+# keeps the copy exact whichever path wrote the weights (optimizer, all-gather, set_weights).
+_WT = {"on": None, "stream": None}
+_WT_MAIN = _os.environ.get("FF_WT_STREAM", "side") == "main"  # refresh on the compute stream instead
+_WT_BLOCKS = int(_os.environ.get("FF_WT_BLOCKS", "32"))  # side-stream refresh: workgroups per launch
+
+
+def wt_copy_enabled() -> bool:
+    if _WT["on"] is None:
+        _WT["on"] = _os.environ.get("FF_WT_COPY", "1") != "0"
+    return _WT["on"]
+
+
+def weight_t(store: dict, w: torch.Tensor):
+    """Refresh store's transposed copy of w [out, in] -> (wt [in, out], ready event or None), or
+    None when w does not qualify (not a contiguous device bf16 matrix with dims % 8 == 0)."""
+    if not (wt_copy_enabled() and native(w) and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0):
+        return None
+    buf = store.get("wt_buf")
+    if buf is None or buf.shape != (w.shape[1], w.shape[0]) or buf.device != w.device:
+        buf = store["wt_buf"] = torch.empty(w.shape[1], w.shape[0], device=w.device, dtype=w.dtype)
+    X = ext()
+    if torch.cuda.is_current_stream_capturing() or _WT_MAIN:
+        X.transpose2d(w, buf)  # on the compute stream (inside a captured step the graph orders it)
+        return buf, None
+    cur = torch.cuda.current_stream(w.device)
+    st = _WT["stream"]
+    if st is None or st.device != w.device:
+        st = _WT["stream"] = torch.cuda.Stream(device=w.device)
+    fork = store.get("wt_fork")
+    if fork is None:
+        fork = store["wt_fork"] = torch.cuda.Event()
+        store["wt_ready"] = torch.cuda.Event()
+    fork.record(cur)  # behind everything queued so far, incl. the last backward's read of buf
+    with torch.cuda.stream(st):
+        st.wait_event(fork)
+        X.transpose2d(w, buf, _WT_BLOCKS)
+        store["wt_ready"].record(st)
+    return buf, store["wt_ready"]
+
+
+def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None, on_dx=None,
+               wt=None):
     """Backward of linear_fwd. dw/db are fp32 gradient accumulators (+= ; dw_beta=0 overwrites dw
     when the executor knows this op is the weight's only user). dx_out: an existing input gradient
     [M, K] to accumulate into (dgrad GEMM with beta = 1, no separate add). dact = (z, act, db) of
     the Linear that produced x: the returned dx is then already that producer's pre-activation
     gradient (and its bias gradient is summed), see gemm_dact. on_dx(dx) is called between the
-    dgrad and the wgrad GEMM (the executor starts dx's collective there). Returns dx (or None)."""
+    dgrad and the wgrad GEMM (the executor starts dx's collective there). wt: weight_t()'s
+    (W^T, ready event) for a TN dgrad. Returns dx (or None)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     if act != ACT_NONE:
@@ -690,19 +741,25 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
     if dact is not None:
         assert need_dx and dx_out is None
         dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
-        gemm_dact(dz, w, dx, dact[0], dact[2], M, K, N, True, False, N, K, K, dact[1])
+        if wt is not None and wt[0].shape == (K, N) and dy2d.dtype == torch.bfloat16:
+            if wt[1] is not None:
+                torch.cuda.current_stream(dy2d.device).wait_event(wt[1])
+            gemm_dact(dz, wt[0], dx, dact[0], dact[2], M, K, N, True, True, N, N, K, dact[1])
+        else:
+            gemm_dact(dz, w, dx, dact[0], dact[2], M, K, N, True, False, N, K, K, dact[1])
         need_dx = False
         if on_dx is not None:
             on_dx(dx)
     if native(dy2d) and dy2d.dtype in (torch.bfloat16, torch.float32) and w.dtype == dy2d.dtype \
             and x2d.dtype == dy2d.dtype:
         if need_dx:
-            if dx_out is not None:
-                dx = dx_out
-                gemm(dz, w, dx, M, K, N, True, False, N, K, K, beta=1.0)
+            dx = dx_out if dx_out is not None else torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
+            if wt is not None and wt[0].shape == (K, N) and dy2d.dtype == torch.bfloat16:
+                if wt[1] is not None:
+                    torch.cuda.current_stream(dy2d.device).wait_event(wt[1])
+                gemm(dz, wt[0], dx, M, K, N, True, True, N, N, K, beta=1.0 if dx_out is not None else 0.0)
             else:
-                dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
-                gemm(dz, w, dx, M, K, N, True, False, N, K, K)
+                gemm(dz, w, dx, M, K, N, True, False, N, K, K, beta=1.0 if dx_out is not None else 0.0)
             if on_dx is not None:
                 on_dx(dx)
         if dw is not None:

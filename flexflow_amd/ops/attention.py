@@ -132,6 +132,8 @@ class MultiHeadAttention(OpImpl):
             qv, kv, vv = qkv.view(-1), qkv.view(-1)[Hl * kd:], qkv.view(-1)[2 * Hl * kd:]
             qs = ks = vs = st
             s.update(x2=x2, wqkv=wq, qkv=qkv)
+            if ctx.training and ctx.extra.get("need_dx0", True):  # TN dgrad (kernels.weight_t)
+                s["wqkv_t"] = K.weight_t(ctx.extra.setdefault("wt_store_qkv", {}), wq)
         else:
             outs = []
             for name, t, d in (("q", q_in, kd), ("k", k_in, kd), ("v", v_in, vd)):
@@ -179,6 +181,8 @@ class MultiHeadAttention(OpImpl):
             o.copy_(_attn_ref(q4, k4, v4, scale, causal).permute(0, 2, 1, 3))
         o2 = o.view(B * Sq, Hl * vd)
         wo = W["o_weight"].reshape(E, Hl * vd)
+        if ctx.training:
+            s["wo_t"] = K.weight_t(ctx.extra.setdefault("wt_store_o", {}), wo)
         y, _ = K.linear_fwd(o2, wo, bo, K.ACT_NONE, False)
         if ctx.training:
             s.update(o=o, wo=wo, has_bo=bo is not None, shape=(B, Sq, Sk, Hl, kd, vd, E), fused=fused,
@@ -203,7 +207,7 @@ class MultiHeadAttention(OpImpl):
         dbo = gw("o_bias") if (s["has_bo"] and not ctx.extra.get("bias_grad_fused")) else None
         wb = 0.0 if ctx.extra.get("wgrad_overwrite") else 1.0
         do2 = K.linear_bwd(dy2, o2, s["wo"], None, K.ACT_NONE,
-                           dwo.view(E, Hl * vd) if dwo is not None else None, dbo, dw_beta=wb)
+                           dwo.view(E, Hl * vd) if dwo is not None else None, dbo, dw_beta=wb, wt=s.get("wo_t"))
         do = do2.view(B, Sq, Hl, vd)
         scale, causal = s["scale"], s["causal"]
         qs, ks, vs, os_ = s["qs"], s["ks"], s["vs"], s["os"]
@@ -259,7 +263,7 @@ class MultiHeadAttention(OpImpl):
             dx2 = K.linear_bwd(dqkv, s["x2"], s["wqkv"], None, K.ACT_NONE,
                                dw.view(3 * Hl * kd, -1) if dw is not None else None,
                                db.view(-1) if db is not None else None, dw_beta=wb,
-                               dx_out=acc.view(B * Sq, -1) if acc is not None else None)
+                               dx_out=acc.view(B * Sq, -1) if acc is not None else None, wt=s.get("wqkv_t"))
             dx = acc if acc is not None else dx2.view(B, Sq, -1)
             ctx.saved.clear()
             return [dx, None, None]  # all three inputs are the same tensor: gradient once

@@ -82,8 +82,14 @@ class Linear(OpImpl):
         # backward pass moves the same bytes either way (its act' VALU hides under HBM time).
         sg = bool(ctx.training and ctx.extra.get("dact_fused") and self.act != K.ACT_NONE
                   and os.environ.get("FF_DACT_STORE_GRAD", "0") == "1")
+        wt = None
+        if ctx.training and ctx.extra.get("need_dx0", True):
+            # the dgrad GEMM reads W^T K-contiguous (kernels.weight_t: refreshed on a side stream
+            # beside this forward GEMM)
+            wt = K.weight_t(ctx.extra.setdefault("wt_store", {}), w)
         y, z = K.linear_fwd(x2, w, b, self.act, save_z=ctx.training, store_grad=sg)
         if ctx.training:
+            ctx.saved["wt"] = wt
             ctx.saved["x"] = x2
             ctx.saved["z"] = z
             ctx.saved["z_is_grad"] = sg
@@ -124,7 +130,8 @@ class Linear(OpImpl):
                 ready(0, acc if acc is not None else d.reshape(out_shape))
         dx = K.linear_bwd(dy2, x2, w, z, act, dw, db, need_dx=ctx.extra.get("need_dx0", True),
                           dw_beta=0.0 if ctx.extra.get("wgrad_overwrite") else 1.0,
-                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None, dact=dact, on_dx=on_dx)
+                          dx_out=acc.view(-1, x2.shape[1]) if acc is not None else None, dact=dact, on_dx=on_dx,
+                          wt=ctx.saved.get("wt"))
         ctx.saved.clear()
         if dx is None:
             return [None]

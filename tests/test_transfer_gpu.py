@@ -246,3 +246,42 @@ def test_concat_rows_kernel_matches_torch_cat(dtype, case):
     odd = [torch.randn(3, 5, device=DEV).to(dtype), torch.randn(3, 7, device=DEV).to(dtype)]
     r = _concat_rows(odd, 1)
     assert r is None or torch.equal(r, torch.cat(odd, 1))
+
+
+@pytest.mark.parametrize("rows,cols", [(8, 8), (64, 64), (1024, 4096), (3072, 1024), (200, 136), (30528, 1024)])
+def test_transpose2d_matches_torch(rows, cols):
+    """transpose16 (the Linear layers' W^T copy) against torch's .t(), bitwise; edge tiles included."""
+    from flexflow_amd import kernels as Kn
+    w = torch.randn(rows, cols, device=DEV).bfloat16()
+    out = torch.full((cols, rows), float("nan"), device=DEV, dtype=torch.bfloat16)
+    Kn.ext().transpose2d(w, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, w.t().contiguous())
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_linear_bwd_transposed_weight_matches_nn(accumulate):
+    """The TN dgrad through weight_t's W^T copy (side stream + event) against the NN dgrad and an fp32
+    torch reference."""
+    from flexflow_amd import kernels as Kn
+    torch.manual_seed(0)
+    M, N, K = 512, 384, 256  # tokens, out, in
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 16).bfloat16()
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    store = {}
+    wt = Kn.weight_t(store, w)
+    assert wt is not None and wt[0].shape == (K, N)
+    base = torch.randn(M, K, device=DEV).bfloat16() if accumulate else None
+    outs = []
+    for use_wt in (False, True):
+        dx_out = base.clone() if accumulate else None
+        dw = torch.zeros(N, K, device=DEV)
+        dx = Kn.linear_bwd(dy, x, w, None, Kn.ACT_NONE, dw, None, dx_out=dx_out, wt=wt if use_wt else None)
+        outs.append((dx.float(), dw))
+    torch.cuda.synchronize()
+    ref = dy.float() @ w.float() + (base.float() if accumulate else 0)
+    for dx, dw in outs:
+        assert torch.allclose(dx, ref, atol=3e-2, rtol=2e-2), (dx - ref).abs().max()
+        assert torch.allclose(dw, dy.float().t() @ x.float(), atol=5e-2, rtol=1e-2)
+    assert torch.allclose(outs[0][0], outs[1][0], atol=3e-2, rtol=2e-2)
