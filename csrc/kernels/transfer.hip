@@ -172,9 +172,8 @@ void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, 
 // 16-B loads along source rows, 16-B stores along destination rows; the LDS row pitch of 72
 // elements (144 B) keeps every 16-B chunk aligned and spreads the column reads over the banks.
 // Grid: one workgroup per tile, or (max_blocks > 0) at most max_blocks workgroups striding over the
-// tiles — a refresh on a side stream then holds only that many CU slots beside the compute stream's
-// GEMMs (a full grid of 1024 workgroups per weight slowed the concurrent forward GEMMs by more than
-// the transposes cost on the compute stream).
+// tiles. (Refreshing on a side stream beside the forward GEMMs was measured slower than on the
+// compute stream, with the full grid and with a 16-workgroup cap: kernels/__init__.py weight_t.)
 __global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ src,
                                                           uint16_t* __restrict__ dst, int rows, int cols) {
   constexpr int P = 72;

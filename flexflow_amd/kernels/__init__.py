@@ -672,17 +672,19 @@ def linear_fwd(x2d, w, bias, act, save_z, store_grad=False):
 
 
 # Transposed weight copies (FF_WT_COPY, default on). The input-gradient GEMM dx = dy . W reads the
-# [out, in] weight N-contiguous ("NN"); on MI355X that form is 14-25 % slower than the K-contiguous
-# "TN" GEMM of the same M / N / K for BERT-Large's dgrad shapes, in the library (shipped TunableOp
-# table: nn_1024_16384_4096 0.0967 ms vs tn_1024_16384_4096 0.0726) and in our ping-pong kernel
-# (its MN-contiguous B path reads LDS through ds_read_b64_tr_b16). So every training forward of a
-# Linear whose input gradient is needed refreshes a persistent W^T [in, out] (transpose16 kernel,
-# ~4 B moved per weight element) on a side stream forked from the compute stream — it overlaps
-# the forward's GEMMs — and the backward waits for it before its dgrad. Refreshing every forward
-# keeps the copy exact whichever path wrote the weights (optimizer, all-gather, set_weights).
-_WT = {"on": None, "stream": None}
-_WT_MAIN = _os.environ.get("FF_WT_STREAM", "side") == "main"  # refresh on the compute stream instead
-_WT_BLOCKS = int(_os.environ.get("FF_WT_BLOCKS", "32"))  # side-stream refresh: workgroups per launch
+# [out, in] weight N-contiguous ("NN"); on MI355X that form is 11-16 % slower than the K-contiguous
+# "TN" GEMM of the same M / N / K for BERT-Large's dgrad shapes (in-step tuner timings, library:
+# 16384 x 1024 x 4096 0.1045 -> 0.0914 ms, x 3072 0.0801 -> 0.0716, vocabulary 0.726 -> 0.608;
+# profiles/dgrad_layout_r6.txt). So every training forward of a Linear / attention projection
+# whose input gradient is needed refreshes a persistent W^T [in, out] (transpose16 kernel, ~4 B
+# moved per weight element, 0.3 ms per BERT-Large step) on the compute stream, and the backward's
+# dgrad reads it. Refreshing every forward keeps the copy exact whichever path wrote the weights
+# (optimizer, all-gather, set_weights). Measured alternatives (profiles/wt_copy_ab_r6.txt): the
+# refresh on a side stream beside the forward GEMMs (+0.4 ms/step: the transposes' workgroups slowed
+# the concurrent GEMMs more than they cost serially), the same with the grid capped at 16
+# workgroups (+2.5 ms), and weight gradients on a side stream beside the rest of the backward
+# (+0.5 ms once its buffer hazards were joined).
+_WT = {"on": None}
 
 
 def wt_copy_enabled() -> bool:
@@ -692,32 +694,16 @@ def wt_copy_enabled() -> bool:
 
 
 def weight_t(store: dict, w: torch.Tensor):
-    """Refresh store's transposed copy of w [out, in] -> (wt [in, out], ready event or None), or
-    None when w does not qualify (not a contiguous device bf16 matrix with dims % 8 == 0)."""
+    """Refresh store's transposed copy of w [out, in] -> wt [in, out], or None when w does not
+    qualify (not a contiguous device bf16 matrix with dims % 8 == 0)."""
     if not (wt_copy_enabled() and native(w) and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
             and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0):
         return None
     buf = store.get("wt_buf")
     if buf is None or buf.shape != (w.shape[1], w.shape[0]) or buf.device != w.device:
         buf = store["wt_buf"] = torch.empty(w.shape[1], w.shape[0], device=w.device, dtype=w.dtype)
-    X = ext()
-    if torch.cuda.is_current_stream_capturing() or _WT_MAIN:
-        X.transpose2d(w, buf)  # on the compute stream (inside a captured step the graph orders it)
-        return buf, None
-    cur = torch.cuda.current_stream(w.device)
-    st = _WT["stream"]
-    if st is None or st.device != w.device:
-        st = _WT["stream"] = torch.cuda.Stream(device=w.device)
-    fork = store.get("wt_fork")
-    if fork is None:
-        fork = store["wt_fork"] = torch.cuda.Event()
-        store["wt_ready"] = torch.cuda.Event()
-    fork.record(cur)  # behind everything queued so far, incl. the last backward's read of buf
-    with torch.cuda.stream(st):
-        st.wait_event(fork)
-        X.transpose2d(w, buf, _WT_BLOCKS)
-        store["wt_ready"].record(st)
-    return buf, store["wt_ready"]
+    ext().transpose2d(w, buf)
+    return buf
 
 
 def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None, on_dx=None,
@@ -727,8 +713,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
     [M, K] to accumulate into (dgrad GEMM with beta = 1, no separate add). dact = (z, act, db) of
     the Linear that produced x: the returned dx is then already that producer's pre-activation
     gradient (and its bias gradient is summed), see gemm_dact. on_dx(dx) is called between the
-    dgrad and the wgrad GEMM (the executor starts dx's collective there). wt: weight_t()'s
-    (W^T, ready event) for a TN dgrad. Returns dx (or None)."""
+    dgrad and the wgrad GEMM (the executor starts dx's collective there). wt: weight_t()'s W^T for
+    a TN dgrad. Returns dx (or None)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     if act != ACT_NONE:
@@ -741,10 +727,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
     if dact is not None:
         assert need_dx and dx_out is None
         dx = torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
-        if wt is not None and wt[0].shape == (K, N) and dy2d.dtype == torch.bfloat16:
-            if wt[1] is not None:
-                torch.cuda.current_stream(dy2d.device).wait_event(wt[1])
-            gemm_dact(dz, wt[0], dx, dact[0], dact[2], M, K, N, True, True, N, N, K, dact[1])
+        if wt is not None and wt.shape == (K, N) and dy2d.dtype == torch.bfloat16:
+            gemm_dact(dz, wt, dx, dact[0], dact[2], M, K, N, True, True, N, N, K, dact[1])
         else:
             gemm_dact(dz, w, dx, dact[0], dact[2], M, K, N, True, False, N, K, K, dact[1])
         need_dx = False
@@ -754,10 +738,8 @@ def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=N
             and x2d.dtype == dy2d.dtype:
         if need_dx:
             dx = dx_out if dx_out is not None else torch.empty(M, K, device=dy2d.device, dtype=dy2d.dtype)
-            if wt is not None and wt[0].shape == (K, N) and dy2d.dtype == torch.bfloat16:
-                if wt[1] is not None:
-                    torch.cuda.current_stream(dy2d.device).wait_event(wt[1])
-                gemm(dz, wt[0], dx, M, K, N, True, True, N, N, K, beta=1.0 if dx_out is not None else 0.0)
+            if wt is not None and wt.shape == (K, N) and dy2d.dtype == torch.bfloat16:
+                gemm(dz, wt, dx, M, K, N, True, True, N, N, K, beta=1.0 if dx_out is not None else 0.0)
             else:
                 gemm(dz, w, dx, M, K, N, True, False, N, K, K, beta=1.0 if dx_out is not None else 0.0)
             if on_dx is not None:

@@ -84,8 +84,7 @@ class Linear(OpImpl):
                   and os.environ.get("FF_DACT_STORE_GRAD", "0") == "1")
         wt = None
         if ctx.training and ctx.extra.get("need_dx0", True):
-            # the dgrad GEMM reads W^T K-contiguous (kernels.weight_t: refreshed on a side stream
-            # beside this forward GEMM)
+            # the dgrad GEMM reads W^T K-contiguous (kernels.weight_t)
             wt = K.weight_t(ctx.extra.setdefault("wt_store", {}), w)
         y, z = K.linear_fwd(x2, w, b, self.act, save_z=ctx.training, store_grad=sg)
         if ctx.training:
