@@ -189,7 +189,8 @@ _ADDMM_F32_OUT = [True]  # torch.addmm(out_dtype=fp32, out=C) usable in place
 # a mismatching table is ignored). FF_TUNABLEOP=use (default) reads the table with tuning off
 # (unlisted shapes keep the library default), =tune tunes every shape met and writes the table
 # to FF_TUNABLEOP_FILE at exit, =off leaves TunableOp alone.
-TUNABLE_CSV = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..", "tuning", "tunableop_gfx950.csv")
+TUNABLE_CSV = _os.environ.get("FF_TUNABLEOP_TABLE") or _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "..",
+                                                                     "tuning", "tunableop_gfx950.csv")
 _tunable_state = [None]
 
 
