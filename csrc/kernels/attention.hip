@@ -954,7 +954,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd1b_kernel(AttnArgs a, int nkb,
   char* k_l = smem + 2 * TILE;
   char* ds0 = k_l + KB * D * 2;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const bool late = a.stagger && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
   const int groups = CHAIN ? 1 : nkb;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);

@@ -102,22 +102,25 @@ __device__ __forceinline__ int opaque_lane() {
 // plus the per-128-row fp32 column sums of that product for the producer's bias gradient (2 more
 // stores). (Round 5's first attempt loaded every zin row up front and summed columns per element
 // pass: ~150 VGPRs spilled; here the sums are 8 registers folded across lanes once per tile.)
-template <bool F32OUT, bool ACT = false, bool DACT = false>
-constexpr int epi_ops() { return DACT ? 16 + 14 + 2 : (F32OUT ? 32 : 16) + 2 + (ACT ? 16 : 0); }
+// HB = false (no bias): no bias loads, and no 8 bias registers live across the 8 row passes — with
+// them the bf16-output epilogue spilled ~12 VGPRs to scratch inside the main loop, and each reload's
+// s_waitcnt vmcnt(0) also waited for the LDS-DMA pieces in flight (round 6).
+template <bool F32OUT, bool ACT = false, bool DACT = false, bool HB = true>
+constexpr int epi_ops() { return DACT ? 16 + 14 + 2 : (F32OUT ? 32 : 16) + (HB ? 2 : 0) + (ACT ? 16 : 0); }
 
 // ACTK: 0, or the activation (ACT_RELU / ACT_GELU) as a compile-time constant: one code path per
 // instantiation (a run-time switch over every activation cost ~10 more VGPR spills). DK: 0, or
 // ACT_GRADMUL for the DACT epilogue (zin already holds act'(z), stored by the producer's forward).
 // (Evaluating GELU' from z here was tried: ~14 VALU per element in the memory phase, 96 B/lane of
 // spills, and wrong results on 1/3 of the elements on gfx950 — not built.)
-template <bool A_K, bool B_K, bool F32OUT, bool SPLIT, int ACTK = 0, int DK = 0>
+template <bool A_K, bool B_K, bool F32OUT, bool SPLIT, int ACTK = 0, int DK = 0, bool HB = true>
 __global__ void __attribute__((amdgpu_flat_work_group_size(NTHR, NTHR), amdgpu_waves_per_eu(2, 2)))
 gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   constexpr bool DACT = DK != 0;
   // DACT: + 32 B per lane of running column sums (8 waves x 2 KiB, 160 KiB in all)
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 4 * 4096 + (DACT ? 8 * 2048 : 0)];
   constexpr bool ACT = ACTK != 0;
-  constexpr int EPI = epi_ops<F32OUT, ACT, DACT>();
+  constexpr int EPI = epi_ops<F32OUT, ACT, DACT, HB>();
   static_assert(!ACT || (!F32OUT && !SPLIT), "activation epilogue: bf16 output, no split-K");
   static_assert(!DACT || (!F32OUT && !SPLIT && !ACT), "dgrad-activation epilogue: bf16 output, no split-K");
 
@@ -364,7 +367,7 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
     const int n = tni * BN + wj * 64 + 8 * cc;  // this lane's 8 read-back columns
     const bool nin = n < p.N;
     float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (DACT) {
+    if constexpr (DACT || !HB) {
       // no bias (dgrad): no bias registers live across the passes
     } else if (p.bias_bf16) {
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rbias, nin ? n * 2 : -16, 0, 0);
@@ -597,12 +600,17 @@ gemm_pp_kernel(GemmArgs p, int64_t a_bytes, int64_t b_bytes) {
   }
 }
 
+template <bool F32OUT, bool SPLIT, int ACTK, bool HB>
+static void launch_hb(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
+  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, SPLIT, ACTK, 0, HB>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, SPLIT, ACTK, 0, HB>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, SPLIT, ACTK, 0, HB>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT, ACTK, 0, HB>), grid, dim3(NTHR), 0, s, p, ab, bb);
+}
 template <bool F32OUT, bool SPLIT, int ACTK = 0>
 static void launch(const GemmArgs& p, dim3 grid, hipStream_t s, int64_t ab, int64_t bb) {
-  if (p.a_kcontig && p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, true, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.a_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<true, false, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else if (p.b_kcontig) hipLaunchKernelGGL((gemm_pp_kernel<false, true, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
-  else hipLaunchKernelGGL((gemm_pp_kernel<false, false, F32OUT, SPLIT, ACTK>), grid, dim3(NTHR), 0, s, p, ab, bb);
+  if (SPLIT || !p.bias) launch_hb<F32OUT, SPLIT, ACTK, false>(p, grid, s, ab, bb);  // split-K never has a bias
+  else launch_hb<F32OUT, SPLIT, ACTK, true>(p, grid, s, ab, bb);
 }
 
 // the DACT epilogue is built for the dgrad layout only: A = dY [M][K] K-contiguous, B = W [K][N]
