@@ -433,6 +433,8 @@ def _time(fn, reps=8):
 
 
 _TUNE_ROUNDS = int(_os.environ.get("FF_TUNE_ROUNDS", "3"))
+_GEMM_TRACE = _os.environ.get("FF_GEMM_TRACE", "0") == "1"  # print each call site's choice once
+_traced = set()
 _TUNE_LIB_MARGIN = float(_os.environ.get("FF_TUNE_LIB_MARGIN", "0.03"))
 
 
@@ -537,6 +539,10 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                                  "times_ms": {str(k): round(v, 4) for k, v in times.items()}, "choice": str(choice)})
                 _timed.add(key)
             _tuned[key] = choice
+        if _GEMM_TRACE and key not in _traced:
+            _traced.add(key)
+            print(f"[gemm] M={M} N={N} K={K} a_k={a_k} b_k={b_k} bias={bias is not None} Z={Z is not None} "
+                  f"act={act} beta={beta} -> {choice}", flush=True)
         if isinstance(choice, tuple):
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
         elif isinstance(choice, str) and choice.startswith("pp_sk"):
