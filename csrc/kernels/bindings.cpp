@@ -164,7 +164,7 @@ void concat_rows(std::vector<Tensor> srcs, std::vector<int64_t> lens, Tensor out
 }
 
 // dst [cols][rows] = src [rows][cols]^T (2-byte elements, both contiguous, dims multiples of 8)
-void transpose2d(Tensor src, Tensor dst, int64_t max_blocks) {
+void transpose2d(Tensor src, Tensor dst) {
   check_dev(src, "src"); check_dev(dst, "dst");
   TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.is_contiguous() && dst.is_contiguous() &&
               src.element_size() == 2 && dst.scalar_type() == src.scalar_type(), "transpose2d: contiguous 2-D 16-bit");
@@ -173,7 +173,15 @@ void transpose2d(Tensor src, Tensor dst, int64_t max_blocks) {
   TORCH_CHECK(r % 8 == 0 && c % 8 == 0 && r * c < (1LL << 31), "transpose2d: dims multiples of 8, < 2^31 elements");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16) == 0,
               "transpose2d: 16-B aligned");
-  ffk::transpose16(src.data_ptr(), dst.data_ptr(), (int)r, (int)c, (int)max_blocks, cur_stream());
+  ffk::transpose16(src.data_ptr(), dst.data_ptr(), (int)r, (int)c, cur_stream());
+}
+// desc: int64 device tensor [n][5] = {src, dst, rows, cols, first tile}, built by the caller from
+// tensors it validated with transpose2d's rules (kernels.wt_refresh_all)
+void transpose2d_batch(Tensor desc, int64_t n, int64_t tiles) {
+  check_dev(desc, "desc");
+  TORCH_CHECK(desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.numel() >= n * 5 && n > 0 &&
+              tiles > 0 && tiles < (1LL << 31), "transpose2d_batch: descriptors");
+  ffk::transpose16_batch(desc.data_ptr<int64_t>(), (int)n, tiles, cur_stream());
 }
 
 // x [.., xd, inner] and idx / out [.., dsz, inner], contiguous, other dims equal (checked by caller)
@@ -885,7 +893,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill", &fill);
   m.def("slab_sum", &slab_sum);
   m.def("concat_rows", &concat_rows);
-  m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("dst"), py::arg("max_blocks") = 0);
+  m.def("transpose2d", &transpose2d);
+  m.def("transpose2d_batch", &transpose2d_batch);
   m.def("gemm_f32", &gemm_f32);
   m.def("causal_mask_f32", &causal_mask_f32);
   m.def("topk_fwd", &topk_fwd);

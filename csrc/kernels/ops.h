@@ -61,7 +61,9 @@ void box_copy(const void* const* srcs, int nsrc, void* dst, const int64_t* desc,
 void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, int outer, int vec_bytes,
                  hipStream_t st);
 // dst [cols][rows] = src [rows][cols]^T, 2-byte elements, rows % 8 == cols % 8 == 0 (transfer.hip)
-void transpose16(const void* src, void* dst, int rows, int cols, int max_blocks, hipStream_t st);
+void transpose16(const void* src, void* dst, int rows, int cols, hipStream_t st);
+// desc[i] = {src, dst, rows, cols, first tile} (int64, device), tiles = 64 x 64 tiles in all
+void transpose16_batch(const int64_t* desc, int n, int64_t tiles, hipStream_t st);
 
 // moe.hip: TopK and the mixture-of-experts routing (GroupBy / Aggregate / AggregateSpec), fully
 // on the device. Expert tensors are passed as arrays of up to kMoeMaxExperts device pointers.

@@ -174,42 +174,68 @@ void concat_rows(const void* const* srcs, const int* lens, int nsrc, void* out, 
 // Grid: one workgroup per tile, or (max_blocks > 0) at most max_blocks workgroups striding over the
 // tiles. (Refreshing on a side stream beside the forward GEMMs was measured slower than on the
 // compute stream, with the full grid and with a 16-workgroup cap: kernels/__init__.py weight_t.)
-__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ src,
-                                                          uint16_t* __restrict__ dst, int rows, int cols) {
+// one 64 x 64 tile (r0, c0) of dst = src^T through the LDS image t (72-element row pitch)
+__device__ __forceinline__ void transpose16_tile(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                 int rows, int cols, int r0, int c0, uint16_t* t) {
   constexpr int P = 72;
-  __shared__ __attribute__((aligned(16))) uint16_t t[64 * P];
-  const int tc = (cols + 63) / 64, ntiles = tc * ((rows + 63) / 64);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int c0 = (tile % tc) * 64, r0 = (tile / tc) * 64;
-    if (tile != (int)blockIdx.x) __syncthreads();  // the previous tile's reads of t are done
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int id = threadIdx.x + 256 * j, r = id >> 3, ch = id & 7;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (r0 + r < rows && c0 + 8 * ch < cols)
-        v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + r) * cols + c0 + 8 * ch);
-      *reinterpret_cast<uint4*>(t + r * P + 8 * ch) = v;
-    }
-    __syncthreads();
+  for (int j = 0; j < 2; ++j) {
+    const int id = threadIdx.x + 256 * j, r = id >> 3, ch = id & 7;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (r0 + r < rows && c0 + 8 * ch < cols)
+      v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + r) * cols + c0 + 8 * ch);
+    *reinterpret_cast<uint4*>(t + r * P + 8 * ch) = v;
+  }
+  __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int id = threadIdx.x + 256 * j, oc = id >> 3, ch = id & 7;
-      if (c0 + oc >= cols || r0 + 8 * ch >= rows) continue;
-      uint32_t w[4];
+  for (int j = 0; j < 2; ++j) {
+    const int id = threadIdx.x + 256 * j, oc = id >> 3, ch = id & 7;
+    if (c0 + oc >= cols || r0 + 8 * ch >= rows) continue;
+    uint32_t w[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        w[e] = (uint32_t)t[(8 * ch + 2 * e) * P + oc] | ((uint32_t)t[(8 * ch + 2 * e + 1) * P + oc] << 16);
-      *reinterpret_cast<uint4*>(dst + (int64_t)(c0 + oc) * rows + r0 + 8 * ch) = uint4{w[0], w[1], w[2], w[3]};
-    }
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)t[(8 * ch + 2 * e) * P + oc] | ((uint32_t)t[(8 * ch + 2 * e + 1) * P + oc] << 16);
+    *reinterpret_cast<uint4*>(dst + (int64_t)(c0 + oc) * rows + r0 + 8 * ch) = uint4{w[0], w[1], w[2], w[3]};
   }
 }
 
-void transpose16(const void* src, void* dst, int rows, int cols, int max_blocks, hipStream_t st) {
+__global__ void __launch_bounds__(256) transpose16_kernel(const uint16_t* __restrict__ src,
+                                                          uint16_t* __restrict__ dst, int rows, int cols) {
+  __shared__ __attribute__((aligned(16))) uint16_t t[64 * 72];
+  const int tc = (cols + 63) / 64;
+  transpose16_tile(src, dst, rows, cols, (blockIdx.x / tc) * 64, (blockIdx.x % tc) * 64, t);
+}
+
+void transpose16(const void* src, void* dst, int rows, int cols, hipStream_t st) {
   if (rows <= 0 || cols <= 0) return;
-  int tiles = ((cols + 63) / 64) * ((rows + 63) / 64);
-  if (max_blocks > 0) tiles = std::min(tiles, max_blocks);
+  const int tiles = ((cols + 63) / 64) * ((rows + 63) / 64);
   hipLaunchKernelGGL(transpose16_kernel, dim3((unsigned)tiles), dim3(256), 0, st, (const uint16_t*)src, (uint16_t*)dst,
                      rows, cols);
+}
+
+// Every registered W^T of a model in ONE launch (the executor refreshes them at the start of each
+// training forward): desc[i] = {src, dst, rows, cols, first tile}, tiles of matrix i numbered from
+// its first tile; a workgroup finds its matrix by binary search over the n first-tile entries. The
+// per-weight launches cost 5-6 us each at ~3 TB/s on BERT-Large's 4M-element weights (98 per step).
+__global__ void __launch_bounds__(256) transpose16_batch_kernel(const int64_t* __restrict__ desc, int n) {
+  __shared__ __attribute__((aligned(16))) uint16_t t[64 * 72];
+  const int64_t tile = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last matrix whose first tile <= tile
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid * 5 + 4] <= tile) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* d = desc + lo * 5;
+  const int rows = (int)d[2], cols = (int)d[3];
+  const int tc = (cols + 63) / 64, k = (int)(tile - d[4]);
+  transpose16_tile(reinterpret_cast<const uint16_t*>(d[0]), reinterpret_cast<uint16_t*>(d[1]), rows, cols,
+                   (k / tc) * 64, (k % tc) * 64, t);
+}
+
+void transpose16_batch(const int64_t* desc, int n, int64_t tiles, hipStream_t st) {
+  if (n <= 0 || tiles <= 0) return;
+  hipLaunchKernelGGL(transpose16_batch_kernel, dim3((unsigned)tiles), dim3(256), 0, st, desc, n);
 }
 
 // ------------------------------------------------------------------------------- gather

@@ -691,7 +691,7 @@ def linear_fwd(x2d, w, bias, act, save_z, store_grad=False):
 # the concurrent GEMMs more than they cost serially), the same with the grid capped at 16
 # workgroups (+2.5 ms), and weight gradients on a side stream beside the rest of the backward
 # (+0.5 ms once its buffer hazards were joined).
-_WT = {"on": None}
+_WT = {"on": None, "step": 0, "in_fwd": False}
 
 
 def wt_copy_enabled() -> bool:
@@ -701,16 +701,57 @@ def wt_copy_enabled() -> bool:
 
 
 def weight_t(store: dict, w: torch.Tensor):
-    """Refresh store's transposed copy of w [out, in] -> wt [in, out], or None when w does not
-    qualify (not a contiguous device bf16 matrix with dims % 8 == 0)."""
+    """store's transposed copy of w [out, in] -> wt [in, out], current for this forward, or None
+    when w does not qualify (not a contiguous device bf16 matrix with dims % 8 == 0). Inside an
+    executor forward that already refreshed every registered copy in one launch (wt_refresh_all) the
+    copy is returned as is; otherwise it is refreshed here and registered for the next batch."""
     if not (wt_copy_enabled() and native(w) and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
-            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0):
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.data_ptr() % 16 == 0
+            and w.numel() < (1 << 31)):
         return None
     buf = store.get("wt_buf")
+    src = store.get("wt_src")
+    same = src is not None and src.data_ptr() == w.data_ptr() and src.shape == w.shape
+    if same and buf is not None and _WT["in_fwd"] and store.get("wt_step") == _WT["step"]:
+        return buf
     if buf is None or buf.shape != (w.shape[1], w.shape[0]) or buf.device != w.device:
         buf = store["wt_buf"] = torch.empty(w.shape[1], w.shape[0], device=w.device, dtype=w.dtype)
     ext().transpose2d(w, buf)
+    store["wt_src"] = w
+    store["wt_step"] = _WT["step"]
     return buf
+
+
+def wt_refresh_all(stores, cache: dict):
+    """Refresh the transposed copies of `stores` (the weight_t stores of one executor's ops) in ONE
+    launch (transpose16_batch) — called by the executor at the start of a training forward, once
+    the optimizer's writes of the weights are ordered before it; weight_t() then hands the copies
+    out without a launch per weight (98 launches of 5-6 us each per BERT-Large step). `cache` keeps
+    the device descriptor table between calls. Returns the number of copies refreshed."""
+    _WT["step"] += 1
+    if not wt_copy_enabled():
+        return 0
+    items = [st for st in stores if st.get("wt_src") is not None and st.get("wt_buf") is not None]
+    if not items:
+        return 0
+    key = tuple((st["wt_src"].data_ptr(), st["wt_buf"].data_ptr(), st["wt_src"].shape[0], st["wt_src"].shape[1])
+                for st in items)
+    if cache.get("key") != key:
+        rows, tile = [], 0
+        for sp, dp, r, c in key:
+            rows.append([sp, dp, r, c, tile])
+            tile += ((r + 63) // 64) * ((c + 63) // 64)
+        cache.update(key=key, desc=torch.tensor(rows, dtype=torch.int64).to(items[0]["wt_buf"].device),
+                     n=len(rows), tiles=tile)
+    ext().transpose2d_batch(cache["desc"], cache["n"], cache["tiles"])
+    for st in items:
+        st["wt_step"] = _WT["step"]
+    return cache["n"]
+
+
+def wt_forward(active: bool):
+    """The executor marks its training forward (weight_t may then trust wt_refresh_all's copies)."""
+    _WT["in_fwd"] = bool(active)
 
 
 def linear_bwd(dy2d, x2d, w, z, act, dw, db, need_dx=True, dw_beta=1.0, dx_out=None, dact=None, on_dx=None,

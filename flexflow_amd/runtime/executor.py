@@ -450,6 +450,21 @@ class Executor:
     def forward(self, training: Optional[bool] = None):
         tr = self.training if training is None else training
         self._fwd_training = tr
+        # every registered transposed weight copy (kernels.weight_t) in one launch; a sharded
+        # optimizer's weights still arrive by all-gather during the forward, so those ops refresh
+        # their own copies (weight_t outside a batched forward)
+        batched = bool(tr and self.device.type == "cuda" and not self._ag_pending
+                       and os.environ.get("FF_WT_BATCH", "1") != "0")
+        if batched:
+            stores = [st for c in self.ctx.values() for k, st in c.extra.items() if k.startswith("wt_store")]
+            K.wt_refresh_all(stores, self.__dict__.setdefault("_wt_batch", {}))
+        K.wt_forward(batched)
+        try:
+            return self._forward(tr)
+        finally:
+            K.wt_forward(False)
+
+    def _forward(self, tr):
         vals = self.values
         inflight = {}
         for L in self.layers:

@@ -284,3 +284,65 @@ def test_linear_bwd_transposed_weight_matches_nn(accumulate):
         assert torch.allclose(dx, ref, atol=3e-2, rtol=2e-2), (dx - ref).abs().max()
         assert torch.allclose(dw, dy.float().t() @ x.float(), atol=5e-2, rtol=1e-2)
     assert torch.allclose(outs[0][0], outs[1][0], atol=3e-2, rtol=2e-2)
+
+
+def test_transpose2d_batch_matches_torch():
+    """One transpose16_batch launch over matrices of different shapes (the executor's per-forward
+    W^T refresh) against torch's .t()."""
+    from flexflow_amd import kernels as Kn
+    shapes = [(1024, 3072), (8, 8), (200, 136), (4096, 1024), (64, 4096)]
+    srcs = [torch.randn(r, c, device=DEV).bfloat16() for r, c in shapes]
+    stores = []
+    for w in srcs:
+        st = {}
+        Kn.weight_t(st, w)
+        st["wt_buf"].fill_(float("nan"))  # the batch must rewrite every element
+        stores.append(st)
+    cache = {}
+    assert Kn.wt_refresh_all(stores, cache) == len(shapes)
+    for w in srcs:  # new weight values, same tensors: the cached descriptor table is reused
+        w.mul_(-2)
+    assert Kn.wt_refresh_all(stores, cache) == len(shapes)
+    torch.cuda.synchronize()
+    for w, st in zip(srcs, stores):
+        assert torch.equal(st["wt_buf"], w.t().contiguous())
+
+
+def test_bert_losses_with_batched_transposed_weights():
+    """A small BERT trained 3 Adam steps with the W^T copies (batched refresh each forward, TN
+    dgrads) against the same run with NN dgrads: the losses agree to bf16 summation-order noise."""
+    import numpy as np
+    from flexflow_amd import kernels as Kn
+    from flexflow_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_amd.models.bert import BertConfig, build_bert
+
+    def run(wt_on):
+        Kn._WT["on"] = wt_on
+        torch.manual_seed(0)
+        cfg = FFConfig(["--dtype", "bf16", "--no-hip-graphs"])
+        bc = BertConfig(hidden=256, heads=4, layers=2, ffn=1024, vocab=1024, max_pos=128, seq=128)
+        cfg.batch_size = 4
+        ff = FFModel(cfg)
+        ids, pos, _ = build_bert(ff, 4, bc)
+        ff.optimizer = AdamOptimizer(ff, 1e-3)
+        ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        rng = np.random.default_rng(0)
+        ids.set_tensor(ff, rng.integers(0, bc.vocab, (4, bc.seq), dtype=np.int32))
+        pos.set_tensor(ff, np.tile(np.arange(bc.seq, dtype=np.int32), (4, 1)))
+        ff.label_tensor.set_tensor(ff, rng.integers(0, bc.vocab, (4, bc.seq, 1), dtype=np.int32))
+        losses = []
+        for _ in range(3):
+            ff.reset_metrics()
+            ff.forward()
+            ff.zero_gradients()
+            ff.backward()
+            ff.update()
+            losses.append(ff.get_perf_metrics().get_loss())
+        torch.cuda.synchronize()
+        return np.array(losses)
+
+    try:
+        on, off = run(True), run(False)
+    finally:
+        Kn._WT["on"] = None
+    assert np.allclose(on, off, rtol=2e-3), (on, off)
