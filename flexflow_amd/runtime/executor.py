@@ -625,10 +625,20 @@ class Executor:
             self._upd_stream.wait_event(ev)
             if handle is not None:
                 handle.wait()  # the side stream waits for the bucket's all-reduce
-            if self._upd_blocks:
-                self.model.optimizer.step_range(ar, b["lo"], b["hi"], max_blocks=self._upd_blocks)
-            else:  # plain call: user optimizers may implement step_range(arena, lo, hi) only
-                self.model.optimizer.step_range(ar, b["lo"], b["hi"])
+            # the bucket's update as launches of at most FF_UPD_CHUNK elements (default 4 Mi = 16 MB
+            # per fp32 stream, ~23 us): each full-grid sweep holds every wave slot of every CU until
+            # it ends, so a compute-stream kernel queued behind it waited out the whole 64 MiB
+            # bucket (~93 us: col_reduce 5 -> 68 us, the persistent wgrad GEMM 125 -> 200 us);
+            # between shorter launches the backward's kernels get the CUs. Same-box A/B, BERT-Large:
+            # 43.76 -> 43.43 ms (1 Mi: no gain, 8 Mi: -0.1; profiles/update_interference_r6.txt); 0 = whole bucket
+            ch = int(os.environ.get("FF_UPD_CHUNK", "4194304")) // 8 * 8
+            pieces = [(a, min(a + ch, b["hi"])) for a in range(b["lo"], b["hi"], ch)] if ch > 0 else \
+                [(b["lo"], b["hi"])]
+            for lo, hi in pieces:
+                if self._upd_blocks:
+                    self.model.optimizer.step_range(ar, lo, hi, max_blocks=self._upd_blocks)
+                else:  # plain call: user optimizers may implement step_range(arena, lo, hi) only
+                    self.model.optimizer.step_range(ar, lo, hi)
         self._upd_done.add(id(b))
 
     def _make_upd_stream(self):
