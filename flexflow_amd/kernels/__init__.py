@@ -539,10 +539,13 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                                  "times_ms": {str(k): round(v, 4) for k, v in times.items()}, "choice": str(choice)})
                 _timed.add(key)
             _tuned[key] = choice
-        if _GEMM_TRACE and key not in _traced:
-            _traced.add(key)
+        if _GEMM_TRACE and (key, choice) not in _traced:
+            _traced.add((key, choice))
             print(f"[gemm] M={M} N={N} K={K} a_k={a_k} b_k={b_k} bias={bias is not None} Z={Z is not None} "
                   f"act={act} beta={beta} -> {choice}", flush=True)
+            if _os.environ.get("FF_GEMM_TRACE_STACK"):
+                import traceback
+                traceback.print_stack(limit=8)
         if isinstance(choice, tuple):
             _lt_dispatch(choice, A, B, C, Z, M, N, K, a_k, b_k, lda, ldb, alpha, beta, bias, act)
         elif isinstance(choice, str) and choice.startswith("pp_sk"):
