@@ -119,6 +119,12 @@ constexpr int ACT_STORE_GRAD = 0x100;  // bias_act_fwd flag: write act'(z) to zo
 // sequence (div_scale x2, rcp, div_fmas, div_fixup + refinement FMAs), which doubled the VALU cost
 // of the GELU passes.
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// e^x as the bare v_exp_f32 (2^(x log2 e)): __expf lowers to v_exp_f32 wrapped in a range reduction
+// (v_rndne, v_cvt_i32, v_ldexp, three compares / selects: ~9 VALU instead of 2) that the activation
+// functions below do not need — their arguments are <= 0 (GELU's e^(-x^2/2)) or feed a reciprocal
+// that absorbs the overflow (sigmoid); results below 2^-126 flush to zero. Round 6: the GELU' pass
+// of BERT-Large's FFN backward (bias_act_bwd) was VALU-bound on these sequences.
+__device__ __forceinline__ float fast_expe(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float erf_poly_t(float t) {  // A&S 7.1.26 polynomial times t
   float y = __builtin_fmaf(1.061405429f, t, -1.453152027f);
   y = __builtin_fmaf(y, t, 1.421413741f);
@@ -129,14 +135,14 @@ __device__ __forceinline__ float erf_poly_t(float t) {  // A&S 7.1.26 polynomial
 __device__ __forceinline__ float fast_erf(float x) {
   const float ax = fabsf(x);
   const float t = fast_rcp(__builtin_fmaf(0.3275911f, ax, 1.f));
-  const float y = 1.f - erf_poly_t(t) * __expf(-ax * ax);
+  const float y = 1.f - erf_poly_t(t) * fast_expe(-ax * ax);
   return copysignf(y, x);
 }
 
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ACT_RELU: return fmaxf(x, 0.f);
-    case ACT_SIGMOID: return fast_rcp(1.f + __expf(-x));
+    case ACT_SIGMOID: return fast_rcp(1.f + fast_expe(-x));
     case ACT_TANH: return tanhf(x);
     case ACT_GELU: return 0.5f * x * (1.f + fast_erf(x * 0.70710678118654752f));
     default: return x;
@@ -147,14 +153,14 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
-    case ACT_SIGMOID: { float s = fast_rcp(1.f + __expf(-x)); return s * (1.f - s); }
+    case ACT_SIGMOID: { float s = fast_rcp(1.f + fast_expe(-x)); return s * (1.f - s); }
     case ACT_TANH: { float t = tanhf(x); return 1.f - t * t; }
     case ACT_GRADMUL: return x;
     case ACT_GELU: {
       // Phi(x) + x phi(x); erf(x / sqrt 2) and phi share one exp(-x^2 / 2)
       const float au = fabsf(x) * 0.70710678118654752f;
       const float t = fast_rcp(__builtin_fmaf(0.3275911f, au, 1.f));
-      const float e = __expf(-au * au);
+      const float e = fast_expe(-au * au);
       const float erf_abs = 1.f - erf_poly_t(t) * e;
       const float cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
       return __builtin_fmaf(x * 0.3989422804014327f, e, cdf);
@@ -166,7 +172,7 @@ __device__ __forceinline__ void act_fwd_grad(int act, float x, float& y, float& 
   if (act == ACT_GELU) {
     const float au = fabsf(x) * 0.70710678118654752f;
     const float t = fast_rcp(__builtin_fmaf(0.3275911f, au, 1.f));
-    const float e = __expf(-au * au);
+    const float e = fast_expe(-au * au);
     const float erf_abs = 1.f - erf_poly_t(t) * e;
     const float cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
     y = x * cdf;

@@ -250,10 +250,14 @@ __global__ void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 // col_reduce_add with <= 32 adders per address (the full-rate regime of MI355X_MICROARCH
 // 'Global float atomics'; all blocks into one row is 14x slower, hence no direct atomics).
 constexpr int BAB_COLS = 512;
-template <typename T, bool ACT>
+// AK: the activation as a compile-time constant (GELU / ReLU, BERT's and the CNN zoo's), 0: the
+// run-time `act` — a per-element switch over every activation left scalar branches around each
+// element's act' in the loop (round 6: ~400 s_cbranch per 32-element group)
+template <typename T, bool ACT, int AK = 0>
 __global__ void __launch_bounds__(256) bias_act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ z,
                                                            T* __restrict__ dz, float* __restrict__ part, int rows,
-                                                           int cols, int act, int rpb) {
+                                                           int cols, int act_rt, int rpb) {
+  const int act = AK ? AK : act_rt;
   __shared__ float red[4][BAB_COLS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = blockIdx.x * BAB_COLS + lane * 8;
@@ -509,10 +513,11 @@ int bias_act_bwd_chunks(int rows, int cols) {
 // ACT_STORE_GRAD in act, zout receives act'(zb) instead (the consumer's dgrad epilogue then only
 // multiplies by it; zout may alias z). bf16, cols % 8 == 0: one 16-B vector per thread-step. In
 // place (y == z) is allowed.
+template <int AK = 0>  // the activation as a compile-time constant (see bias_act_bwd_kernel), 0: run time
 __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __restrict__ bias, int bias_bf16,
-                                    bf16_t* zout, bf16_t* y, int64_t rows, int cols, int act) {
-  const bool sg = (act & ACT_STORE_GRAD) != 0 && zout != nullptr;
-  act &= 0xff;
+                                    bf16_t* zout, bf16_t* y, int64_t rows, int cols, int act_rt) {
+  const bool sg = (act_rt & ACT_STORE_GRAD) != 0 && zout != nullptr;
+  const int act = AK ? AK : (act_rt & 0xff);
   const int64_t nv = rows * (int64_t)cols / 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -656,8 +661,16 @@ void dropout_bwd(int dt, const void* dy, const uint8_t* mask, void* dx, int64_t 
 void bias_act_fwd(const void* z, const void* bias, int bias_bf16, void* zout, void* y, int64_t rows, int cols,
                   int act, hipStream_t st) {
   if (rows == 0 || cols == 0) return;
-  hipLaunchKernelGGL(bias_act_fwd_kernel, dim3(ew_grid(rows * cols / 8, 256)), dim3(256), 0, st, (const bf16_t*)z,
-                     bias, bias_bf16, (bf16_t*)zout, (bf16_t*)y, rows, cols, act);
+  const dim3 grid(ew_grid(rows * cols / 8, 256));
+  if ((act & 0xff) == ACT_GELU)
+    hipLaunchKernelGGL(bias_act_fwd_kernel<ACT_GELU>, grid, dim3(256), 0, st, (const bf16_t*)z, bias, bias_bf16,
+                       (bf16_t*)zout, (bf16_t*)y, rows, cols, act);
+  else if ((act & 0xff) == ACT_RELU)
+    hipLaunchKernelGGL(bias_act_fwd_kernel<ACT_RELU>, grid, dim3(256), 0, st, (const bf16_t*)z, bias, bias_bf16,
+                       (bf16_t*)zout, (bf16_t*)y, rows, cols, act);
+  else
+    hipLaunchKernelGGL(bias_act_fwd_kernel<>, grid, dim3(256), 0, st, (const bf16_t*)z, bias, bias_bf16,
+                       (bf16_t*)zout, (bf16_t*)y, rows, cols, act);
 }
 
 void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias, float* ws, int rows, int cols,
@@ -677,7 +690,13 @@ void bias_act_bwd(int dt, const void* dy, const void* z, void* dz, float* dbias,
     return;
   }
   FFK_DT_DISPATCH(dt, {
-    if (act != ACT_NONE)
+    if (act == ACT_GELU)
+      hipLaunchKernelGGL((bias_act_bwd_kernel<T, true, ACT_GELU>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy,
+                         (const T*)z, (T*)dz, dbias ? ws : nullptr, rows, cols, act, rpb);
+    else if (act == ACT_RELU)
+      hipLaunchKernelGGL((bias_act_bwd_kernel<T, true, ACT_RELU>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy,
+                         (const T*)z, (T*)dz, dbias ? ws : nullptr, rows, cols, act, rpb);
+    else if (act != ACT_NONE)
       hipLaunchKernelGGL((bias_act_bwd_kernel<T, true>), dim3(gx, gy), dim3(256), 0, st, (const T*)dy, (const T*)z,
                          (T*)dz, dbias ? ws : nullptr, rows, cols, act, rpb);
     else if (dbias)
