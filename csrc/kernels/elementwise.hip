@@ -62,8 +62,11 @@ __device__ __forceinline__ float unary_df(int op, float x, float y, float s) {
   }
 }
 
-template <typename T>
-__global__ void unary_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int op, float s) {
+// OP >= 0: the op as a compile-time constant (ReLU, the CNN zoo's), -1: the run-time `op_rt` (a
+// per-element switch over every op otherwise sits in the loop)
+template <typename T, int OP = -1>
+__global__ void unary_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int op_rt, float s) {
+  const int op = OP >= 0 ? OP : op_rt;
   constexpr int V = 16 / sizeof(T);
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -78,16 +81,24 @@ __global__ void unary_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int
     y[i] = Cvt<T>::from_f(unary_f(op, Cvt<T>::to_f(x[i]), s));
 }
 
-template <typename T>
+// OP = U_RELU: the gradient needs only y (y > 0 exactly where x > 0), so x is not read — a third
+// less traffic than the generic form
+template <typename T, int OP = -1>
 __global__ void unary_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y, const T* __restrict__ dy,
-                                 T* __restrict__ dx, int64_t n, int op, float s, int accumulate) {
+                                 T* __restrict__ dx, int64_t n, int op_rt, float s, int accumulate) {
+  const int op = OP >= 0 ? OP : op_rt;
   constexpr int V = 16 / sizeof(T);
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     float xv[V], yv[V], g[V], o[V];
-    load16(x + i * V, xv);
     load16(y + i * V, yv);
+    if constexpr (OP == U_RELU) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) xv[j] = yv[j];
+    } else {
+      load16(x + i * V, xv);
+    }
     load16(dy + i * V, g);
     if (accumulate) load16(dx + i * V, o);
 #pragma unroll
@@ -98,7 +109,8 @@ __global__ void unary_bwd_kernel(const T* __restrict__ x, const T* __restrict__ 
     store16(dx + i * V, o);
   }
   for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float d = Cvt<T>::to_f(dy[i]) * unary_df(op, Cvt<T>::to_f(x[i]), Cvt<T>::to_f(y[i]), s);
+    const float yi = Cvt<T>::to_f(y[i]);
+    float d = Cvt<T>::to_f(dy[i]) * unary_df(op, OP == U_RELU ? yi : Cvt<T>::to_f(x[i]), yi, s);
     dx[i] = Cvt<T>::from_f(accumulate ? Cvt<T>::to_f(dx[i]) + d : d);
   }
 }
@@ -124,9 +136,10 @@ __device__ __forceinline__ float binary_act(int op, float a, float b) {
 }
 
 // Same-shape fast path.
-template <typename T>
+template <typename T, int OP = -1>  // OP >= 0: compile-time op (B_ADD: residual adds), -1: run time
 __global__ void binary_same_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ c,
-                                   int64_t n, int op) {
+                                   int64_t n, int op_rt) {
+  const int op = OP >= 0 ? OP : op_rt;
   constexpr int V = 16 / sizeof(T);
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -590,16 +603,22 @@ __global__ void bias_act_fwd_kernel(const bf16_t* __restrict__ z, const void* __
 void unary_fwd(int dt, const void* x, void* y, int64_t n, int op, float s, hipStream_t st) {
   if (n == 0) return;
   FFK_DT_DISPATCH(dt, {
-    hipLaunchKernelGGL(unary_fwd_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
-                       (const T*)x, (T*)y, n, op, s);
+    const dim3 grid(ew_grid(n / (16 / sizeof(T)) + 1, 256));
+    if (op == U_RELU) hipLaunchKernelGGL((unary_fwd_kernel<T, U_RELU>), grid, dim3(256), 0, st, (const T*)x, (T*)y, n, op, s);
+    else hipLaunchKernelGGL(unary_fwd_kernel<T>, grid, dim3(256), 0, st, (const T*)x, (T*)y, n, op, s);
   });
 }
 void unary_bwd(int dt, const void* x, const void* y, const void* dy, void* dx, int64_t n, int op, float s,
                int accumulate, hipStream_t st) {
   if (n == 0) return;
   FFK_DT_DISPATCH(dt, {
-    hipLaunchKernelGGL(unary_bwd_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
-                       (const T*)x, (const T*)y, (const T*)dy, (T*)dx, n, op, s, accumulate);
+    const dim3 grid(ew_grid(n / (16 / sizeof(T)) + 1, 256));
+    if (op == U_RELU)
+      hipLaunchKernelGGL((unary_bwd_kernel<T, U_RELU>), grid, dim3(256), 0, st, (const T*)x, (const T*)y,
+                         (const T*)dy, (T*)dx, n, op, s, accumulate);
+    else
+      hipLaunchKernelGGL(unary_bwd_kernel<T>, grid, dim3(256), 0, st, (const T*)x, (const T*)y, (const T*)dy,
+                         (T*)dx, n, op, s, accumulate);
   });
 }
 void binary_fwd(int dt, const void* a, const void* b, void* c, int64_t n, int op, int ndim,
@@ -609,9 +628,16 @@ void binary_fwd(int dt, const void* a, const void* b, void* c, int64_t n, int op
   d.ndim = ndim;
   for (int i = 0; i < ndim; ++i) { d.shape[i] = shape[i]; d.sa[i] = sa[i]; d.sb[i] = sb[i]; }
   FFK_DT_DISPATCH(dt, {
-    if (same && ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && ((uintptr_t)c % 16 == 0))
-      hipLaunchKernelGGL(binary_same_kernel<T>, dim3(ew_grid(n / (16 / sizeof(T)) + 1, 256)), dim3(256), 0, st,
-                         (const T*)a, (const T*)b, (T*)c, n, op);
+    if (same && ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && ((uintptr_t)c % 16 == 0)) {
+      const dim3 grid(ew_grid(n / (16 / sizeof(T)) + 1, 256));
+      if (op == B_ADD)
+        hipLaunchKernelGGL((binary_same_kernel<T, B_ADD>), grid, dim3(256), 0, st, (const T*)a, (const T*)b, (T*)c, n, op);
+      else if (op == (B_ADD | B_RELU))
+        hipLaunchKernelGGL((binary_same_kernel<T, B_ADD | B_RELU>), grid, dim3(256), 0, st, (const T*)a, (const T*)b,
+                           (T*)c, n, op);
+      else
+        hipLaunchKernelGGL(binary_same_kernel<T>, grid, dim3(256), 0, st, (const T*)a, (const T*)b, (T*)c, n, op);
+    }
     else {
       if (same) { d.ndim = 1; d.shape[0] = n; d.sa[0] = 1; d.sb[0] = 1; }
       hipLaunchKernelGGL(binary_bcast_kernel<T>, dim3(ew_grid(n, 256)), dim3(256), 0, st, (const T*)a,
