@@ -865,6 +865,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("col_reduce_set_gy", [](int64_t g) { ffk::col_reduce_set_gy((int)g); });
   m.def("col_reduce_gy", []() { return ffk::col_reduce_gy(); });
+  m.def("fold_record", [](bool on) { ffk::fold_record(on); });
+  m.def("fold_pending", []() { return ffk::fold_pending(); });
+  m.def("fold_flush", []() { ffk::fold_flush(cur_stream()); });
   m.def("layernorm_bwd_ws", &layernorm_bwd_ws);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("layernorm_fwd", &layernorm_fwd);

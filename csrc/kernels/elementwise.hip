@@ -5,6 +5,8 @@
 #include "common.h"
 #include "ops.h"
 
+#include <vector>
+
 namespace ffk {
 
 __device__ __forceinline__ float unary_f(int op, float x, float s) {
@@ -460,6 +462,77 @@ int col_reduce_gy() {
 }
 void col_reduce_set_gy(int g) { g_cr_gy = std::max(0, g); }
 
+// Batched deterministic folds: up to FOLD_MAX (slab, output) pairs in one launch, each pair's
+// column blocks a contiguous range of blockIdx.x; the per-pair arithmetic is col_reduce_det_kernel's
+// (same order: bitwise equal results). Lets the ~76 parameter-gradient folds of a BERT-Large backward
+// (LayerNorm gamma / beta, biases; 5-8 us each, latency-bound at 32-96 workgroups) run a few per
+// launch, queued until a gradient bucket needs them (fold_record / fold_flush).
+constexpr int FOLD_MAX = 24;
+struct FoldRow { const float* part; float* out; int R, C, first, pad; };
+struct FoldBatch { FoldRow r[FOLD_MAX]; int n; };
+__global__ void __launch_bounds__(1024) col_reduce_batch_kernel(FoldBatch b) {
+  constexpr int CW = 32, RL = 32, U = 8;
+  __shared__ float red[RL][CW + 1];
+  int i = 0;
+  while (i + 1 < b.n && b.r[i + 1].first <= (int)blockIdx.x) ++i;  // uniform: scalar loop over <= 24 rows
+  const float* p = b.r[i].part;
+  float* out = b.r[i].out;
+  const int R = b.r[i].R, C = b.r[i].C;
+  const int c = ((int)blockIdx.x - b.r[i].first) * CW + (threadIdx.x % CW);
+  const int rl = threadIdx.x / CW;
+  float acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.f;
+  if (c < C) {
+    int r = rl;
+    for (; r + (U - 1) * RL < R; r += U * RL) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(r + u * RL) * C + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += v[u];
+    }
+    for (; r < R; r += RL) acc[0] += p[(int64_t)r * C + c];
+  }
+  float t0 = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) t0 += acc[u];
+  red[rl][threadIdx.x % CW] = t0;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < RL; ++k) t += red[k][threadIdx.x];
+    out[c] += t;
+  }
+}
+
+// fold recorder: while on, col_reduce_add3's deterministic folds are queued instead of launched;
+// fold_flush launches the queue. A second fold into an output already queued flushes first (two
+// read-modify-writes of one output must not share a launch). Host-side state: one queue per
+// process, used from the thread that runs the backward.
+static bool g_fold_rec = false;
+static std::vector<FoldRow> g_fold_q;
+static hipStream_t g_fold_st = nullptr;
+void fold_record(bool on) { g_fold_rec = on; }
+int fold_pending() { return (int)g_fold_q.size(); }
+void fold_flush(hipStream_t st) {
+  size_t i = 0;
+  while (i < g_fold_q.size()) {
+    FoldBatch b;
+    b.n = 0;
+    int blocks = 0;
+    for (; i < g_fold_q.size() && b.n < FOLD_MAX; ++i) {
+      b.r[b.n] = g_fold_q[i];
+      b.r[b.n].first = blocks;
+      blocks += (g_fold_q[i].C + 31) / 32;
+      ++b.n;
+    }
+    hipLaunchKernelGGL(col_reduce_batch_kernel, dim3(blocks), dim3(1024), 0, st, b);
+  }
+  g_fold_q.clear();
+}
+
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st) {
   if (R == 0 || C == 0) return;
   Outs3 o{{out0, out1, out2}, {0, 0, 0}};
@@ -467,6 +540,20 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
   for (int k = 0; k < 3; ++k)
     if (o.p[k]) o.which[nz++] = k;
   if (!nz) return;
+  if (g_fold_rec && col_reduce_gy() == 0) {
+    if (!g_fold_q.empty() && st != g_fold_st) fold_flush(g_fold_st);
+    g_fold_st = st;
+    for (int z = 0; z < nz; ++z) {
+      const int k = o.which[z];
+      for (const FoldRow& q : g_fold_q)
+        if (q.out == o.p[k]) {
+          fold_flush(st);
+          break;
+        }
+      g_fold_q.push_back(FoldRow{part + (int64_t)k * R * C, o.p[k], R, C, 0, 0});
+    }
+    return;
+  }
   if (col_reduce_gy() == 0) {
     hipLaunchKernelGGL(col_reduce_det_kernel, dim3((C + 31) / 32, nz), dim3(1024), 0, st, part, o, R, C);
     return;

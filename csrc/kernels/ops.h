@@ -44,6 +44,10 @@ void col_reduce_add2(const float* part, float* out0, float* out1, int R, int C, 
 int col_reduce_gy();
 void col_reduce_set_gy(int g);
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st);
+// queue (record on) / launch (flush) the deterministic column folds, see elementwise.hip
+void fold_record(bool on);
+int fold_pending();
+void fold_flush(hipStream_t st);
 
 // transfer.hip: one launch over a list of boxes (pack / unpack / local re-layout of activation
 // shards); desc: device int64 [nbox][box_words()] (see transfer.hip), units of vec_bytes (copy)

@@ -516,10 +516,12 @@ def gemm(A, B, C, M, N, K, a_k, b_k, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=No
                         cands["lib_bias_act"] = lambda: _lib_gemm_bias_act(A, B, scratch, zs, M, N, K, a_k, b_k, lda,
                                                                            ldb, bias, act)
                 red, _RED["stream"] = _RED["stream"], None  # time every candidate with its folds inline
+                fq, _FOLDQ["on"] = _FOLDQ["on"], False
                 try:
                     times = _time_all(cands)
                 finally:
                     _RED["stream"] = red
+                    _FOLDQ["on"] = fq
                 if _LT and C.dtype in (torch.bfloat16, torch.float32):
                     _lt_candidates(A, B, C, scratch, M, N, K, a_k, b_k, lda, ldb, ldc, alpha, beta, bias, Z, act,
                                    batch, sA, sB, sC, plain, times)
@@ -614,7 +616,11 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
 
     def unfused(out=C, dbo=db):
         gemm(A, B, out, M, N, K, a_k, b_k, lda, ldb, ldc)
-        X.bias_act_bwd(out, Zp, out, dbo, M, N, act)
+        if dbo is not None and _FOLDQ["on"] and _RED["stream"] is None:  # bias fold batched like the others
+            ws = torch.empty(int(X.bias_act_bwd_ws(M, N)), device=out.device, dtype=torch.float32)
+            _staged_fold(lambda st: X.bias_act_bwd(out, Zp, out, dbo, M, N, act, ws, st), (ws, dbo))
+        else:
+            X.bias_act_bwd(out, Zp, out, dbo, M, N, act)
 
     key = ("dact", M, N, K, a_k, b_k, lda, ldb, ldc, act, db is not None)
     choice = _tuned.get(key)
@@ -637,9 +643,13 @@ def gemm_dact(A, B, C, Zp, db, M, N, K, a_k, b_k, lda, ldb, ldc, act):
             if not cands:
                 choice = "unfused"
             else:
-                unfused(scratch, dbs)  # tune the plain GEMM's call site outside the timing
-                cands["unfused"] = lambda: unfused(scratch, dbs)
-                times = _time_all(cands)
+                fq, _FOLDQ["on"] = _FOLDQ["on"], False  # candidates timed with their folds inline
+                try:
+                    unfused(scratch, dbs)  # tune the plain GEMM's call site outside the timing
+                    cands["unfused"] = lambda: unfused(scratch, dbs)
+                    times = _time_all(cands)
+                finally:
+                    _FOLDQ["on"] = fq
                 choice = min(times, key=lambda k: times[k])
                 TUNE_LOG.append({"op": "gemm_dact", "M": M, "N": N, "K": K, "a_k": a_k, "b_k": b_k, "act": act,
                                  "times_ms": {k: round(v, 4) for k, v in times.items()}, "choice": choice})
@@ -832,6 +842,38 @@ def reductions_deferred() -> int:
     return _RED["deferred"]
 
 
+# Batched parameter-gradient folds. With batching on (the executor turns it on for a training
+# backward, FF_FOLD_BATCH=1 default), a bias / LayerNorm backward runs its row pass inline and its
+# deterministic column folds are queued (native fold recorder) instead of launched; fold_flush()
+# launches the queue as a few col_reduce_batch_kernel launches (up to 24 slab / output pairs each),
+# right before a gradient bucket is reduced or updated and at the end of the backward. Same
+# arithmetic, same order: bitwise equal gradients; the slab workspaces stay referenced until then.
+_FOLDQ = {"on": False, "keep": []}
+
+
+def set_fold_batching(on: bool):
+    _FOLDQ["on"] = bool(on)
+
+
+def fold_flush():
+    if _FOLDQ["keep"]:
+        ext().fold_flush()
+        _FOLDQ["keep"] = []
+
+
+def _staged_fold(run, keep):
+    """run(stage): stage 1 (row pass) inline, stage 2's folds queued; keep: the slab workspace and
+    the fold outputs, referenced until the queue is launched."""
+    X = ext()
+    run(1)
+    X.fold_record(True)
+    try:
+        run(2)
+    finally:
+        X.fold_record(False)
+    _FOLDQ["keep"].append(keep)
+
+
 def _fold(main, fold, keep=()):
     """main() on the current stream, then fold() inline or on the reduction stream."""
     main()
@@ -860,6 +902,10 @@ def _bias_act_bwd_dev(dy2d, z, dz, db, act):
     X = ext()
     rows, cols = dy2d.shape
     if db is None or _RED["stream"] is None:
+        if db is not None and _FOLDQ["on"]:
+            ws = torch.empty(int(X.bias_act_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)
+            _staged_fold(lambda st: X.bias_act_bwd(dy2d, z, dz, db, rows, cols, act, ws, st), (ws, db))
+            return
         X.bias_act_bwd(dy2d, z, dz, db, rows, cols, act)
         return
     ws = torch.empty(int(X.bias_act_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)
@@ -964,6 +1010,12 @@ def layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dgamma, dbeta, dres=None, dsum=
         X = ext()
         dx = torch.empty_like(dy2d)
         if _RED["stream"] is None or (dgamma is None and dbeta is None and dsum is None):
+            if _FOLDQ["on"] and not (dgamma is None and dbeta is None and dsum is None):
+                ws = torch.empty(int(X.layernorm_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)
+                _staged_fold(lambda st: X.layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta,
+                                                        rows, cols, False, dsum, ws, st),
+                             (ws, dgamma, dbeta, dsum))
+                return dx
             X.layernorm_bwd(dy2d, xs2d, gamma, mean, rstd, dx, dres, dgamma, dbeta, rows, cols, False, dsum)
             return dx
         ws = torch.empty(int(X.layernorm_bwd_ws(rows, cols)), device=dy2d.device, dtype=torch.float32)

@@ -721,6 +721,9 @@ class GradBucketer:
         self.param_buckets = {}  # sharded arenas: a parameter may straddle bucket boundaries
         self.handles = []
         self.on_ready = None  # callback(bucket, async handle or None) once a bucket's grads are final
+        # callback() right before a completed bucket is reduced / handed to on_ready: the executor
+        # launches the parameter-gradient folds it queued (kernels.fold_flush), which finish those grads
+        self.before_launch = None
 
     def add_sharded_arena(self, group_ranks, flat, segments, rank):
         """ZeRO-1 arena (flexflow_amd/runtime/executor.py 'sharded optimizer'): buckets are fixed
@@ -779,6 +782,8 @@ class GradBucketer:
         for b in bs:
             b["ready"].add(key)
             if len(b["ready"]) == len(b["params"]):
+                if self.before_launch is not None:
+                    self.before_launch()
                 h = self._launch(b)
                 if self.on_ready is not None:
                     self.on_ready(b, h)
@@ -806,6 +811,8 @@ class GradBucketer:
         return h
 
     def flush(self):
+        if self.before_launch is not None:
+            self.before_launch()
         for _, _, buckets in self.arenas:
             for b in buckets:
                 if len(b["ready"]) != len(b["params"]):

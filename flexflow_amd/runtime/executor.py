@@ -678,9 +678,21 @@ class Executor:
                 self._upd_stream = self._make_upd_stream()
             K.set_reduce_stream(self._upd_stream)
             self._folds_pending = True
+        # batched folds (kernels.fold_flush): the bias / LayerNorm gradient folds of the backward
+        # queue up and launch a few per kernel, before each gradient bucket is reduced or updated
+        # and at the end; not under per-op timing hooks (they would book the folds elsewhere)
+        batch = (not defer and self.training and self.device.type == "cuda" and not self.hooks
+                 and os.environ.get("FF_FOLD_BATCH", "1") != "0")
+        if batch:
+            K.set_fold_batching(True)
+            self.bucketer.before_launch = K.fold_flush
         try:
             return self._backward(overlap_update)
         finally:
+            if batch:
+                K.fold_flush()
+                K.set_fold_batching(False)
+                self.bucketer.before_launch = None
             K.set_reduce_stream(None)
 
     def _join_folds(self):
