@@ -620,7 +620,9 @@ void channel_sum(int dt, const void* dy, const void* y, void* dz, float* db, flo
     const ColGeom q = nhwc_geom((int64_t)N * HW, C);
     hipLaunchKernelGGL(nhwc_colred_kernel<CR_SUM>, dim3((q.C8 + 31) / 32, q.S), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)y, (bf16_t*)dz, nullptr, nullptr, nullptr, nullptr, ws, q, 0);
-    if (db)
+    // the [S][C] partials' fold into the bias gradient: queued with the other parameter-gradient
+    // folds while the backward records them (fold_queue, elementwise.hip), else the finalize pass
+    if (db && !fold_queue(ws, db, q.S, C, st))
       hipLaunchKernelGGL(nhwc_finalize_kernel<CR_SUM>, dim3((C + 7) / 8), dim3(256), 0, st, ws, C, q.S, 0.f, 0.f, nullptr,
                          nullptr, nullptr, nullptr, nullptr, db);
     return;

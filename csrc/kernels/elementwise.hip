@@ -533,6 +533,22 @@ void fold_flush(hipStream_t st) {
   g_fold_q.clear();
 }
 
+static void fold_push(const float* part, float* out, int R, int C, hipStream_t st) {
+  if (!g_fold_q.empty() && st != g_fold_st) fold_flush(g_fold_st);
+  g_fold_st = st;
+  for (const FoldRow& q : g_fold_q)
+    if (q.out == out) {
+      fold_flush(st);
+      break;
+    }
+  g_fold_q.push_back(FoldRow{part, out, R, C, 0, 0});
+}
+bool fold_queue(const float* part, float* out, int R, int C, hipStream_t st) {
+  if (!g_fold_rec || col_reduce_gy() != 0 || R <= 0 || C <= 0) return false;
+  fold_push(part, out, R, C, st);
+  return true;
+}
+
 void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, int R, int C, hipStream_t st) {
   if (R == 0 || C == 0) return;
   Outs3 o{{out0, out1, out2}, {0, 0, 0}};
@@ -541,17 +557,7 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
     if (o.p[k]) o.which[nz++] = k;
   if (!nz) return;
   if (g_fold_rec && col_reduce_gy() == 0) {
-    if (!g_fold_q.empty() && st != g_fold_st) fold_flush(g_fold_st);
-    g_fold_st = st;
-    for (int z = 0; z < nz; ++z) {
-      const int k = o.which[z];
-      for (const FoldRow& q : g_fold_q)
-        if (q.out == o.p[k]) {
-          fold_flush(st);
-          break;
-        }
-      g_fold_q.push_back(FoldRow{part + (int64_t)k * R * C, o.p[k], R, C, 0, 0});
-    }
+    for (int z = 0; z < nz; ++z) fold_push(part + (int64_t)o.which[z] * R * C, o.p[o.which[z]], R, C, st);
     return;
   }
   if (col_reduce_gy() == 0) {

@@ -48,6 +48,8 @@ void col_reduce_add3(const float* part, float* out0, float* out1, float* out2, i
 void fold_record(bool on);
 int fold_pending();
 void fold_flush(hipStream_t st);
+// out[c] += sum_r part[r][c] queued when recording (true), else nothing done (false)
+bool fold_queue(const float* part, float* out, int R, int C, hipStream_t st);
 
 // transfer.hip: one launch over a list of boxes (pack / unpack / local re-layout of activation
 // shards); desc: device int64 [nbox][box_words()] (see transfer.hip), units of vec_bytes (copy)

@@ -1873,6 +1873,15 @@ def conv_bias_relu_bwd(dy, y, db):
         dy = cl_dense(dy, nhwc)
         dz = torch.empty_like(dy) if y is not None else None
         ws = torch.empty(ext().bn_ws(N, C, HW), device=dy.device, dtype=torch.float32)
+        if db is not None and nhwc and _FOLDQ["on"]:  # the bias fold joins the batched folds
+            X = ext()
+            X.fold_record(True)
+            try:
+                X.channel_sum(dy, cl_dense(y, nhwc) if y is not None else None, dz, db, ws, N, C, HW, nhwc)
+            finally:
+                X.fold_record(False)
+            _FOLDQ["keep"].append((ws, db))
+            return dz if dz is not None else dy
         ext().channel_sum(dy, cl_dense(y, nhwc) if y is not None else None, dz, db, ws, N, C, HW, nhwc)
         return dz if dz is not None else dy
     dz = dy * (y > 0) if y is not None else dy

@@ -449,3 +449,50 @@ def test_batched_gradient_folds_match_inline_folds(monkeypatch):
         torch.cuda.synchronize()
         losses.append(np.array(ls))
     assert np.allclose(losses[0], losses[1], rtol=1e-3), losses
+
+
+def test_batched_conv_bias_folds_match_inline(monkeypatch):
+    """The channel-last conv bias-gradient fold (the [S][C] partials of nhwc_colred) joins the
+    batched folds (fold_queue) instead of its finalize launch. A pool-free conv net (every reduction
+    in its backward fixed-order): after an autotuning pass, two backward passes with batching on and
+    off give bitwise-equal weight gradients and bias gradients equal up to fp32 summation order."""
+    from flexflow_amd.core import (ActiMode, DataType, FFConfig, FFModel, LossType, MetricsType,
+                                   SGDOptimizer)
+    from flexflow_amd import kernels as Kn
+    torch.manual_seed(0)
+    cfg = FFConfig(["--dtype", "bf16", "--no-hip-graphs"])
+    B = 8
+    cfg.batch_size = B
+    ff = FFModel(cfg)
+    x = ff.create_tensor([B, 64, 32, 32], DataType.DT_FLOAT, name="x")
+    t = ff.conv2d(x, 64, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = ff.conv2d(t, 128, 3, 3, 2, 2, 1, 1, ActiMode.AC_MODE_RELU, name="c2")
+    t = ff.conv2d(t, 128, 1, 1, 1, 1, 0, 0, ActiMode.AC_MODE_RELU, name="c3")
+    t = ff.flat(t, name="fl")
+    t = ff.dense(t, 10, ActiMode.AC_MODE_NONE, name="fc")
+    ff.softmax(t, name="sm")
+    ff.optimizer = SGDOptimizer(ff, 0.0)
+    ff.compile(loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+    rng = np.random.default_rng(1)
+    x.set_tensor(ff, rng.standard_normal((B, 64, 32, 32)).astype(np.float32))
+    ff.label_tensor.set_tensor(ff, rng.integers(0, 10, (B, 1), dtype=np.int32))
+    grads = []
+    for on in ("0", "1", "0"):  # the first pass autotunes the kernels (its outputs come from trials)
+        monkeypatch.setenv("FF_FOLD_BATCH", on)
+        ff.forward()
+        ff.zero_gradients()
+        ff.backward()
+        torch.cuda.synchronize()
+        assert Kn._FOLDQ["keep"] == []
+        grads.append({(L.name, i): ff.executor.get_weight_grad(w).detach().float().clone()
+                      for L in ff.layers for i, w in enumerate(L.weights)})
+    assert torch.equal(grads[0][("c1", 0)], grads[2][("c1", 0)])  # the backward is deterministic
+    nb = 0
+    for k, g in grads[1].items():
+        ref = grads[2][k]
+        if g.dim() == 1:
+            nb += 1
+            assert torch.allclose(g, ref, rtol=1e-5, atol=1e-6 * max(1e-3, ref.abs().max().item())), k
+        else:
+            assert torch.equal(g, ref), k
+    assert nb >= 3
